@@ -1,0 +1,182 @@
+"""Benchmark: train frames/s of the 228M NeuroSync Seq2Seq on MI355X (BASELINE.json metric).
+
+One step = one reference training step (utils/training_utils.py:56-80) on one
+batch of B=128 windows x T=128 frames per GPU: zero_grad -> forward -> fused
+Loss -> backward (+ RCCL gradient all-reduce when n>1) -> clip(2.0) + Adam.
+bf16 compute, dropout 0.3 on, synthetic seeded inputs of the reference shapes
+(features [B,T,256] f32, targets [B,T,61] f32, already resident in HBM).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Prints ONE JSON line on rank 0.  `roofline` is measured live for the dominant
+kernel (nstl GEMM: ~97% of the step's FLOPs): HIP events around every GEMM launch
+in the timed region on the stream it runs on; achieved = algorithmic GEMM FLOPs /
+GEMM time.  `cpu_baseline` times the fp32 CPU oracle step (the reference step
+restated in torch-CPU) on a bounded sample on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+BF16_DENSE_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def frames_flops(W, T, D, n_attn=24):
+    """Algorithmic train FLOPs per frame: 6W + 12*T*D*24."""
+    return 6 * W + 12 * T * D * n_attn
+
+
+def cpu_baseline(cfg, T, budget_s=25.0):
+    """fp32 oracle step (reference semantics) on the host cores, bounded sample."""
+    from oracle import model_ref
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    B = 2
+    params = model_ref.seeded_params(model_ref.param_shapes(cfg["input_dim"], cfg["hidden_dim"], cfg["n_layers"],
+                                                            cfg["output_dim"]), 0)
+    tr = model_ref.OracleTrainer(params, cfg["num_heads"], dropout=cfg["dropout"])
+    g = torch.Generator().manual_seed(0)
+    src = torch.randn(B, T, cfg["input_dim"], generator=g)
+    trg = torch.randn(B, T, cfg["output_dim"], generator=g) * 20
+    tr.step(src, trg)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while n < 2 or (time.perf_counter() - t0 < budget_s * 0.5 and n < 5):
+        tr.step(src, trg)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * B * T / dt, 2), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": "228M fp32 oracle step (fwd+loss+bwd+clip+Adam, dropout 0.3), B=%d x T=%d frames, %d timed steps"
+                      % (B, T, n)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from neurosync_trainer_lite_amd import _hip as K
+    from neurosync_trainer_lite_amd import parallel
+    from neurosync_trainer_lite_amd.config import training_config
+    from neurosync_trainer_lite_amd.utils.model_utils import build_model, prepare_training_components
+
+    rank, world, local = parallel.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = dict(training_config)
+    B, T = args.batch, args.seq
+    cfg.update(micro_batch_size=T, frame_size=T, batch_size=B)
+    torch.manual_seed(1234)  # identical init on every rank
+    model = build_model(cfg, dev)
+    model.train()
+    crit, opt, sched = prepare_training_components(cfg, model)
+    eng = model.engine()
+    if world > 1:
+        eng.grad_reducer = parallel.GradAllReducer(eng.g32)
+        eng.grad_scale_t = torch.full((1,), 1.0 / world, device=dev)
+    W = sum(p.numel() for n, p in model.named_parameters() if n.endswith("weight") and p.dim() == 2)
+
+    g = torch.Generator(device=dev).manual_seed(100 + rank)
+    src = torch.randn(B, T, cfg["input_dim"], device=dev, generator=g)
+    trg = torch.randn(B, T, cfg["output_dim"], device=dev, generator=g) * 20
+
+    def step():
+        opt.zero_grad()
+        loss = crit(model(src), trg)
+        loss.backward()
+        opt.step(max_norm=2.0)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # live per-launch timing of the dominant kernel (GEMM) inside the timed region
+    gemm_events = []
+    real_gemm = K.gemm
+
+    def timed_gemm(A, B_, C, M, N, Kd, **kw):
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        real_gemm(A, B_, C, M, N, Kd, **kw)
+        e1.record(st)
+        gemm_events.append((e0, e1, 2.0 * M * N * Kd))
+
+    K.gemm = timed_gemm
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    K.gemm = real_gemm
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = tt.item()
+    loss_v = loss.item()
+    if not (loss_v == loss_v):
+        raise RuntimeError("non-finite loss %r" % loss_v)
+
+    gemm_ms = sum(a.elapsed_time(b) for a, b, _ in gemm_events)
+    gemm_flops = sum(f for _, _, f in gemm_events)
+    n_launch = len(gemm_events)
+    achieved_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+    ms_step = elapsed / args.steps * 1e3
+    frames = B * T * world * args.steps
+    value = frames / elapsed
+    step_tf = frames_flops(W, T, cfg["hidden_dim"]) * B * T * world / (elapsed / args.steps) / 1e12 / world
+
+    if rank == 0:
+        out = {
+            "metric": "train frames/sec (audio->blendshape) 228M cfg",
+            "value": round(value, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (seeded features [B,T,256] + targets [B,T,61], resident in HBM)",
+            "config": {"workload": "228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam)",
+                       "model": "NeuroSync Seq2Seq 228M", "global_batch": B * world, "seq_len": T,
+                       "frames_per_step": B * T * world, "parallelism": "dp%d" % world},
+            "roofline": {"bound": "mfma", "kernel": "nstl gemm_kernel (all launches in timed region)",
+                         "achieved": round(achieved_tf, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": None,
+                         "launches": n_launch, "avg_launch_us": round(gemm_ms * 1e3 / max(1, n_launch), 2),
+                         "gemm_share_of_step": round(gemm_ms / (elapsed * 1e3), 3)},
+            "step_tflops_per_gpu": round(step_tf, 1),
+            "step_mfma_frac": round(step_tf / BF16_DENSE_PEAK_TFLOPS, 4),
+            "final_loss": round(loss_v, 4),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg, T)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,182 @@
+/*
+ * nstl.h — C ABI of libnstl_hip.so, the MI355X (gfx950) kernels behind the
+ * NeuroSync Trainer Lite training hot path.
+ *
+ * The reference (wolfi/NeuroSync_Trainer_Lite) has no native code and no FFI:
+ * its hot path is PyTorch eager.  Each entry point below replaces the PyTorch
+ * op(s) the reference dispatches to at the cited file:line; the Python host
+ * layer (neurosync_trainer_lite_amd/, loaded with ctypes) keeps the reference's
+ * module/function surface on top of it.
+ *
+ * Conventions
+ *   - plain pointers + sizes; every buffer is caller-owned (device memory);
+ *     no allocation inside any call; scratch comes in via *workspace.
+ *   - `stream` is a hipStream_t passed as void*; every launch goes on it.
+ *   - return 0 on success, a hipError_t value otherwise (1 = invalid value);
+ *     nstl_last_error_string() describes the last failure on this thread.
+ *   - dtype codes: NSTL_F32 = 0, NSTL_BF16 = 1.  Row-major everywhere.
+ */
+#ifndef NSTL_H
+#define NSTL_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { NSTL_F32 = 0, NSTL_BF16 = 1 };
+
+enum {
+  NSTL_EPI_NONE = 0,           /* C = alpha*acc + beta*C                        */
+  NSTL_EPI_BIAS = 1,           /* + bias[j]                                     */
+  NSTL_EPI_BIAS_RELU_DROP = 2, /* dropout(relu(acc + bias))                     */
+  NSTL_EPI_BIAS_ROPE = 3,      /* rotate pairs of (acc + bias), cols < rope_cols */
+  NSTL_EPI_DRELU_DROP = 4      /* acc * (aux[i,j] > 0) / (1-p)  (backward)       */
+};
+
+/* C[i,j] = alpha * sum_r A(i,r) B(j,r)  (+ beta*C, + epilogue).
+ *   a_kmajor: A stored [M][K] (r contiguous) else [K][M];
+ *   b_kmajor: B stored [N][K] else [K][N].
+ * Replaces nn.Linear forward/backward GEMMs: utils/model.py:113-115,138
+ * (MultiHeadAttention q/k/v/out_linear), :154,:157 (FeedForwardNetwork),
+ * :216/:224 (Encoder.embedding), :242/:251 (Decoder.fc_output); the bias+ReLU+
+ * dropout epilogue replaces F.relu + nn.Dropout at :155-156, the RoPE epilogue
+ * replaces apply_rope_qk (:60-83) and GlobalPositionalEncoding (:29-53). */
+typedef struct nstl_gemm_args {
+  int dtype;      /* element type of A and B */
+  int c_dtype;    /* element type of C */
+  int a_kmajor, b_kmajor;
+  const void* A; int64_t lda;
+  const void* B; int64_t ldb;
+  void* C; int64_t ldc;
+  int M, N, K;
+  float alpha, beta;
+  int epilogue;
+  const float* bias;                   /* [N] f32 */
+  const void* aux; int64_t ld_aux;     /* DRELU_DROP: saved post-dropout activation (dtype) */
+  float p_drop; uint64_t seed;         /* BIAS_RELU_DROP / DRELU_DROP */
+  const float* rope_cos; const float* rope_sin; /* [rope_T][rope_dim/2] f32 */
+  int rope_T, rope_dim, rope_cols;
+  int split_k;                         /* >1: f32 partials in workspace, then reduce */
+  void* workspace; int64_t workspace_bytes;
+} nstl_gemm_args;
+int nstl_gemm(const nstl_gemm_args* args, void* stream);
+int64_t nstl_gemm_workspace_bytes(int M, int N, int split_k);
+
+/* Non-causal multi-head attention with per-head RoPE already applied to q,k
+ * (by the projection epilogue), softmax scale 1/sqrt(dh), attention-probability
+ * dropout.  Replaces F.scaled_dot_product_attention at utils/model.py:126-127.
+ * Element (b,t,h,d) of X lives at X[(b*T + t)*X_ld + h*dh + d].
+ * Constraints: dh == 64; T % 16 == 0; T <= 256 (bf16) / 128 (f32). */
+typedef struct nstl_attn_args {
+  int dtype;
+  int B, T, H, dh;
+  const void* q; int64_t q_ld;
+  const void* k; int64_t k_ld;
+  const void* v; int64_t v_ld;
+  void* o; int64_t o_ld;
+  float* lse;                 /* [B*H*T] f32: log-sum-exp of scaled scores */
+  float p_drop; uint64_t seed;
+  const void* dout; int64_t dout_ld;   /* backward only */
+  void* dq; int64_t dq_ld;
+  void* dk; int64_t dk_ld;
+  void* dv; int64_t dv_ld;
+  const float* rope_cos; const float* rope_sin;  /* [T][dh/2]; non-null: dq,dk rotated back */
+  int rope_q, rope_k;
+} nstl_attn_args;
+int nstl_attn_fwd(const nstl_attn_args* args, void* stream);
+int nstl_attn_bwd(const nstl_attn_args* args, void* stream);
+
+/* Post-LN residual block tail: s = x + dropout(dropout(y)); out = LN(s).
+ * Replaces `src = src + self.dropoutN(src2); src = self.normN(src)` at
+ * utils/model.py:175-180, :198-207, the final LayerNorms :228-229, :249-250, and
+ * (rot_out) the decoder-input GlobalPositionalEncoding at :246. */
+typedef struct nstl_ln_args {
+  int dtype; int rows, D;
+  const void* x;           /* residual (dtype), may be NULL */
+  const void* y;           /* branch (dtype) */
+  int n_masks; float p_drop; uint64_t seed1, seed2;
+  const float* gamma; const float* beta; float eps;
+  void* s_out;             /* saved pre-norm sum (dtype) */
+  void* out;               /* LN output (dtype) */
+  float* mean; float* rstd;
+  void* rot_out; const float* rope_cos; const float* rope_sin; int rope_T;
+  /* backward */
+  const void* s_in;        /* saved pre-norm sum */
+  const float* dout;       /* f32 [rows][D] */
+  float* ds;               /* f32 [rows][D] (may alias dout) */
+  void* dbranch;           /* dtype: ds * masks / (1-p)^n_masks, may be NULL */
+  float* dgamma_part; float* dbeta_part; int n_part;   /* [n_part][D] */
+} nstl_ln_args;
+int nstl_ln_fwd(const nstl_ln_args* args, void* stream);
+int nstl_ln_bwd(const nstl_ln_args* args, void* stream);
+
+/* out[j] = beta*out[j] + sum_p part[p][j]  (f32) */
+int nstl_reduce_rows(const float* part, int n_part, int cols, float* out, float beta, void* stream);
+/* Column sums of X[rows][cols] (bias gradients): out[j] = beta*out[j] + sum_i X[i][j].
+ * partial: [ceil(rows/256)][cols] f32 scratch. */
+int nstl_colsum(int dtype, const void* x, int64_t ld, int rows, int cols, float* partial,
+                float* out, float beta, void* stream);
+
+/* Interleaved-pair rotation of rows (RoPE / global PE).  inverse: rotate by -theta.
+ * accumulate: out += result (out must be f32). Position t = row % T. */
+int nstl_rope(int in_dtype, const void* in, int64_t in_ld, int out_dtype, void* out, int64_t out_ld,
+              int rows, int cols, const float* cos_t, const float* sin_t, int T, int rope_dim,
+              int inverse, int accumulate, void* stream);
+
+/* Fused Loss forward + backward.  Replaces Loss.forward (utils/model.py:278-291)
+ * and its autograd backward.  loss_out[0..3] = total, rec, temp, dir. */
+typedef struct nstl_loss_args {
+  int B, T, F;
+  const float* pred; int64_t pred_ld;
+  const float* trg; int64_t trg_ld;
+  float delta, w1, w2, w3;
+  float grad_scale;
+  void* dpred; int dpred_dtype; int64_t dpred_ld;   /* columns F..dpred_ld-1 zeroed */
+  float* partial;          /* [B][4] scratch */
+  float* loss_out;         /* [4] */
+} nstl_loss_args;
+int nstl_loss_fwd_bwd(const nstl_loss_args* args, void* stream);
+
+/* Global gradient L2 norm, stage 1: partial[i] = sum of squares of a slice.
+ * n_partial <= 1024. Replaces clip_grad_norm_'s norm (utils/training_utils.py:73). */
+int nstl_sumsq(const float* g, int64_t n, float* partial, int n_partial, void* stream);
+
+/* Clip + Adam(coupled L2) over one flat f32 arena: replaces
+ * torch.nn.utils.clip_grad_norm_(params, max_norm) + torch.optim.Adam.step
+ * (utils/training_utils.py:73-74, utils/model_utils.py:11). */
+typedef struct nstl_adam_args {
+  float* p; const float* g; float* m; float* v;
+  void* p_lowp; int lowp_dtype;        /* optional low-precision shadow copy of p */
+  int64_t n;
+  float lr, beta1, beta2, eps, weight_decay;
+  int step;                            /* post-increment step count (>= 1) */
+  const float* sumsq_partial; int n_partial;   /* NULL: no clipping */
+  float max_norm;
+  float* norm_out;                     /* [1] pre-clip total norm, may be NULL */
+} nstl_adam_args;
+int nstl_adam_step(const nstl_adam_args* args, void* stream);
+
+/* 2-D strided copy with conversion: dst[i][j] = scale * src[i][j] for j < cols,
+ * 0 for cols <= j < dst_cols (zero padding).  scale: device f32 scalar or NULL (1). */
+int nstl_copy2d(int src_dtype, const void* src, int64_t src_ld, int dst_dtype, void* dst, int64_t dst_ld,
+                int rows, int cols, int dst_cols, const float* scale, void* stream);
+
+/* dtype conversion (f32 <-> bf16), n elements. */
+int nstl_cast(int src_dtype, const void* src, int dst_dtype, void* dst, int64_t n, void* stream);
+
+/* Feature extraction (utils/audio/extraction/extract_features_utils.py:54-113):
+ * per 120 Hz frame of the reflect-padded clip: DC removal, symmetric Hann,
+ * autocorrelation lags 1..n_lags normalised by lag 0, edge-frame fix.
+ * y: f32 [n_samples]; out: f64 [n_frames][n_lags]. */
+int nstl_autocorr(const float* y, int64_t n_samples, int frame_length, int hop_length, int n_lags,
+                  double* out, int n_frames, void* stream);
+
+const char* nstl_last_error_string(void);
+int nstl_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,254 @@
+"""ctypes bindings to libnstl_hip.so (C ABI declared in include/nstl.h).
+
+The shared library is built in-tree (``python __graft_entry__.py`` / ``make -C
+neurosync_trainer_lite_amd/csrc``).  There is no fallback: if the library is
+missing or a call fails, a RuntimeError is raised.
+
+torch must be imported before the library is loaded, so that the HIP runtime
+torch already mapped (SONAME libamdhip64.so.7) is the one the library binds to.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load order: torch's HIP runtime first)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnstl_hip.so")
+
+F32, BF16 = 0, 1
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU_DROP, EPI_BIAS_ROPE, EPI_DRELU_DROP = 0, 1, 2, 3, 4
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_u64 = ctypes.c_uint64
+_fp = ctypes.POINTER(ctypes.c_float)
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i32), ("c_dtype", _i32), ("a_kmajor", _i32), ("b_kmajor", _i32),
+        ("A", _vp), ("lda", _i64), ("B", _vp), ("ldb", _i64), ("C", _vp), ("ldc", _i64),
+        ("M", _i32), ("N", _i32), ("K", _i32),
+        ("alpha", _f32), ("beta", _f32), ("epilogue", _i32),
+        ("bias", _vp), ("aux", _vp), ("ld_aux", _i64),
+        ("p_drop", _f32), ("seed", _u64),
+        ("rope_cos", _vp), ("rope_sin", _vp), ("rope_T", _i32), ("rope_dim", _i32), ("rope_cols", _i32),
+        ("split_k", _i32), ("workspace", _vp), ("workspace_bytes", _i64),
+    ]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i32), ("B", _i32), ("T", _i32), ("H", _i32), ("dh", _i32),
+        ("q", _vp), ("q_ld", _i64), ("k", _vp), ("k_ld", _i64), ("v", _vp), ("v_ld", _i64),
+        ("o", _vp), ("o_ld", _i64), ("lse", _vp),
+        ("p_drop", _f32), ("seed", _u64),
+        ("dout", _vp), ("dout_ld", _i64), ("dq", _vp), ("dq_ld", _i64), ("dk", _vp), ("dk_ld", _i64),
+        ("dv", _vp), ("dv_ld", _i64),
+        ("rope_cos", _vp), ("rope_sin", _vp), ("rope_q", _i32), ("rope_k", _i32),
+    ]
+
+
+class LnArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i32), ("rows", _i32), ("D", _i32),
+        ("x", _vp), ("y", _vp),
+        ("n_masks", _i32), ("p_drop", _f32), ("seed1", _u64), ("seed2", _u64),
+        ("gamma", _vp), ("beta", _vp), ("eps", _f32),
+        ("s_out", _vp), ("out", _vp), ("mean", _vp), ("rstd", _vp),
+        ("rot_out", _vp), ("rope_cos", _vp), ("rope_sin", _vp), ("rope_T", _i32),
+        ("s_in", _vp), ("dout", _vp), ("ds", _vp), ("dbranch", _vp),
+        ("dgamma_part", _vp), ("dbeta_part", _vp), ("n_part", _i32),
+    ]
+
+
+class LossArgs(ctypes.Structure):
+    _fields_ = [
+        ("B", _i32), ("T", _i32), ("F", _i32),
+        ("pred", _vp), ("pred_ld", _i64), ("trg", _vp), ("trg_ld", _i64),
+        ("delta", _f32), ("w1", _f32), ("w2", _f32), ("w3", _f32), ("grad_scale", _f32),
+        ("dpred", _vp), ("dpred_dtype", _i32), ("dpred_ld", _i64),
+        ("partial", _vp), ("loss_out", _vp),
+    ]
+
+
+class AdamArgs(ctypes.Structure):
+    _fields_ = [
+        ("p", _vp), ("g", _vp), ("m", _vp), ("v", _vp),
+        ("p_lowp", _vp), ("lowp_dtype", _i32), ("n", _i64),
+        ("lr", _f32), ("beta1", _f32), ("beta2", _f32), ("eps", _f32), ("weight_decay", _f32),
+        ("step", _i32), ("sumsq_partial", _vp), ("n_partial", _i32), ("max_norm", _f32), ("norm_out", _vp),
+    ]
+
+
+# every symbol include/nstl.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "nstl_gemm", "nstl_gemm_workspace_bytes", "nstl_attn_fwd", "nstl_attn_bwd", "nstl_ln_fwd", "nstl_ln_bwd",
+    "nstl_reduce_rows", "nstl_colsum", "nstl_rope", "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step",
+    "nstl_cast", "nstl_copy2d", "nstl_autocorr", "nstl_last_error_string", "nstl_version",
+]
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the library is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                "libnstl_hip.so not found at %s: build it with `python __graft_entry__.py` "
+                "(make -C neurosync_trainer_lite_amd/csrc). There is no CPU fallback." % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        P = ctypes.POINTER
+        L.nstl_gemm.argtypes = [P(GemmArgs), _vp]
+        L.nstl_gemm_workspace_bytes.argtypes = [_i32, _i32, _i32]
+        L.nstl_gemm_workspace_bytes.restype = _i64
+        L.nstl_attn_fwd.argtypes = [P(AttnArgs), _vp]
+        L.nstl_attn_bwd.argtypes = [P(AttnArgs), _vp]
+        L.nstl_ln_fwd.argtypes = [P(LnArgs), _vp]
+        L.nstl_ln_bwd.argtypes = [P(LnArgs), _vp]
+        L.nstl_reduce_rows.argtypes = [_vp, _i32, _i32, _vp, _f32, _vp]
+        L.nstl_colsum.argtypes = [_i32, _vp, _i64, _i32, _i32, _vp, _vp, _f32, _vp]
+        L.nstl_rope.argtypes = [_i32, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _vp]
+        L.nstl_loss_fwd_bwd.argtypes = [P(LossArgs), _vp]
+        L.nstl_sumsq.argtypes = [_vp, _i64, _vp, _i32, _vp]
+        L.nstl_adam_step.argtypes = [P(AdamArgs), _vp]
+        L.nstl_cast.argtypes = [_i32, _vp, _i32, _vp, _i64, _vp]
+        L.nstl_copy2d.argtypes = [_i32, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp]
+        L.nstl_autocorr.argtypes = [_vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp]
+        L.nstl_last_error_string.restype = ctypes.c_char_p
+        L.nstl_version.restype = _i32
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().nstl_last_error_string().decode(errors="replace")
+        raise RuntimeError("%s failed (code %d): %s" % (what, rc, msg))
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise TypeError("unsupported dtype %s (float32 / bfloat16)" % dt)
+
+
+# ---------------------------------------------------------------------------
+# thin call wrappers
+# ---------------------------------------------------------------------------
+def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None,
+         alpha=1.0, beta=0.0, epilogue=EPI_NONE, bias=None, aux=None, ld_aux=0, p_drop=0.0, seed=0,
+         rope=None, rope_cols=0, split_k=1, workspace=None, stream=None):
+    """C[i,j] = alpha sum_r A(i,r) B(j,r) (+beta C) + epilogue.  See include/nstl.h."""
+    a = GemmArgs()
+    a.dtype = dtype_code(A.dtype)
+    a.c_dtype = dtype_code(C.dtype)
+    a.a_kmajor, a.b_kmajor = int(a_kmajor), int(b_kmajor)
+    a.A, a.B, a.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
+    a.lda = lda if lda is not None else A.stride(-2) if A.dim() > 1 else K
+    a.ldb = ldb if ldb is not None else B.stride(-2) if B.dim() > 1 else K
+    a.ldc = ldc if ldc is not None else C.stride(-2)
+    a.M, a.N, a.K = M, N, K
+    a.alpha, a.beta = alpha, beta
+    a.epilogue = epilogue
+    a.bias = ptr(bias)
+    a.aux = ptr(aux)
+    a.ld_aux = ld_aux
+    a.p_drop = p_drop
+    a.seed = seed & 0xFFFFFFFFFFFFFFFF
+    if rope is not None:
+        cos_t, sin_t, rT, rdim = rope
+        a.rope_cos, a.rope_sin, a.rope_T, a.rope_dim = cos_t.data_ptr(), sin_t.data_ptr(), rT, rdim
+        a.rope_cols = rope_cols
+    a.split_k = split_k
+    if workspace is not None:
+        a.workspace = workspace.data_ptr()
+        a.workspace_bytes = workspace.numel() * workspace.element_size()
+    check(lib().nstl_gemm(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_gemm")
+
+
+def attn_args(dtype, B, T, H, q, q_ld, k, k_ld, v, v_ld, o, o_ld, lse, p_drop, seed):
+    a = AttnArgs()
+    a.dtype = dtype
+    a.B, a.T, a.H, a.dh = B, T, H, 64
+    a.q, a.q_ld, a.k, a.k_ld, a.v, a.v_ld = q, q_ld, k, k_ld, v, v_ld
+    a.o, a.o_ld, a.lse = o, o_ld, lse
+    a.p_drop, a.seed = p_drop, seed & 0xFFFFFFFFFFFFFFFF
+    return a
+
+
+def attn_fwd(a, stream=None):
+    check(lib().nstl_attn_fwd(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_attn_fwd")
+
+
+def attn_bwd(a, stream=None):
+    check(lib().nstl_attn_bwd(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_attn_bwd")
+
+
+def ln_fwd(a, stream=None):
+    check(lib().nstl_ln_fwd(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_ln_fwd")
+
+
+def ln_bwd(a, stream=None):
+    check(lib().nstl_ln_bwd(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_ln_bwd")
+
+
+def reduce_rows(part, n_part, cols, out, beta, stream=None):
+    check(lib().nstl_reduce_rows(part.data_ptr(), n_part, cols, out.data_ptr(), beta,
+                                 stream if stream is not None else stream_of()), "nstl_reduce_rows")
+
+
+def colsum(x, ld, rows, cols, partial, out, beta, stream=None):
+    check(lib().nstl_colsum(dtype_code(x.dtype), x.data_ptr(), ld, rows, cols, partial.data_ptr(), out.data_ptr(),
+                            beta, stream if stream is not None else stream_of()), "nstl_colsum")
+
+
+def rope(inp, in_ld, out, out_ld, rows, cols, cos_t, sin_t, T, rope_dim, inverse=False, accumulate=False,
+         stream=None):
+    check(lib().nstl_rope(dtype_code(inp.dtype), inp.data_ptr(), in_ld, dtype_code(out.dtype), out.data_ptr(), out_ld,
+                          rows, cols, cos_t.data_ptr(), sin_t.data_ptr(), T, rope_dim, int(inverse), int(accumulate),
+                          stream if stream is not None else stream_of()), "nstl_rope")
+
+
+def loss_fwd_bwd(a, stream=None):
+    check(lib().nstl_loss_fwd_bwd(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_loss_fwd_bwd")
+
+
+def sumsq(g, n, partial, n_partial, stream=None):
+    check(lib().nstl_sumsq(g.data_ptr(), n, partial.data_ptr(), n_partial,
+                           stream if stream is not None else stream_of()), "nstl_sumsq")
+
+
+def adam_step(a, stream=None):
+    check(lib().nstl_adam_step(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_adam_step")
+
+
+def cast(src, dst, n=None, stream=None):
+    n = src.numel() if n is None else n
+    check(lib().nstl_cast(dtype_code(src.dtype), src.data_ptr(), dtype_code(dst.dtype), dst.data_ptr(), n,
+                          stream if stream is not None else stream_of()), "nstl_cast")
+
+
+def copy2d(src, src_ld, dst, dst_ld, rows, cols, dst_cols, scale=None, stream=None):
+    check(lib().nstl_copy2d(dtype_code(src.dtype), src.data_ptr(), src_ld, dtype_code(dst.dtype), dst.data_ptr(),
+                            dst_ld, rows, cols, dst_cols, ptr(scale), stream if stream is not None else stream_of()),
+          "nstl_copy2d")
+
+
+def autocorr(y, frame_length, hop_length, n_lags, out, n_frames, stream=None):
+    check(lib().nstl_autocorr(y.data_ptr(), y.numel(), frame_length, hop_length, n_lags, out.data_ptr(), n_frames,
+                              stream if stream is not None else stream_of()), "nstl_autocorr")

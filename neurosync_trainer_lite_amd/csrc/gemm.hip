@@ -1,0 +1,318 @@
+// MFMA GEMM for gfx950: C[i,j] = alpha * sum_r A(i,r) B(j,r) (+beta*C) + epilogue.
+//
+// One kernel template covers the three products of nn.Linear training
+// (utils/model.py Linear layers):
+//   forward  Y  = X W^T   A=X [M][K] (K-major), B=W [N][K] (K-major)
+//   backward dX = dY W    A=dY [M][N] (K-major), B=W [N][K] read as [r][j] (MN-major)
+//   backward dW = dY^T X  A=dY [M][N] read as [r][i], B=X [M][K] read as [r][j]
+// K-major tiles are staged into 128-byte-row LDS images and read with
+// ds_read_b128; MN-major tiles keep the global layout in LDS and are read with
+// the gfx950 transpose read ds_read_b64_tr_b16 (bf16), so no transpose pass.
+//
+// Tile 128x128, BK = 128 bytes of reduction index (64 bf16 / 32 f32), 4 waves
+// (2x2) each owning 64x64 = 4x4 MFMA 16x16 tiles, register-staged double-
+// buffered LDS (one barrier per K tile), XCD-aware tile order.
+#include "../../include/nstl.h"
+#include "common.h"
+#include "status.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, NTHREADS = 256;
+constexpr int TILE_BYTES = 16384;
+
+struct GemmParams {
+  const char* A; int64_t lda;
+  const char* B; int64_t ldb;
+  char* C; int64_t ldc;
+  int M, N, K;
+  int c_f32;
+  float alpha, beta;
+  int epi;
+  const float* bias;
+  const char* aux; int64_t ld_aux; int aux_f32;
+  float inv_keep; uint32_t thresh; uint64_t seed;
+  const float* rope_cos; const float* rope_sin; int rope_T, rope_dim, rope_cols;
+  float* ws; int k_chunk;  // split-K: partial slabs [z][M][N]
+};
+
+template <typename T, bool KMAJ, int RB>
+struct Stager {
+  // 16 KB tile = 1024 chunks of 16 B, 4 per thread.
+  static constexpr int EPC = 16 / (int)sizeof(T);  // elements per chunk
+  uint4 reg[4];
+  int lds_off[4];
+
+  // rows_total: extent of the non-reduction dim (M or N); row0: tile origin in it.
+  NSTL_DEV void load(const char* base, int64_t ld, int row0, int rows_total, int k0, int K, int tid) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = s * NTHREADS + tid;
+      int gi, gk;
+      if (KMAJ) {
+        const int row = c >> 3, chunk = c & 7;
+        gi = row0 + row;
+        gk = k0 + chunk * EPC;
+        lds_off[s] = ImgK<128>::off(row, chunk * 16);
+      } else {
+        constexpr int CPR = RB / 16;
+        const int row = c / CPR, chunk = c % CPR;
+        gk = k0 + row;
+        gi = row0 + chunk * EPC;
+        lds_off[s] = ImgMN<RB>::off(row, chunk * 16);
+      }
+      const bool ok = gi < rows_total && gk < K;
+      const int64_t e = KMAJ ? ((int64_t)gi * ld + gk) : ((int64_t)gk * ld + gi);
+      if (ok)
+        reg[s] = *(const uint4*)(base + e * (int64_t)sizeof(T));
+      else
+        reg[s] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  NSTL_DEV void store(char* img) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) *(uint4*)(img + lds_off[s]) = reg[s];
+  }
+};
+
+template <typename T, bool AK, bool BKM>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmParams p) {
+  typedef typename FragT<T>::type Frag;
+  constexpr int BK = 128 / (int)sizeof(T);
+  constexpr int MN_RB = 128 * (int)sizeof(T);
+  constexpr int A_RB = AK ? 128 : MN_RB;
+  constexpr int B_RB = BKM ? 128 : MN_RB;
+  __shared__ __attribute__((aligned(16))) char smem[2][2][TILE_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nt_m = (p.M + BM - 1) / BM, nt_n = (p.N + BN - 1) / BN;
+  const int id = xcd_remap(blockIdx.x, nt_m * nt_n);
+  const int tm = id / nt_n, tn = id % nt_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kz0 = blockIdx.y * p.k_chunk;
+  const int kz1 = min(p.K, kz0 + p.k_chunk);
+  const int nk = (kz1 - kz0 + BK - 1) / BK;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  Stager<T, AK, A_RB> sa;
+  Stager<T, BKM, B_RB> sb;
+  if (nk > 0) {
+    sa.load(p.A, p.lda, m0, p.M, kz0, kz1, tid);
+    sb.load(p.B, p.ldb, n0, p.N, kz0, kz1, tid);
+    sa.store(smem[0][0]);
+    sb.store(smem[0][1]);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k1 = kz0 + (kt + 1) * BK;
+      sa.load(p.A, p.lda, m0, p.M, k1, kz1, tid);
+      sb.load(p.B, p.ldb, n0, p.N, k1, kz1, tid);
+    }
+    const char* Ai = smem[cur][0];
+    const char* Bi = smem[cur][1];
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      Frag fa[4], fb[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (AK)
+          frag_row<ImgK<128>>(fa[t], Ai, wm * 64 + t * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4));
+        else
+          frag_col<ImgMN<A_RB>>(fa[t], Ai, wm * 64 + t * 16, kk * 32, lane);
+        if (BKM)
+          frag_row<ImgK<128>>(fb[t], Bi, wn * 64 + t * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4));
+        else
+          frag_col<ImgMN<B_RB>>(fb[t], Bi, wn * 64 + t * 16, kk * 32, lane);
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) mma16(acc[a][b], fa[a], fb[b]);
+    }
+    if (more) {
+      sa.store(smem[cur ^ 1][0]);
+      sb.store(smem[cur ^ 1][1]);
+    }
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  const int epi = p.epi;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int j = n0 + wn * 64 + b * 16 + (lane & 15);
+    const bool jok = j < p.N;
+    float bj = 0.f;
+    if (p.bias != nullptr && jok && epi != NSTL_EPI_NONE && epi != NSTL_EPI_DRELU_DROP) bj = p.bias[j];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = m0 + wm * 64 + a * 16 + 4 * (lane >> 4) + r;
+        float v = acc[a][b][r] * p.alpha;
+        if (p.ws != nullptr) {  // split-K partial
+          if (jok && i < p.M) p.ws[((int64_t)blockIdx.y * p.M + i) * p.N + j] = v;
+          continue;
+        }
+        v += bj;
+        if (epi == NSTL_EPI_BIAS_RELU_DROP) {
+          v = fmaxf(v, 0.f);
+          if (p.thresh) v = nstl_keep(p.seed, (uint64_t)i * p.N + j, p.thresh) ? v * p.inv_keep : 0.f;
+        } else if (epi == NSTL_EPI_BIAS_ROPE) {
+          const float partner = __shfl_xor(v, 1);
+          if (j < p.rope_cols) {
+            const int t = i % p.rope_T;
+            const int half = p.rope_dim >> 1;
+            const int pair = (j % p.rope_dim) >> 1;
+            const float c = p.rope_cos[t * half + pair], s = p.rope_sin[t * half + pair];
+            v = (j & 1) ? (partner * s + v * c) : (v * c - partner * s);
+          }
+        } else if (epi == NSTL_EPI_DRELU_DROP) {
+          if (jok && i < p.M) {
+            const int64_t e = (int64_t)i * p.ld_aux + j;
+            const float av = p.aux_f32 ? ((const float*)p.aux)[e] : (float)((const bf16*)p.aux)[e];
+            v = av > 0.f ? v * p.inv_keep : 0.f;
+          }
+        }
+        if (jok && i < p.M) {
+          const int64_t e = (int64_t)i * p.ldc + j;
+          if (p.c_f32) {
+            float* c = (float*)p.C + e;
+            if (p.beta != 0.f) v += p.beta * *c;
+            *c = v;
+          } else {
+            bf16* c = (bf16*)p.C + e;
+            if (p.beta != 0.f) v += p.beta * (float)*c;
+            *c = (bf16)v;
+          }
+        }
+      }
+    }
+  }
+}
+
+// split-K combine: C = sum_z ws[z] (+bias) (+beta*C)
+__global__ void splitk_reduce(const float* ws, int splits, int M, int N, char* C, int64_t ldc, int c_f32,
+                              float beta, const float* bias) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += ws[(int64_t)z * total + e];
+    const int i = (int)(e / N), j = (int)(e % N);
+    if (bias) v += bias[j];
+    const int64_t o = (int64_t)i * ldc + j;
+    if (c_f32) {
+      float* c = (float*)C + o;
+      if (beta != 0.f) v += beta * *c;
+      *c = v;
+    } else {
+      bf16* c = (bf16*)C + o;
+      if (beta != 0.f) v += beta * (float)*c;
+      *c = (bf16)v;
+    }
+  }
+}
+
+template <typename T>
+int launch_typed(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t st) {
+  const int nt = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
+  dim3 grid(nt, splits), block(NTHREADS);
+  if (a->a_kmajor && a->b_kmajor)
+    hipLaunchKernelGGL((gemm_kernel<T, true, true>), grid, block, 0, st, p);
+  else if (a->a_kmajor && !a->b_kmajor)
+    hipLaunchKernelGGL((gemm_kernel<T, true, false>), grid, block, 0, st, p);
+  else if (!a->a_kmajor && !a->b_kmajor)
+    hipLaunchKernelGGL((gemm_kernel<T, false, false>), grid, block, 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_kernel<T, false, true>), grid, block, 0, st, p);
+  NSTL_LAUNCH_CHECK("nstl_gemm");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int64_t nstl_gemm_workspace_bytes(int M, int N, int split_k) {
+  return split_k > 1 ? (int64_t)split_k * M * N * 4 : 0;
+}
+
+extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
+  NSTL_CHECK_ARG(a != nullptr, "nstl_gemm: null args");
+  NSTL_CHECK_ARG(a->dtype == NSTL_F32 || a->dtype == NSTL_BF16, "nstl_gemm: bad dtype %d", a->dtype);
+  NSTL_CHECK_ARG(a->c_dtype == NSTL_F32 || a->c_dtype == NSTL_BF16, "nstl_gemm: bad c_dtype");
+  NSTL_CHECK_ARG(a->M > 0 && a->N > 0 && a->K > 0, "nstl_gemm: empty problem %dx%dx%d", a->M, a->N, a->K);
+  const int esz = a->dtype == NSTL_F32 ? 4 : 2;
+  const int vec = 16 / esz;
+  NSTL_CHECK_ARG(((uintptr_t)a->A % 16) == 0 && ((uintptr_t)a->B % 16) == 0,
+                 "nstl_gemm: A and B must be 16-byte aligned");
+  NSTL_CHECK_ARG(a->lda % vec == 0 && a->ldb % vec == 0, "nstl_gemm: lda/ldb must be multiples of %d", vec);
+  // K-major rows are read in 16-byte chunks: the reduction extent is rounded up to
+  // a chunk and must be readable (zero-padded) up to lda/ldb.
+  NSTL_CHECK_ARG(!a->a_kmajor || a->lda >= ((a->K + vec - 1) / vec) * vec, "nstl_gemm: lda < K");
+  NSTL_CHECK_ARG(!a->b_kmajor || a->ldb >= ((a->K + vec - 1) / vec) * vec, "nstl_gemm: ldb < K");
+  NSTL_CHECK_ARG(a->a_kmajor || a->lda >= ((a->M + vec - 1) / vec) * vec, "nstl_gemm: lda < M");
+  NSTL_CHECK_ARG(a->b_kmajor || a->ldb >= ((a->N + vec - 1) / vec) * vec, "nstl_gemm: ldb < N");
+  NSTL_CHECK_ARG(a->ldc >= a->N, "nstl_gemm: ldc < N");
+  NSTL_CHECK_ARG(a->epilogue >= 0 && a->epilogue <= 4, "nstl_gemm: bad epilogue %d", a->epilogue);
+  if (a->epilogue == NSTL_EPI_BIAS_ROPE) {
+    NSTL_CHECK_ARG(a->rope_cos && a->rope_sin && a->rope_T > 0 && a->rope_dim > 0 && a->rope_dim % 2 == 0,
+                   "nstl_gemm: rope tables missing");
+    NSTL_CHECK_ARG(a->rope_cols % 16 == 0, "nstl_gemm: rope_cols must be a multiple of 16");
+  }
+  if (a->epilogue == NSTL_EPI_DRELU_DROP) NSTL_CHECK_ARG(a->aux != nullptr, "nstl_gemm: aux missing");
+  NSTL_CHECK_ARG(a->p_drop >= 0.f && a->p_drop < 1.f, "nstl_gemm: p_drop out of range");
+
+  GemmParams p;
+  p.A = (const char*)a->A; p.lda = a->lda;
+  p.B = (const char*)a->B; p.ldb = a->ldb;
+  p.C = (char*)a->C; p.ldc = a->ldc;
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.c_f32 = a->c_dtype == NSTL_F32;
+  p.alpha = a->alpha; p.beta = a->beta;
+  p.epi = a->epilogue;
+  p.bias = a->bias;
+  p.aux = (const char*)a->aux; p.ld_aux = a->ld_aux; p.aux_f32 = a->dtype == NSTL_F32;
+  p.thresh = nstl_drop_thresh(a->p_drop);
+  p.inv_keep = 1.0f / (1.0f - a->p_drop);
+  p.seed = a->seed;
+  p.rope_cos = a->rope_cos; p.rope_sin = a->rope_sin;
+  p.rope_T = a->rope_T; p.rope_dim = a->rope_dim; p.rope_cols = a->rope_cols;
+  p.ws = nullptr;
+
+  const int BKe = 128 / esz;
+  int splits = a->split_k > 1 ? a->split_k : 1;
+  if (splits > 1) {
+    NSTL_CHECK_ARG(a->epilogue == NSTL_EPI_NONE || a->epilogue == NSTL_EPI_BIAS,
+                   "nstl_gemm: split-K supports NONE/BIAS epilogues only");
+    NSTL_CHECK_ARG(a->workspace != nullptr && a->workspace_bytes >= nstl_gemm_workspace_bytes(a->M, a->N, splits),
+                   "nstl_gemm: split-K workspace too small");
+    p.ws = (float*)a->workspace;
+  }
+  int chunk = (a->K + splits - 1) / splits;
+  chunk = ((chunk + BKe - 1) / BKe) * BKe;
+  splits = (a->K + chunk - 1) / chunk;
+  p.k_chunk = chunk;
+  if (splits == 1) p.ws = nullptr;
+
+  hipStream_t st = (hipStream_t)stream;
+  int rc = a->dtype == NSTL_BF16 ? launch_typed<bf16>(a, p, splits, st) : launch_typed<float>(a, p, splits, st);
+  if (rc) return rc;
+  if (p.ws != nullptr) {
+    const int64_t total = (int64_t)a->M * a->N;
+    int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, p.ws, splits, a->M, a->N, p.C, a->ldc,
+                       p.c_f32, a->beta, a->epilogue == NSTL_EPI_BIAS ? a->bias : nullptr);
+    NSTL_LAUNCH_CHECK("nstl_gemm splitk_reduce");
+  }
+  return 0;
+}

@@ -1,0 +1,162 @@
+// Fused Loss forward + backward (replaces Loss.forward, utils/model.py:278-291,
+// and its autograd graph: SmoothL1 + L1 of first differences + directional
+// cosine of first differences, eps 1e-8 added to the difference norms).
+//
+//   rec  = mean_{b,t,f} huber_delta(p - y)
+//   temp = mean_{b,t<T-1,f} |dp - dy|                   dp_t = p_{t+1} - p_t
+//   dir  = 1 - mean_{b,t<T-1} <dp_t/(|dp_t|+eps), dy_t/(|dy_t|+eps)>
+//   loss = w1 rec + w2 temp + w3 dir
+// One workgroup per sequence b: the clip is staged in LDS, per-step norms are
+// wave reductions, the gradient is written straight into the (zero-padded)
+// dpred operand of the output-head backward GEMMs.
+#include "../../include/nstl.h"
+#include "common.h"
+#include "status.h"
+
+namespace {
+constexpr int NT = 256;
+constexpr int TMAX = 256, FMAX = 64;
+
+struct LossParams {
+  int B, T, F;
+  const float* pred; int64_t pred_ld;
+  const float* trg; int64_t trg_ld;
+  float delta, w1, w2, w3, gscale;
+  char* dpred; int d_f32; int64_t dpred_ld;
+  float* partial; float* out;
+};
+
+__global__ __launch_bounds__(NT) void loss_kernel(LossParams p) {
+  __shared__ float P[TMAX][FMAX + 1];
+  __shared__ float Y[TMAX][FMAX + 1];
+  // per-step scalars: 1/(|dp|+eps), 1/(|dy|+eps), cos_t, |dp|
+  __shared__ float s_inp[TMAX], s_iny[TMAX], s_cos[TMAX], s_np[TMAX];
+  __shared__ float red[3][NT / 64];
+  const int b = blockIdx.x, T = p.T, F = p.F;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int e = tid; e < T * F; e += NT) {
+    const int t = e / F, f = e % F;
+    P[t][f] = p.pred[((int64_t)b * T + t) * p.pred_ld + f];
+    Y[t][f] = p.trg[((int64_t)b * T + t) * p.trg_ld + f];
+  }
+  __syncthreads();
+  // per-step cosine terms (one wave per step)
+  float cos_acc = 0.f;
+  for (int t = w; t < T - 1; t += NT / 64) {
+    float np2 = 0.f, ny2 = 0.f;
+    for (int f = lane; f < F; f += 64) {
+      const float dp = P[t + 1][f] - P[t][f], dy = Y[t + 1][f] - Y[t][f];
+      np2 += dp * dp;
+      ny2 += dy * dy;
+    }
+    const float np = sqrtf(wave_sum(np2)), ny = sqrtf(wave_sum(ny2));
+    const float inp = 1.f / (np + 1e-8f), iny = 1.f / (ny + 1e-8f);
+    float dot = 0.f;
+    for (int f = lane; f < F; f += 64) {
+      const float dp = P[t + 1][f] - P[t][f], dy = Y[t + 1][f] - Y[t][f];
+      dot += (dp * inp) * (dy * iny);
+    }
+    const float cs = wave_sum(dot);  // cos_t = sum_f pn * tn (same value in every lane)
+    if (lane == 0) cos_acc += cs;
+    if (lane == 0) {
+      s_inp[t] = inp;
+      s_iny[t] = iny;
+      s_cos[t] = cs;
+      s_np[t] = np;
+    }
+  }
+  __syncthreads();
+  const float n_rec = (float)p.B * T * F;
+  const float n_tmp = (float)p.B * (T - 1) * F;
+  const float n_dir = (float)p.B * (T - 1);
+  float rec_acc = 0.f, tmp_acc = 0.f;
+  const int ldd = (int)p.dpred_ld;
+  // d cos_t / d dp_{t,f} = tn_f/(|dp|+eps) - cos_t * dp_f / (|dp| (|dp|+eps))  (2nd term 0 if |dp| == 0,
+  // torch's norm backward at the origin)
+  auto gcos = [&](int t, int f) {
+    const float dp = P[t + 1][f] - P[t][f], dy = Y[t + 1][f] - Y[t][f];
+    float gv = dy * s_iny[t] * s_inp[t];
+    const float np = s_np[t];
+    if (np > 0.f) gv -= s_cos[t] * dp / (np * (np + 1e-8f));
+    return gv;
+  };
+  for (int e = tid; e < T * ldd; e += NT) {
+    const int t = e / ldd, f = e % ldd;
+    float g = 0.f;
+    if (f < F) {
+      const float d = P[t][f] - Y[t][f], ad = fabsf(d);
+      rec_acc += ad < p.delta ? 0.5f * d * d / p.delta : ad - 0.5f * p.delta;
+      g = p.w1 * (ad < p.delta ? d / p.delta : (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f))) / n_rec;
+      // gradient w.r.t. dp_{t-1} (+) and dp_t (-)
+      float gd_prev = 0.f, gd_cur = 0.f;
+      if (t >= 1) {
+        const float z = (P[t][f] - P[t - 1][f]) - (Y[t][f] - Y[t - 1][f]);
+        gd_prev = p.w2 * (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f)) / n_tmp - p.w3 * gcos(t - 1, f) / n_dir;
+      }
+      if (t < T - 1) {
+        const float z = (P[t + 1][f] - P[t][f]) - (Y[t + 1][f] - Y[t][f]);
+        tmp_acc += fabsf(z);
+        gd_cur = p.w2 * (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f)) / n_tmp - p.w3 * gcos(t, f) / n_dir;
+      }
+      g = (g + gd_prev - gd_cur) * p.gscale;
+    }
+    const int64_t o = ((int64_t)b * T + t) * p.dpred_ld + f;
+    if (p.d_f32) ((float*)p.dpred)[o] = g;
+    else ((bf16*)p.dpred)[o] = (bf16)g;
+  }
+  rec_acc = wave_sum(rec_acc);
+  tmp_acc = wave_sum(tmp_acc);
+  cos_acc = wave_sum(cos_acc);
+  if (lane == 0) {
+    red[0][w] = rec_acc;
+    red[1][w] = tmp_acc;
+    red[2][w] = cos_acc;
+  }
+  __syncthreads();
+  if (tid < 3) {
+    float s = 0.f;
+    for (int k = 0; k < NT / 64; ++k) s += red[tid][k];
+    p.partial[b * 4 + tid] = s;
+  }
+}
+
+__global__ void loss_final(LossParams p) {
+  // deterministic serial combine over the (few hundred) sequences, in double
+  if (threadIdx.x != 0) return;
+  double r = 0, t = 0, c = 0;
+  for (int b = 0; b < p.B; ++b) {
+    r += p.partial[b * 4 + 0];
+    t += p.partial[b * 4 + 1];
+    c += p.partial[b * 4 + 2];
+  }
+  const double rec = r / ((double)p.B * p.T * p.F);
+  const double tmp = t / ((double)p.B * (p.T - 1) * p.F);
+  const double dir = 1.0 - c / ((double)p.B * (p.T - 1));
+  p.out[0] = (float)(p.w1 * rec + p.w2 * tmp + p.w3 * dir);
+  p.out[1] = (float)rec;
+  p.out[2] = (float)tmp;
+  p.out[3] = (float)dir;
+}
+}  // namespace
+
+extern "C" int nstl_loss_fwd_bwd(const nstl_loss_args* a, void* stream) {
+  NSTL_CHECK_ARG(a != nullptr, "nstl_loss: null args");
+  NSTL_CHECK_ARG(a->B > 0 && a->T >= 2 && a->T <= TMAX && a->F > 0 && a->F <= FMAX,
+                 "nstl_loss: shape B=%d T=%d F=%d unsupported (T in [2,%d], F <= %d)", a->B, a->T, a->F, TMAX, FMAX);
+  NSTL_CHECK_ARG(a->pred && a->trg && a->dpred && a->partial && a->loss_out, "nstl_loss: null tensor");
+  NSTL_CHECK_ARG(a->dpred_ld >= a->F && a->pred_ld >= a->F && a->trg_ld >= a->F, "nstl_loss: ld < F");
+  NSTL_CHECK_ARG(a->delta > 0.f, "nstl_loss: delta must be > 0");
+  LossParams p;
+  p.B = a->B; p.T = a->T; p.F = a->F;
+  p.pred = a->pred; p.pred_ld = a->pred_ld;
+  p.trg = a->trg; p.trg_ld = a->trg_ld;
+  p.delta = a->delta; p.w1 = a->w1; p.w2 = a->w2; p.w3 = a->w3; p.gscale = a->grad_scale;
+  p.dpred = (char*)a->dpred; p.d_f32 = a->dpred_dtype == NSTL_F32; p.dpred_ld = a->dpred_ld;
+  p.partial = a->partial; p.out = a->loss_out;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(loss_kernel, dim3(a->B), dim3(NT), 0, st, p);
+  NSTL_LAUNCH_CHECK("nstl_loss_fwd_bwd");
+  hipLaunchKernelGGL(loss_final, dim3(1), dim3(64), 0, st, p);
+  NSTL_LAUNCH_CHECK("nstl_loss_fwd_bwd final");
+  return 0;
+}

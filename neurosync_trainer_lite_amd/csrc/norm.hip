@@ -1,0 +1,253 @@
+// Post-LN residual tails of the NeuroSync Seq2Seq layers (utils/model.py:175-180,
+// :198-207, final norms :228-229/:249-250):
+//   forward : s = x + y * m1 * m2 / (1-p)^n ; out = (s - mean) * rstd * gamma + beta
+//             (+ optional global-PE rotation of `out`, model.py:246)
+//   backward: ds = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat));
+//             dbranch = ds * masks / (1-p)^n ; per-block dgamma/dbeta partials.
+// One wave per row; each lane owns VPL = D/64 contiguous columns (vector I/O).
+#include <algorithm>
+
+#include "../../include/nstl.h"
+#include "common.h"
+#include "status.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+template <typename T, int VPL>
+NSTL_DEV void load_row(const T* p, float (&v)[VPL]) {
+  if constexpr ((VPL * sizeof(T)) % 16 == 0) {
+    constexpr int NV = VPL * sizeof(T) / 16;
+    constexpr int EPV = 16 / sizeof(T);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const uint4 u = ((const uint4*)p)[k];
+      const T* e = (const T*)&u;
+#pragma unroll
+      for (int j = 0; j < EPV; ++j) v[k * EPV + j] = to_f32(e[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) v[j] = to_f32(p[j]);
+  }
+}
+
+template <typename T, int VPL>
+NSTL_DEV void store_row(T* p, const float (&v)[VPL]) {
+  if constexpr ((VPL * sizeof(T)) % 16 == 0) {
+    constexpr int NV = VPL * sizeof(T) / 16;
+    constexpr int EPV = 16 / sizeof(T);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      uint4 u;
+      T* e = (T*)&u;
+#pragma unroll
+      for (int j = 0; j < EPV; ++j) e[j] = from_f32<T>(v[k * EPV + j]);
+      ((uint4*)p)[k] = u;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) p[j] = from_f32<T>(v[j]);
+  }
+}
+
+struct LnParams {
+  const char* x; const char* y;
+  int rows, D;
+  int n_masks; uint32_t thresh; float inv_keep; uint64_t seed1, seed2;
+  const float* gamma; const float* beta; float eps;
+  char* s_out; char* out; float* mean; float* rstd;
+  char* rot_out; const float* rope_cos; const float* rope_sin; int rope_T;
+  const char* s_in; const float* dout; float* ds; char* dbranch;
+  float* dgp; float* dbp;
+};
+
+NSTL_DEV float branch_scale(const LnParams& p, uint64_t idx) {
+  float m = 1.f;
+  if (p.n_masks >= 1) m = nstl_keep(p.seed1, idx, p.thresh) ? p.inv_keep : 0.f;
+  if (p.n_masks >= 2) m = nstl_keep(p.seed2, idx, p.thresh) ? m * p.inv_keep : 0.f;
+  return m;
+}
+
+template <typename T, int VPL>
+__global__ __launch_bounds__(NT) void ln_fwd_kernel(LnParams p) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  const int c0 = lane * VPL;
+  const int64_t base = (int64_t)row * p.D + c0;
+  float s[VPL];
+  load_row<T, VPL>((const T*)p.y + base, s);
+  if (p.thresh && p.n_masks > 0) {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) s[j] *= branch_scale(p, (uint64_t)base + j);
+  }
+  if (p.x) {
+    float xv[VPL];
+    load_row<T, VPL>((const T*)p.x + base, xv);
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) s[j] += xv[j];
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) sum += s[j];
+  const float mean = wave_sum(sum) / p.D;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const float d = s[j] - mean;
+    sq += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / p.D + p.eps);
+  if (p.s_out) store_row<T, VPL>((T*)p.s_out + base, s);
+  float o[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) o[j] = (s[j] - mean) * rstd * p.gamma[c0 + j] + p.beta[c0 + j];
+  // round to the storage type first so `rot_out` rotates exactly what `out` holds
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) o[j] = to_f32(from_f32<T>(o[j]));
+  store_row<T, VPL>((T*)p.out + base, o);
+  if (lane == 0) {
+    p.mean[row] = mean;
+    p.rstd[row] = rstd;
+  }
+  if (p.rot_out) {
+    const int t = row % p.rope_T, half = p.D >> 1;
+    float r[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; j += 2) {
+      const int pr = (c0 + j) >> 1;
+      const float c = p.rope_cos[t * half + pr], sn = p.rope_sin[t * half + pr];
+      r[j] = o[j] * c - o[j + 1] * sn;
+      r[j + 1] = o[j] * sn + o[j + 1] * c;
+    }
+    store_row<T, VPL>((T*)p.rot_out + base, r);
+  }
+}
+
+template <typename T, int VPL>
+__global__ __launch_bounds__(NT) void ln_bwd_kernel(LnParams p) {
+  const int lane = threadIdx.x & 63;
+  const int c0 = lane * VPL;
+  float gam[VPL], dg[VPL], db[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    gam[j] = p.gamma[c0 + j];
+    dg[j] = 0.f;
+    db[j] = 0.f;
+  }
+  for (int row = blockIdx.x * (NT / 64) + (threadIdx.x >> 6); row < p.rows; row += gridDim.x * (NT / 64)) {
+    const int64_t base = (int64_t)row * p.D + c0;
+    const float mean = p.mean[row], rstd = p.rstd[row];
+    float xh[VPL], gy[VPL];
+    load_row<T, VPL>((const T*)p.s_in + base, xh);
+    load_row<float, VPL>(p.dout + base, gy);
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      xh[j] = (xh[j] - mean) * rstd;
+      dg[j] += gy[j] * xh[j];
+      db[j] += gy[j];
+      const float gg = gy[j] * gam[j];
+      a1 += gg;
+      a2 += gg * xh[j];
+    }
+    const float m1 = wave_sum(a1) / p.D, m2 = wave_sum(a2) / p.D;
+    float d[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) d[j] = rstd * (gy[j] * gam[j] - m1 - xh[j] * m2);
+    store_row<float, VPL>(p.ds + base, d);
+    if (p.dbranch) {
+      if (p.thresh && p.n_masks > 0) {
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) d[j] *= branch_scale(p, (uint64_t)base + j);
+      }
+      store_row<T, VPL>((T*)p.dbranch + base, d);
+    }
+  }
+  // per-block partials: reduce the 4 waves through LDS
+  __shared__ float red[2][NT / 64][1024];
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    red[0][w][c0 + j] = dg[j];
+    red[1][w][c0 + j] = db[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < p.D; c += NT) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) {
+      a += red[0][k][c];
+      b += red[1][k][c];
+    }
+    p.dgp[(int64_t)blockIdx.x * p.D + c] = a;
+    p.dbp[(int64_t)blockIdx.x * p.D + c] = b;
+  }
+}
+
+template <typename T, bool BWD>
+int dispatch(const LnParams& p, int grid, hipStream_t st) {
+#define NSTL_LN_CASE(V)                                                                     \
+  case V:                                                                                   \
+    if (BWD) hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(grid), dim3(NT), 0, st, p);    \
+    else hipLaunchKernelGGL((ln_fwd_kernel<T, V>), dim3(grid), dim3(NT), 0, st, p);        \
+    break;
+  switch (p.D / 64) {
+    NSTL_LN_CASE(2)
+    NSTL_LN_CASE(4)
+    NSTL_LN_CASE(8)
+    NSTL_LN_CASE(16)
+    default:
+      return nstl::fail((int)hipErrorInvalidValue, "nstl_ln: D=%d unsupported (128/256/512/1024)", p.D);
+  }
+#undef NSTL_LN_CASE
+  NSTL_LAUNCH_CHECK(BWD ? "nstl_ln_bwd" : "nstl_ln_fwd");
+  return 0;
+}
+
+int fill(LnParams& p, const nstl_ln_args* a) {
+  NSTL_CHECK_ARG(a != nullptr, "nstl_ln: null args");
+  NSTL_CHECK_ARG(a->dtype == NSTL_F32 || a->dtype == NSTL_BF16, "nstl_ln: bad dtype");
+  NSTL_CHECK_ARG(a->rows > 0 && a->D > 0 && a->D % 64 == 0 && a->D <= 1024, "nstl_ln: bad shape");
+  NSTL_CHECK_ARG(a->gamma && a->beta, "nstl_ln: gamma/beta missing");
+  NSTL_CHECK_ARG(a->n_masks >= 0 && a->n_masks <= 2 && a->p_drop >= 0.f && a->p_drop < 1.f, "nstl_ln: dropout");
+  p.x = (const char*)a->x; p.y = (const char*)a->y;
+  p.rows = a->rows; p.D = a->D;
+  p.n_masks = a->n_masks;
+  p.thresh = nstl_drop_thresh(a->p_drop);
+  p.inv_keep = 1.0f / (1.0f - a->p_drop);
+  p.seed1 = a->seed1; p.seed2 = a->seed2;
+  p.gamma = a->gamma; p.beta = a->beta; p.eps = a->eps;
+  p.s_out = (char*)a->s_out; p.out = (char*)a->out; p.mean = a->mean; p.rstd = a->rstd;
+  p.rot_out = (char*)a->rot_out; p.rope_cos = a->rope_cos; p.rope_sin = a->rope_sin; p.rope_T = a->rope_T;
+  p.s_in = (const char*)a->s_in; p.dout = a->dout; p.ds = a->ds; p.dbranch = (char*)a->dbranch;
+  p.dgp = a->dgamma_part; p.dbp = a->dbeta_part;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int nstl_ln_fwd(const nstl_ln_args* a, void* stream) {
+  LnParams p;
+  int rc = fill(p, a);
+  if (rc) return rc;
+  NSTL_CHECK_ARG(a->y && a->out && a->mean && a->rstd, "nstl_ln_fwd: null tensor");
+  NSTL_CHECK_ARG(!a->rot_out || (a->rope_cos && a->rope_sin && a->rope_T > 0), "nstl_ln_fwd: rope tables");
+  const int grid = (a->rows + NT / 64 - 1) / (NT / 64);
+  return a->dtype == NSTL_BF16 ? dispatch<bf16, false>(p, grid, (hipStream_t)stream)
+                               : dispatch<float, false>(p, grid, (hipStream_t)stream);
+}
+
+extern "C" int nstl_ln_bwd(const nstl_ln_args* a, void* stream) {
+  LnParams p;
+  int rc = fill(p, a);
+  if (rc) return rc;
+  NSTL_CHECK_ARG(a->s_in && a->dout && a->ds && a->mean && a->rstd, "nstl_ln_bwd: null tensor");
+  NSTL_CHECK_ARG(a->dgamma_part && a->dbeta_part && a->n_part > 0, "nstl_ln_bwd: partials");
+  const int grid = std::min(a->n_part, (a->rows + NT / 64 - 1) / (NT / 64));
+  NSTL_CHECK_ARG(grid == a->n_part, "nstl_ln_bwd: n_part (%d) must be <= rows/4", a->n_part);
+  return a->dtype == NSTL_BF16 ? dispatch<bf16, true>(p, grid, (hipStream_t)stream)
+                               : dispatch<float, true>(p, grid, (hipStream_t)stream);
+}

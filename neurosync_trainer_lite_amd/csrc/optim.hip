@@ -1,0 +1,256 @@
+// Optimizer + small memory-bound kernels over flat f32 arenas.
+//   nstl_sumsq      : stage 1 of the global grad norm (clip_grad_norm_, utils/training_utils.py:73)
+//   nstl_adam_step  : clip coefficient + Adam with coupled L2 (torch.optim.Adam(weight_decay),
+//                     utils/model_utils.py:11) + bf16 shadow copy, one pass over the arena
+//   nstl_cast, nstl_colsum (bias grads), nstl_reduce_rows, nstl_rope
+#include <algorithm>
+#include <cmath>
+
+#include "../../include/nstl.h"
+#include "common.h"
+#include "status.h"
+
+namespace {
+constexpr int NT = 256;
+
+__global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, float* partial) {
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(n, lo + per);
+  double acc = 0.0;
+  // vector body (16-byte aligned part)
+  int64_t v0 = (lo + 3) & ~(int64_t)3, v1 = hi & ~(int64_t)3;
+  if (v0 > hi) v0 = hi;
+  if (v1 < v0) v1 = v0;
+  for (int64_t i = lo + threadIdx.x; i < v0; i += NT) acc += (double)g[i] * g[i];
+  for (int64_t i = v0 / 4 + threadIdx.x; i < v1 / 4; i += NT) {
+    const f32x4 x = ((const f32x4*)g)[i];
+    acc += (double)(x[0] * x[0] + x[1] * x[1]) + (double)(x[2] * x[2] + x[3] * x[3]);
+  }
+  for (int64_t i = v1 + threadIdx.x; i < hi; i += NT) acc += (double)g[i] * g[i];
+  __shared__ double red[NT / 64];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0;
+    for (int k = 0; k < NT / 64; ++k) s += red[k];
+    partial[blockIdx.x] = (float)s;
+  }
+}
+
+struct AdamParams {
+  float* p; const float* g; float* m; float* v; char* lowp; int lowp_bf16;
+  int64_t n;
+  float lr, b1, b2, eps, wd, step_size, bc2_sqrt;
+  const float* part; int n_part; float max_norm; float* norm_out;
+};
+
+NSTL_DEV void adam_elem(const AdamParams& a, float coef, int64_t i) {
+  const float pv = a.p[i];
+  float g = a.g[i] * coef;
+  g = g + a.wd * pv;
+  float m = a.m[i];
+  m = m + (1.f - a.b1) * (g - m);
+  float v = a.v[i];
+  v = v * a.b2 + (1.f - a.b2) * g * g;
+  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+  const float np = pv + (-a.step_size) * (m / denom);
+  a.p[i] = np;
+  a.m[i] = m;
+  a.v[i] = v;
+  if (a.lowp) {
+    if (a.lowp_bf16) ((bf16*)a.lowp)[i] = (bf16)np;
+    else ((float*)a.lowp)[i] = np;
+  }
+}
+
+__global__ __launch_bounds__(NT) void adam_kernel(AdamParams a) {
+  __shared__ float coef_s;
+  if (threadIdx.x < 64) {
+    double s = 0;
+    if (a.part) {
+      for (int k = threadIdx.x; k < a.n_part; k += 64) s += a.part[k];
+      s = wave_sum_d(s);
+    }
+    if (threadIdx.x == 0) {
+      float coef = 1.f;
+      if (a.part) {
+        const float total = (float)sqrt(s);
+        const float c = a.max_norm / (total + 1e-6f);
+        coef = c < 1.f ? c : 1.f;
+        if (blockIdx.x == 0 && a.norm_out) a.norm_out[0] = total;
+      }
+      coef_s = coef;
+    }
+  }
+  __syncthreads();
+  const float coef = coef_s;
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) adam_elem(a, coef, i);
+}
+
+__global__ void cast_kernel(int src_bf16, const void* src, int dst_bf16, void* dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = src_bf16 ? (float)((const bf16*)src)[i] : ((const float*)src)[i];
+    if (dst_bf16) ((bf16*)dst)[i] = (bf16)v;
+    else ((float*)dst)[i] = v;
+  }
+}
+
+__global__ void copy2d_kernel(int src_bf16, const void* src, int64_t src_ld, int dst_bf16, void* dst, int64_t dst_ld,
+                              int rows, int cols, int dst_cols, const float* scale) {
+  const float sc = scale ? scale[0] : 1.f;
+  const int64_t total = (int64_t)rows * dst_cols;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / dst_cols), j = (int)(e % dst_cols);
+    float v = 0.f;
+    if (j < cols) {
+      const int64_t s = (int64_t)i * src_ld + j;
+      v = sc * (src_bf16 ? (float)((const bf16*)src)[s] : ((const float*)src)[s]);
+    }
+    const int64_t d = (int64_t)i * dst_ld + j;
+    if (dst_bf16) ((bf16*)dst)[d] = (bf16)v;
+    else ((float*)dst)[d] = v;
+  }
+}
+
+constexpr int COLSUM_ROWS = 256;
+template <typename T>
+__global__ void colsum_kernel(const T* x, int64_t ld, int rows, int cols, float* partial) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cols) return;
+  const int r0 = blockIdx.y * COLSUM_ROWS, r1 = min(rows, r0 + COLSUM_ROWS);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += to_f32(x[(int64_t)r * ld + j]);
+  partial[(int64_t)blockIdx.y * cols + j] = s;
+}
+
+__global__ void reduce_rows_kernel(const float* part, int n_part, int cols, float* out, float beta) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < n_part; ++k) s += part[(int64_t)k * cols + j];
+  out[j] = beta != 0.f ? beta * out[j] + s : s;
+}
+
+template <typename TI, typename TO>
+__global__ void rope_kernel(const TI* in, int64_t in_ld, TO* out, int64_t out_ld, int rows, int cols,
+                            const float* cs, const float* sn, int T, int rope_dim, int inverse, int acc) {
+  const int half = cols >> 1;
+  const int64_t total = (int64_t)rows * half;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / half), pj = (int)(e % half);
+    const int j = 2 * pj;
+    const int t = i % T, pr = (j % rope_dim) >> 1;
+    const float c = cs[t * (rope_dim / 2) + pr], s = inverse ? -sn[t * (rope_dim / 2) + pr] : sn[t * (rope_dim / 2) + pr];
+    const float a = to_f32(in[(int64_t)i * in_ld + j]), b = to_f32(in[(int64_t)i * in_ld + j + 1]);
+    float ra = a * c - b * s, rb = a * s + b * c;
+    TO* o = out + (int64_t)i * out_ld + j;
+    if (acc) {
+      ra += to_f32(o[0]);
+      rb += to_f32(o[1]);
+    }
+    o[0] = from_f32<TO>(ra);
+    o[1] = from_f32<TO>(rb);
+  }
+}
+
+int grid_for(int64_t n, int per_thread = 1) {
+  int64_t g = (n + (int64_t)NT * per_thread - 1) / ((int64_t)NT * per_thread);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 8192));
+}
+}  // namespace
+
+extern "C" int nstl_sumsq(const float* g, int64_t n, float* partial, int n_partial, void* stream) {
+  NSTL_CHECK_ARG(g && partial && n > 0 && n_partial > 0 && n_partial <= 1024, "nstl_sumsq: bad args");
+  NSTL_CHECK_ARG(((uintptr_t)g % 16) == 0, "nstl_sumsq: g must be 16-byte aligned");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(n_partial), dim3(NT), 0, (hipStream_t)stream, g, n, partial);
+  NSTL_LAUNCH_CHECK("nstl_sumsq");
+  return 0;
+}
+
+extern "C" int nstl_adam_step(const nstl_adam_args* a, void* stream) {
+  NSTL_CHECK_ARG(a && a->p && a->g && a->m && a->v && a->n > 0, "nstl_adam_step: bad args");
+  NSTL_CHECK_ARG(a->step >= 1, "nstl_adam_step: step must be >= 1");
+  NSTL_CHECK_ARG(!a->sumsq_partial || (a->n_partial > 0 && a->n_partial <= 1024), "nstl_adam_step: partials");
+  AdamParams p;
+  p.p = a->p; p.g = a->g; p.m = a->m; p.v = a->v;
+  p.lowp = (char*)a->p_lowp; p.lowp_bf16 = a->lowp_dtype == NSTL_BF16;
+  p.n = a->n;
+  p.lr = a->lr; p.b1 = a->beta1; p.b2 = a->beta2; p.eps = a->eps; p.wd = a->weight_decay;
+  // bias corrections in double on the host, handed to the kernel as f32 scalars
+  // (torch's foreach Adam casts its python-float scalars the same way)
+  const double bc1 = 1.0 - std::pow((double)a->beta1, a->step);
+  const double bc2 = 1.0 - std::pow((double)a->beta2, a->step);
+  p.step_size = (float)(a->lr / bc1);
+  p.bc2_sqrt = (float)std::sqrt(bc2);
+  p.part = a->sumsq_partial; p.n_part = a->n_partial; p.max_norm = a->max_norm; p.norm_out = a->norm_out;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(a->n, 4)), dim3(NT), 0, (hipStream_t)stream, p);
+  NSTL_LAUNCH_CHECK("nstl_adam_step");
+  return 0;
+}
+
+extern "C" int nstl_cast(int src_dtype, const void* src, int dst_dtype, void* dst, int64_t n, void* stream) {
+  NSTL_CHECK_ARG(src && dst && n >= 0, "nstl_cast: bad args");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n, 4)), dim3(NT), 0, (hipStream_t)stream,
+                     src_dtype == NSTL_BF16, src, dst_dtype == NSTL_BF16, dst, n);
+  NSTL_LAUNCH_CHECK("nstl_cast");
+  return 0;
+}
+
+extern "C" int nstl_copy2d(int src_dtype, const void* src, int64_t src_ld, int dst_dtype, void* dst, int64_t dst_ld,
+                           int rows, int cols, int dst_cols, const float* scale, void* stream) {
+  NSTL_CHECK_ARG(src && dst && rows >= 0 && cols >= 0 && dst_cols >= cols && src_ld >= cols && dst_ld >= dst_cols,
+                 "nstl_copy2d: bad args");
+  if (rows == 0 || dst_cols == 0) return 0;
+  hipLaunchKernelGGL(copy2d_kernel, dim3(grid_for((int64_t)rows * dst_cols)), dim3(NT), 0, (hipStream_t)stream,
+                     src_dtype == NSTL_BF16, src, src_ld, dst_dtype == NSTL_BF16, dst, dst_ld, rows, cols, dst_cols,
+                     scale);
+  NSTL_LAUNCH_CHECK("nstl_copy2d");
+  return 0;
+}
+
+extern "C" int nstl_colsum(int dtype, const void* x, int64_t ld, int rows, int cols, float* partial, float* out,
+                           float beta, void* stream) {
+  NSTL_CHECK_ARG(x && partial && out && rows > 0 && cols > 0 && ld >= cols, "nstl_colsum: bad args");
+  const int nchunk = (rows + COLSUM_ROWS - 1) / COLSUM_ROWS;
+  dim3 grid((cols + NT - 1) / NT, nchunk);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == NSTL_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(NT), 0, st, (const bf16*)x, ld, rows, cols, partial);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(NT), 0, st, (const float*)x, ld, rows, cols, partial);
+  NSTL_LAUNCH_CHECK("nstl_colsum");
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + NT - 1) / NT), dim3(NT), 0, st, partial, nchunk, cols, out, beta);
+  NSTL_LAUNCH_CHECK("nstl_colsum reduce");
+  return 0;
+}
+
+extern "C" int nstl_reduce_rows(const float* part, int n_part, int cols, float* out, float beta, void* stream) {
+  NSTL_CHECK_ARG(part && out && n_part > 0 && cols > 0, "nstl_reduce_rows: bad args");
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + NT - 1) / NT), dim3(NT), 0, (hipStream_t)stream, part, n_part,
+                     cols, out, beta);
+  NSTL_LAUNCH_CHECK("nstl_reduce_rows");
+  return 0;
+}
+
+extern "C" int nstl_rope(int in_dtype, const void* in, int64_t in_ld, int out_dtype, void* out, int64_t out_ld,
+                         int rows, int cols, const float* cos_t, const float* sin_t, int T, int rope_dim, int inverse,
+                         int accumulate, void* stream) {
+  NSTL_CHECK_ARG(in && out && cos_t && sin_t && rows > 0 && cols > 0 && cols % 2 == 0 && rope_dim % 2 == 0 &&
+                     T > 0, "nstl_rope: bad args");
+  NSTL_CHECK_ARG(!accumulate || out_dtype == NSTL_F32, "nstl_rope: accumulate needs f32 output");
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = grid_for((int64_t)rows * cols / 2);
+#define NSTL_ROPE(TI, TO)                                                                                 \
+  hipLaunchKernelGGL((rope_kernel<TI, TO>), dim3(grid), dim3(NT), 0, st, (const TI*)in, in_ld, (TO*)out, \
+                     out_ld, rows, cols, cos_t, sin_t, T, rope_dim, inverse, accumulate)
+  if (in_dtype == NSTL_BF16 && out_dtype == NSTL_BF16) NSTL_ROPE(bf16, bf16);
+  else if (in_dtype == NSTL_BF16) NSTL_ROPE(bf16, float);
+  else if (out_dtype == NSTL_BF16) NSTL_ROPE(float, bf16);
+  else NSTL_ROPE(float, float);
+#undef NSTL_ROPE
+  NSTL_LAUNCH_CHECK("nstl_rope");
+  return 0;
+}

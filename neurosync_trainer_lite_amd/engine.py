@@ -1,0 +1,566 @@
+"""Seq2Seq training executor on MI355X: the reference forward/backward graph of
+``utils/model.py`` (Seq2Seq, :256-266) scheduled explicitly over libnstl_hip.so.
+
+Design (MI355X-first):
+  * Parameter arena.  All 344 parameters live in ONE flat f32 buffer (plus a
+    same-layout f32 gradient arena and, in bf16 mode, a bf16 shadow the GEMMs
+    read).  nn.Parameters are views into it, so ``state_dict`` keys/shapes are
+    the reference's, while q/k/v (and cross k/v) weights are contiguous and feed
+    one fused projection GEMM.  Layout order = reverse backward order, so
+    gradient buckets complete front-to-back (all-reduce overlap, parallel.py).
+  * Activations are saved in preallocated per-(B, T) workspaces (288 GB HBM:
+    ~8 GB at the 228M / 128x128 config); no allocator traffic in the step.
+  * Fusions: bias+RoPE in the q/k projection epilogue, bias+ReLU+dropout in
+    FFN1, dropout(s)+residual+LayerNorm in one kernel, ReLU/dropout backward in
+    the FFN2 dX epilogue, RoPE backward in the attention-backward store.
+  * Dropout masks are counter hashes (seed, element) regenerated in backward.
+"""
+import weakref
+
+import torch
+
+from . import _hip as K
+
+# per-layer dropout sites (distinct hash streams)
+_SITE = {"attn": 1, "resid": 2, "drop1": 3, "ffn": 4, "drop2": 5,
+         "xattn": 6, "xresid": 7, "drop2x": 8, "drop3": 9}
+
+
+def _seed(base, enc, layer, site):
+    return (base * 0x9E3779B1 + (0 if enc else 1 << 20) + layer * 64 + _SITE[site]) & 0xFFFFFFFFFFFFFFFF
+
+
+def rotation_tables(seq_len, dim, device):
+    """cos/sin [T, dim/2] f32, computed exactly as the reference does (model.py:36-42,
+    :67-73: float32 position * exp(-ln(10000) * 2i / dim)) then moved to the device."""
+    position = torch.arange(seq_len, dtype=torch.float32).unsqueeze(1)
+    two_i = torch.arange(0, dim, 2, dtype=torch.float32)
+    inv_freq = torch.exp(-torch.log(torch.tensor(10000.0)) * two_i / dim)
+    angle = position * inv_freq
+    return torch.cos(angle).contiguous().to(device), torch.sin(angle).contiguous().to(device)
+
+
+def _pad64(n):
+    return (n + 63) // 64 * 64
+
+
+class _Buffers:
+    """Activation workspace for one (B, T, save) shape."""
+
+    def __init__(self, eng, B, T, save):
+        dev, dt = eng.device, eng.dt
+        D, Fd, L = eng.D, eng.Fd, eng.L
+        M = B * T
+        nl = L if save else 1
+        e = lambda *s, dtype=dt: torch.empty(*s, dtype=dtype, device=dev)
+        self.B, self.T, self.M = B, T, M
+        self.src = e(M, eng.in_dim)
+        self.x0 = e(M, D)
+        # encoder
+        self.e_qkv = [e(M, 3 * D) for _ in range(nl)]
+        self.e_o = [e(M, D) for _ in range(nl)]
+        self.e_lse = [e(B * eng.H * T, dtype=torch.float32) for _ in range(nl)]
+        self.e_s1 = [e(M, D) for _ in range(nl)]
+        self.e_x1 = [e(M, D) for _ in range(nl)]
+        self.e_h = [e(M, Fd) for _ in range(nl)]
+        self.e_s2 = [e(M, D) for _ in range(nl)]
+        self.e_x2 = [e(M, D) for _ in range(nl)]
+        self.e_stats = [e(4, M, dtype=torch.float32) for _ in range(nl)]  # mean1 rstd1 mean2 rstd2
+        self.mem = e(M, D)
+        self.xdec0 = e(M, D)
+        self.encf_stats = e(2, M, dtype=torch.float32)
+        # decoder
+        self.d_qkv = [e(M, 3 * D) for _ in range(nl)]
+        self.d_o = [e(M, D) for _ in range(nl)]
+        self.d_lse = [e(B * eng.H * T, dtype=torch.float32) for _ in range(nl)]
+        self.d_s1 = [e(M, D) for _ in range(nl)]
+        self.d_x1 = [e(M, D) for _ in range(nl)]
+        self.d_qc = [e(M, D) for _ in range(nl)]
+        self.d_kvc = [e(M, 2 * D) for _ in range(nl)]
+        self.d_oc = [e(M, D) for _ in range(nl)]
+        self.d_lsec = [e(B * eng.H * T, dtype=torch.float32) for _ in range(nl)]
+        self.d_s2 = [e(M, D) for _ in range(nl)]
+        self.d_x2 = [e(M, D) for _ in range(nl)]
+        self.d_h = [e(M, Fd) for _ in range(nl)]
+        self.d_s3 = [e(M, D) for _ in range(nl)]
+        self.d_x3 = [e(M, D) for _ in range(nl)]
+        self.d_stats = [e(6, M, dtype=torch.float32) for _ in range(nl)]
+        self.xf = e(M, D)
+        self.decf_stats = e(2, M, dtype=torch.float32)
+        self.y = e(M, D)  # branch scratch (out_linear / FFN2 outputs)
+        self.save = save
+        if save:
+            f32 = torch.float32
+            self.dres = e(M, D, dtype=f32)
+            self.dmem = e(M, D, dtype=f32)
+            self.dy = e(M, D)
+            self.dattn = e(M, D)
+            self.dqkv = e(M, 3 * D)
+            self.dq = e(M, D)
+            self.dkv = e(M, 2 * D)
+            self.dh = e(M, Fd)
+            self.demb = e(M, D)
+            self.dpred = torch.zeros(M, 64, dtype=dt, device=dev)
+            self.n_part = max(1, min(256, M // 4))
+            self.ln_part = e(2, self.n_part, D, dtype=f32)
+            self.col_part = e((M + 255) // 256, max(Fd, 3 * D, 64), dtype=f32)
+            self.ws = e(eng.splitk_ws_elems(M), dtype=f32)
+
+    def layer(self, lst, l):
+        return lst[l if self.save else 0]
+
+
+class Seq2SeqEngine:
+    """Owns the parameter/gradient arenas of one Seq2Seq module and runs it."""
+
+    def __init__(self, model, device, compute_dtype):
+        self.model = model
+        self.device = torch.device(device)
+        self.dt = compute_dtype
+        enc, dec = model.encoder, model.decoder
+        self.D = enc.embedding.out_features
+        self.in_dim = enc.embedding.in_features
+        self.out_dim = dec.fc_output.out_features
+        self.L = len(enc.transformer_encoder)
+        self.H = enc.transformer_encoder[0].self_attn.num_heads
+        self.Fd = enc.transformer_encoder[0].ffn.linear1.out_features
+        self.dropout = model.dropout_p
+        self._check_shapes()
+        self._build_arena()
+        self._bufs = {}
+        self._rope = {}
+        self.generation = 0
+        self.grads_fresh = True
+        self.grad_reducer = None   # parallel.GradAllReducer when data-parallel
+        self.grad_scale_t = None   # device f32 [1]: loss-gradient pre-scale (1/world)
+
+    # ------------------------------------------------------------------ setup
+    def _check_shapes(self):
+        D, H = self.D, self.H
+        if D % H or D // H != 64:
+            raise ValueError("MI355X kernels need head_dim == 64 (hidden_dim=%d, num_heads=%d)" % (D, H))
+        if D % 128 or D > 1024:
+            raise ValueError("hidden_dim must be a multiple of 128 and <= 1024 (got %d)" % D)
+        if self.out_dim > 64:
+            raise ValueError("output_dim must be <= 64 (got %d)" % self.out_dim)
+        if self.in_dim % 8:
+            raise ValueError("input_dim must be a multiple of 8 (got %d)" % self.in_dim)
+
+    def _arena_order(self):
+        """Parameter names in arena order (reverse of backward completion)."""
+        L = self.L
+        order = ["decoder.fc_output.weight", "decoder.fc_output.bias",
+                 "decoder.layer_norm.weight", "decoder.layer_norm.bias"]
+        for l in reversed(range(L)):
+            b = "decoder.transformer_decoder.%d." % l
+            for n in ("norm3", "norm2", "norm1"):
+                order += [b + n + ".weight", b + n + ".bias"]
+            order += [b + "ffn.linear2.weight", b + "ffn.linear2.bias", b + "ffn.linear1.weight", b + "ffn.linear1.bias"]
+            m = b + "multihead_attn."
+            order += [m + "out_linear.weight", m + "out_linear.bias", m + "q_linear.weight", m + "q_linear.bias",
+                      m + "k_linear.weight", m + "v_linear.weight", m + "k_linear.bias", m + "v_linear.bias"]
+            s = b + "self_attn."
+            order += [s + "out_linear.weight", s + "out_linear.bias",
+                      s + "q_linear.weight", s + "k_linear.weight", s + "v_linear.weight",
+                      s + "q_linear.bias", s + "k_linear.bias", s + "v_linear.bias"]
+        order += ["encoder.layer_norm.weight", "encoder.layer_norm.bias"]
+        for l in reversed(range(L)):
+            b = "encoder.transformer_encoder.%d." % l
+            for n in ("norm2", "norm1"):
+                order += [b + n + ".weight", b + n + ".bias"]
+            order += [b + "ffn.linear2.weight", b + "ffn.linear2.bias", b + "ffn.linear1.weight", b + "ffn.linear1.bias"]
+            s = b + "self_attn."
+            order += [s + "out_linear.weight", s + "out_linear.bias",
+                      s + "q_linear.weight", s + "k_linear.weight", s + "v_linear.weight",
+                      s + "q_linear.bias", s + "k_linear.bias", s + "v_linear.bias"]
+        order += ["encoder.embedding.weight", "encoder.embedding.bias"]
+        return order
+
+    def _build_arena(self):
+        named = dict(self.model.named_parameters())
+        order = self._arena_order()
+        if sorted(order) != sorted(named):
+            raise RuntimeError("unexpected parameter set: %s" % sorted(set(order) ^ set(named)))
+        self.offsets = {}
+        off = 0
+        for n in order:
+            k = named[n].numel()
+            self.offsets[n] = (off, k, tuple(named[n].shape))
+            off += _pad64(k)
+        self.numel = off
+        self.end_of = {n: o + _pad64(k) for n, (o, k, _) in self.offsets.items()}
+        dev = self.device
+        self.p32 = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.g32 = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.p16 = torch.zeros(off, dtype=self.dt, device=dev) if self.dt != torch.float32 else self.p32
+        with torch.no_grad():
+            for n in order:
+                o, k, shp = self.offsets[n]
+                self.p32[o:o + k].view(shp).copy_(named[n].detach().to(dev))
+        self._params = [(n, named[n]) for n in order]
+        self._rebind()
+        self.refresh_shadow()
+
+    def _rebind(self):
+        me = weakref.ref(self)
+        for n, p in self._params:
+            o, k, shp = self.offsets[n]
+            p.data = self.p32[o:o + k].view(shp)
+            p.grad = self.g32[o:o + k].view(shp)
+            p._nstl_engine = me
+        self.name_of = {id(p): n for n, p in self._params}
+        self._first_ptr = self._params[0][1].data_ptr()
+
+    def ensure_bound(self):
+        """Re-pack if someone replaced parameter storage (e.g. model.to())."""
+        p0 = self._params[0][1]
+        if p0.data_ptr() != self._first_ptr or p0.device != self.device:
+            with torch.no_grad():
+                for n, p in self._params:
+                    o, k, shp = self.offsets[n]
+                    self.p32[o:o + k].view(shp).copy_(p.detach().to(self.device))
+            self._rebind()
+            self.refresh_shadow()
+        gbase = self.g32.data_ptr()
+        for n, p in self._params:
+            o, k, shp = self.offsets[n]
+            if p.grad is None or p.grad.data_ptr() != gbase + 4 * o:
+                p.grad = self.g32[o:o + k].view(shp)
+                self.grads_fresh = True
+        if any(p._version != self._versions.get(n, -1) for n, p in self._params):
+            self.refresh_shadow()
+
+    def refresh_shadow(self):
+        if self.p16 is not self.p32:
+            K.cast(self.p32, self.p16, stream=K.stream_of(self.device))
+        self._versions = {n: p._version for n, p in self._params}
+
+    def zero_grad(self):
+        """Next backward overwrites the gradient arena instead of accumulating."""
+        self.grads_fresh = True
+
+    # views ----------------------------------------------------------------
+    def w(self, name, rows=1):
+        """Compute-dtype view of `rows` consecutive weight matrices starting at `name`."""
+        o, k, shp = self.offsets[name]
+        return self.p16[o:o + k * rows].view(shp[0] * rows, *shp[1:])
+
+    def b(self, name, rows=1):
+        o, k, _ = self.offsets[name]
+        return self.p32[o:o + k * rows]
+
+    def gw(self, name, rows=1):
+        o, k, shp = self.offsets[name]
+        return self.g32[o:o + k * rows].view(shp[0] * rows, *shp[1:])
+
+    def gb(self, name, rows=1):
+        o, k, _ = self.offsets[name]
+        return self.g32[o:o + k * rows]
+
+    def rope(self, T, dim):
+        key = (T, dim)
+        if key not in self._rope:
+            self._rope[key] = rotation_tables(T, dim, self.device)
+        return self._rope[key]
+
+    def bufs(self, B, T, save):
+        key = (B, T, save)
+        if key not in self._bufs:
+            if save:  # keep at most one training workspace alive
+                for k2 in [k for k in self._bufs if k[2]]:
+                    del self._bufs[k2]
+            self._bufs[key] = _Buffers(self, B, T, save)
+        return self._bufs[key]
+
+    def splitk_ws_elems(self, M):
+        best = 0
+        for n, k in ((self.D, self.D), (3 * self.D, self.D), (self.Fd, self.D), (self.D, self.Fd),
+                     (2 * self.D, self.D), (self.D, self.in_dim), (self.out_dim, self.D)):
+            best = max(best, self.splits(n, k, M) * n * k)
+        return max(best, 1)
+
+    @staticmethod
+    def splits(n, k, m):
+        tiles = ((n + 127) // 128) * ((k + 127) // 128)
+        s = max(1, min(16, 512 // max(1, tiles)))
+        while s > 1 and m // s < 1024:
+            s //= 2
+        return s
+
+    # ------------------------------------------------------------ primitives
+    def _gemm_fwd(self, x, wname, out, epi, rows=1, rope=None, rope_cols=0, p_drop=0.0, seed=0):
+        W = self.w(wname, rows)
+        bias = self.b(wname.replace(".weight", ".bias"), rows)
+        K.gemm(x, W, out, x.shape[0], W.shape[0], W.shape[1], epilogue=epi, bias=bias, rope=rope,
+               rope_cols=rope_cols, p_drop=p_drop, seed=seed, stream=self.st)
+
+    def _dw(self, dy, x, wname, rows, bf, ws):
+        """grad(W) (+)= dy^T x ; grad(b) (+)= colsum(dy)."""
+        G = self.gw(wname, rows)
+        n, k = G.shape
+        m = dy.shape[0]
+        s = self.splits(n, k, m)
+        K.gemm(dy, x, G, n, k, m, a_kmajor=False, b_kmajor=False, beta=bf, split_k=s, workspace=ws, stream=self.st)
+        bname = wname.replace(".weight", ".bias")
+        K.colsum(dy, dy.stride(0), m, n, self.cur.col_part, self.gb(bname, rows), bf, stream=self.st)
+
+    def _dx(self, dy, wname, rows, out, beta, epi=K.EPI_NONE, aux=None, p_drop=0.0):
+        """out (+)= dy W  (W: [N][K] read as [r][j])."""
+        W = self.w(wname, rows)
+        n, k = W.shape
+        K.gemm(dy, W, out, dy.shape[0], k, n, a_kmajor=True, b_kmajor=False, beta=beta, epilogue=epi, aux=aux,
+               ld_aux=aux.stride(0) if aux is not None else 0, p_drop=p_drop, stream=self.st)
+
+    def _ln(self, x, y, out, stats, prefix, n_masks, seeds, s_out, rot=None, T=None):
+        a = K.LnArgs()
+        a.dtype = K.dtype_code(self.dt)
+        a.rows, a.D = out.shape[0], self.D
+        a.x, a.y = K.ptr(x), K.ptr(y)
+        a.n_masks, a.p_drop = n_masks, self.p
+        a.seed1, a.seed2 = seeds
+        a.gamma, a.beta, a.eps = self.b(prefix + ".weight").data_ptr(), self.b(prefix + ".bias").data_ptr(), 1e-5
+        a.s_out, a.out, a.mean, a.rstd = K.ptr(s_out), out.data_ptr(), stats[0].data_ptr(), stats[1].data_ptr()
+        if rot is not None:
+            cs, sn = self.rope(T, self.D)
+            a.rot_out, a.rope_cos, a.rope_sin, a.rope_T = rot.data_ptr(), cs.data_ptr(), sn.data_ptr(), T
+        K.ln_fwd(a, stream=self.st)
+
+    def _ln_bwd(self, s_in, stats, prefix, dres_in, dres_out, dbranch, n_masks, seeds, bf):
+        bb = self.cur
+        a = K.LnArgs()
+        a.dtype = K.dtype_code(self.dt)
+        a.rows, a.D = s_in.shape[0], self.D
+        a.n_masks, a.p_drop = n_masks, self.p
+        a.seed1, a.seed2 = seeds
+        a.gamma, a.beta, a.eps = self.b(prefix + ".weight").data_ptr(), self.b(prefix + ".bias").data_ptr(), 1e-5
+        a.mean, a.rstd = stats[0].data_ptr(), stats[1].data_ptr()
+        a.s_in, a.dout, a.ds, a.dbranch = s_in.data_ptr(), dres_in.data_ptr(), dres_out.data_ptr(), K.ptr(dbranch)
+        a.dgamma_part, a.dbeta_part, a.n_part = bb.ln_part[0].data_ptr(), bb.ln_part[1].data_ptr(), bb.n_part
+        K.ln_bwd(a, stream=self.st)
+        K.reduce_rows(bb.ln_part[0], bb.n_part, self.D, self.gb(prefix + ".weight"), bf, stream=self.st)
+        K.reduce_rows(bb.ln_part[1], bb.n_part, self.D, self.gb(prefix + ".bias"), bf, stream=self.st)
+
+    def _attn(self, q, k, v, o, lse, seed, T, B):
+        a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
+                        v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed)
+        K.attn_fwd(a, stream=self.st)
+
+    def _attn_bwd(self, q, k, v, o, lse, do, dq, dk, dv, seed, T, B):
+        a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
+                        v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed)
+        a.dout, a.dout_ld = do.data_ptr(), do.stride(0)
+        a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dq.data_ptr(), dq.stride(0), dk.data_ptr(), dk.stride(0),
+                                                        dv.data_ptr(), dv.stride(0))
+        cs, sn = self.rope(T, 64)
+        a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
+        K.attn_bwd(a, stream=self.st)
+
+    # --------------------------------------------------------------- forward
+    def _enc_layer(self, bb, l, x, T):
+        D, B = self.D, bb.B
+        pre = "encoder.transformer_encoder.%d." % l
+        sd = lambda s: _seed(self.base_seed, True, l, s)
+        qkv, o, lse = bb.layer(bb.e_qkv, l), bb.layer(bb.e_o, l), bb.layer(bb.e_lse, l)
+        self._gemm_fwd(x, pre + "self_attn.q_linear.weight", qkv, K.EPI_BIAS_ROPE, rows=3,
+                       rope=(*self.rope(T, 64), T, 64), rope_cols=2 * D)
+        self._attn(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, sd("attn"), T, B)
+        self._gemm_fwd(o, pre + "self_attn.out_linear.weight", bb.y, K.EPI_BIAS)
+        st = bb.layer(bb.e_stats, l)
+        x1 = bb.layer(bb.e_x1, l)
+        self._ln(x, bb.y, x1, st[0:2], pre + "norm1", 2, (sd("resid"), sd("drop1")), bb.layer(bb.e_s1, l))
+        h = bb.layer(bb.e_h, l)
+        self._gemm_fwd(x1, pre + "ffn.linear1.weight", h, K.EPI_BIAS_RELU_DROP, p_drop=self.p, seed=sd("ffn"))
+        self._gemm_fwd(h, pre + "ffn.linear2.weight", bb.y, K.EPI_BIAS)
+        x2 = bb.layer(bb.e_x2, l)
+        self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 1, (sd("drop2"), 0), bb.layer(bb.e_s2, l))
+        return x2
+
+    def _dec_layer(self, bb, l, x, mem, T):
+        D, B = self.D, bb.B
+        pre = "decoder.transformer_decoder.%d." % l
+        sd = lambda s: _seed(self.base_seed, False, l, s)
+        L_ = lambda lst: bb.layer(lst, l)
+        st = L_(bb.d_stats)
+        qkv = L_(bb.d_qkv)
+        self._gemm_fwd(x, pre + "self_attn.q_linear.weight", qkv, K.EPI_BIAS_ROPE, rows=3,
+                       rope=(*self.rope(T, 64), T, 64), rope_cols=2 * D)
+        self._attn(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], L_(bb.d_o), L_(bb.d_lse), sd("attn"), T, B)
+        self._gemm_fwd(L_(bb.d_o), pre + "self_attn.out_linear.weight", bb.y, K.EPI_BIAS)
+        x1 = L_(bb.d_x1)
+        self._ln(x, bb.y, x1, st[0:2], pre + "norm1", 2, (sd("resid"), sd("drop1")), L_(bb.d_s1))
+        qc, kvc = L_(bb.d_qc), L_(bb.d_kvc)
+        self._gemm_fwd(x1, pre + "multihead_attn.q_linear.weight", qc, K.EPI_BIAS_ROPE,
+                       rope=(*self.rope(T, 64), T, 64), rope_cols=D)
+        self._gemm_fwd(mem, pre + "multihead_attn.k_linear.weight", kvc, K.EPI_BIAS_ROPE, rows=2,
+                       rope=(*self.rope(T, 64), T, 64), rope_cols=D)
+        self._attn(qc, kvc[:, :D], kvc[:, D:], L_(bb.d_oc), L_(bb.d_lsec), sd("xattn"), T, B)
+        self._gemm_fwd(L_(bb.d_oc), pre + "multihead_attn.out_linear.weight", bb.y, K.EPI_BIAS)
+        x2 = L_(bb.d_x2)
+        self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 2, (sd("xresid"), sd("drop2x")), L_(bb.d_s2))
+        h = L_(bb.d_h)
+        self._gemm_fwd(x2, pre + "ffn.linear1.weight", h, K.EPI_BIAS_RELU_DROP, p_drop=self.p, seed=sd("ffn"))
+        self._gemm_fwd(h, pre + "ffn.linear2.weight", bb.y, K.EPI_BIAS)
+        x3 = L_(bb.d_x3)
+        self._ln(x2, bb.y, x3, st[4:6], pre + "norm3", 1, (sd("drop3"), 0), L_(bb.d_s3))
+        return x3
+
+    def _prologue(self, training):
+        self.ensure_bound()
+        self.st = K.stream_of(self.device)
+        self.p = float(self.dropout) if training else 0.0
+
+    def encode(self, bb, src, T):
+        """Encoder forward; returns the encoder output `mem` (compute dtype)."""
+        M = bb.M
+        if self.dt == torch.float32 and src.is_contiguous():
+            x_src = src.view(M, self.in_dim)
+        else:
+            K.copy2d(src.reshape(M, self.in_dim), self.in_dim, bb.src, self.in_dim, M, self.in_dim, self.in_dim,
+                     stream=self.st)
+            x_src = bb.src
+        self._gemm_fwd(x_src, "encoder.embedding.weight", bb.x0, K.EPI_BIAS_ROPE,
+                       rope=(*self.rope(T, self.D), T, self.D), rope_cols=self.D)
+        self.x_src = x_src
+        x = bb.x0
+        for l in range(self.L):
+            x = self._enc_layer(bb, l, x, T)
+        self._ln(None, x, bb.mem, bb.encf_stats, "encoder.layer_norm", 0, (0, 0), None, rot=bb.xdec0, T=T)
+        return bb.mem
+
+    def decode(self, bb, mem, T, xdec0=None):
+        """Decoder forward from `mem`; returns pred f32 [M, 64] (first out_dim valid)."""
+        if xdec0 is None:
+            K.rope(mem, self.D, bb.xdec0, self.D, bb.M, self.D, *self.rope(T, self.D), T, self.D, stream=self.st)
+            xdec0 = bb.xdec0
+        x = xdec0
+        for l in range(self.L):
+            x = self._dec_layer(bb, l, x, mem, T)
+        self._ln(None, x, bb.xf, bb.decf_stats, "decoder.layer_norm", 0, (0, 0), None)
+        pred = torch.empty(bb.M, 64, dtype=torch.float32, device=self.device)
+        self._gemm_fwd(bb.xf, "decoder.fc_output.weight", pred, K.EPI_BIAS)
+        return pred
+
+    def forward(self, src, training, save):
+        B, T, _ = src.shape
+        self._prologue(training)
+        self.base_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self.p > 0 else 0
+        bb = self.bufs(B, T, save)
+        mem = self.encode(bb, src, T)
+        pred = self.decode(bb, mem, T, xdec0=bb.xdec0)
+        if save:
+            self.generation += 1
+            self.saved = dict(bb=bb, T=T, p=self.p, seed=self.base_seed, gen=self.generation, x_src=self.x_src)
+        return pred[:, :self.out_dim].view(B, T, self.out_dim)
+
+    # -------------------------------------------------------------- backward
+    def backward(self, grad_pred, gen):
+        sv = self.saved
+        if gen != sv["gen"]:
+            raise RuntimeError("Seq2Seq forward was run again before backward of an earlier forward")
+        bb, T = sv["bb"], sv["T"]
+        self.ensure_bound()
+        self.cur = bb
+        self.st = K.stream_of(self.device)
+        self.p, self.base_seed = sv["p"], sv["seed"]
+        bf = 0.0 if self.grads_fresh else 1.0
+        M, D, L = bb.M, self.D, self.L
+        ws = bb.ws
+        dres = bb.dres
+        # head: pred = xf W^T + b
+        g = grad_pred.reshape(M, self.out_dim)
+        K.copy2d(g, g.stride(0), bb.dpred, 64, M, self.out_dim, 64, scale=self.grad_scale_t, stream=self.st)
+        red = self.grad_reducer
+        ready = (lambda name: red.ready(self.end_of[name])) if red is not None else (lambda name: None)
+        dpred = bb.dpred[:, :self.out_dim]
+        self._dw(dpred, bb.xf, "decoder.fc_output.weight", 1, bf, ws)
+        K.gemm(bb.dpred, self.w("decoder.fc_output.weight"), dres, M, D, self.out_dim, a_kmajor=True,
+               b_kmajor=False, lda=64, beta=0.0, stream=self.st)
+        x_last = bb.layer(bb.d_x3, L - 1)
+        self._ln_bwd(x_last, bb.decf_stats, "decoder.layer_norm", dres, dres, None, 0, (0, 0), bf)
+        ready("decoder.layer_norm.bias")
+        for l in reversed(range(L)):
+            self._dec_layer_bwd(bb, l, T, bf, first=(l == L - 1))
+            ready("decoder.transformer_decoder.%d.self_attn.v_linear.bias" % l)
+        # decoder input x = GPE(mem): dmem += GPE^T(dres)
+        cs, sn = self.rope(T, D)
+        K.rope(dres, D, bb.dmem, D, M, D, cs, sn, T, D, inverse=True, accumulate=True, stream=self.st)
+        x_last = bb.layer(bb.e_x2, L - 1)
+        self._ln_bwd(x_last, bb.encf_stats, "encoder.layer_norm", bb.dmem, dres, None, 0, (0, 0), bf)
+        ready("encoder.layer_norm.bias")
+        for l in reversed(range(L)):
+            self._enc_layer_bwd(bb, l, T, bf)
+            ready("encoder.transformer_encoder.%d.self_attn.v_linear.bias" % l)
+        # embedding + global PE: x0 = GPE(src W^T + b)
+        K.rope(dres, D, bb.demb, D, M, D, cs, sn, T, D, inverse=True, stream=self.st)
+        self._dw(bb.demb, sv["x_src"], "encoder.embedding.weight", 1, bf, ws)
+        if red is not None:
+            red.finish()
+        self.grads_fresh = False
+
+    def _attn_block_bwd(self, bb, pre, x_in, qkv, o, lse, st, s1, norm, seeds, T, bf):
+        """Backward through x1 = LN(x_in + drop(drop(out_linear(attn(x_in))))) (self-attention)."""
+        D, ws = self.D, bb.ws
+        self._ln_bwd(s1, st, pre + norm, bb.dres, bb.dres, bb.dy, 2, seeds[0:2], bf)
+        self._dw(bb.dy, o, pre + "self_attn.out_linear.weight", 1, bf, ws)
+        self._dx(bb.dy, pre + "self_attn.out_linear.weight", 1, bb.dattn, 0.0)
+        self._attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, bb.dattn,
+                       bb.dqkv[:, :D], bb.dqkv[:, D:2 * D], bb.dqkv[:, 2 * D:], seeds[2], T, bb.B)
+        self._dw(bb.dqkv, x_in, pre + "self_attn.q_linear.weight", 3, bf, ws)
+        self._dx(bb.dqkv, pre + "self_attn.q_linear.weight", 3, bb.dres, 1.0)
+
+    def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf):
+        """Backward through x_out = LN(x_in + drop(FFN(x_in)))."""
+        ws = self.cur.ws
+        self._ln_bwd(s_out, st, pre + norm, bb.dres, bb.dres, bb.dy, 1, (seed_drop, 0), bf)
+        self._dw(bb.dy, h, pre + "ffn.linear2.weight", 1, bf, ws)
+        self._dx(bb.dy, pre + "ffn.linear2.weight", 1, bb.dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p)
+        self._dw(bb.dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws)
+        self._dx(bb.dh, pre + "ffn.linear1.weight", 1, bb.dres, 1.0)
+
+    def _enc_layer_bwd(self, bb, l, T, bf):
+        pre = "encoder.transformer_encoder.%d." % l
+        sd = lambda s: _seed(self.base_seed, True, l, s)
+        st = bb.e_stats[l]
+        x_in = bb.x0 if l == 0 else bb.e_x2[l - 1]
+        self._ffn_bwd(bb, pre, bb.e_x1[l], bb.e_h[l], bb.e_s2[l], st[2:4], "norm2", sd("drop2"), bf)
+        self._attn_block_bwd(bb, pre, x_in, bb.e_qkv[l], bb.e_o[l], bb.e_lse[l], st[0:2], bb.e_s1[l], "norm1",
+                             (sd("resid"), sd("drop1"), sd("attn")), T, bf)
+
+    def _dec_layer_bwd(self, bb, l, T, bf, first):
+        D, ws = self.D, bb.ws
+        pre = "decoder.transformer_decoder.%d." % l
+        sd = lambda s: _seed(self.base_seed, False, l, s)
+        st = bb.d_stats[l]
+        x_in = bb.xdec0 if l == 0 else bb.d_x3[l - 1]
+        self._ffn_bwd(bb, pre, bb.d_x2[l], bb.d_h[l], bb.d_s3[l], st[4:6], "norm3", sd("drop3"), bf)
+        # cross attention block: x2 = LN(x1 + drop(drop(out(attn(q(x1), kv(mem))))))
+        self._ln_bwd(bb.d_s2[l], st[2:4], pre + "norm2", bb.dres, bb.dres, bb.dy, 2, (sd("xresid"), sd("drop2x")), bf)
+        m = pre + "multihead_attn."
+        self._dw(bb.dy, bb.d_oc[l], m + "out_linear.weight", 1, bf, ws)
+        self._dx(bb.dy, m + "out_linear.weight", 1, bb.dattn, 0.0)
+        kvc = bb.d_kvc[l]
+        self._attn_bwd(bb.d_qc[l], kvc[:, :D], kvc[:, D:], bb.d_oc[l], bb.d_lsec[l], bb.dattn,
+                       bb.dq, bb.dkv[:, :D], bb.dkv[:, D:], sd("xattn"), T, bb.B)
+        self._dw(bb.dq, bb.d_x1[l], m + "q_linear.weight", 1, bf, ws)
+        self._dx(bb.dq, m + "q_linear.weight", 1, bb.dres, 1.0)
+        self._dw(bb.dkv, bb.mem, m + "k_linear.weight", 2, bf, ws)
+        self._dx(bb.dkv, m + "k_linear.weight", 2, bb.dmem, 0.0 if first else 1.0)
+        self._attn_block_bwd(bb, pre, x_in, bb.d_qkv[l], bb.d_o[l], bb.d_lse[l], st[0:2], bb.d_s1[l], "norm1",
+                             (sd("resid"), sd("drop1"), sd("attn")), T, bf)
+
+
+class Seq2SeqFunction(torch.autograd.Function):
+    """Autograd node for the whole Seq2Seq: forward saves activations in the
+    engine workspace; backward writes parameter gradients into the arena."""
+
+    @staticmethod
+    def forward(ctx, src, anchor, engine, training):
+        pred = engine.forward(src, training, save=True)
+        ctx.engine = engine
+        ctx.gen = engine.generation
+        return pred
+
+    @staticmethod
+    def backward(ctx, grad_pred):
+        ctx.engine.backward(grad_pred, ctx.gen)
+        return None, None, None, None

@@ -1,0 +1,141 @@
+"""Fused Adam (coupled L2) + global-norm clip over the engine's flat parameter arena.
+
+Drop-in for ``torch.optim.Adam(model.parameters(), lr, weight_decay)`` as built at
+/root/reference/utils/model_utils.py:11, including the state_dict format
+({'state': {i: {'step', 'exp_avg', 'exp_avg_sq'}}, 'param_groups': [...]}) so
+reference checkpoints load and ours load into torch.optim.Adam.  One
+``nstl_sumsq`` + one ``nstl_adam_step`` launch replace clip_grad_norm_'s
+per-tensor norms and Adam's ~5 foreach passes (training_utils.py:73-74), and the
+norm stays on the device (the reference syncs 344 ``.item()``s per step).
+"""
+import torch
+
+from .. import _hip as K
+
+N_PARTIAL = 1024
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False, *,
+                 foreach=None, maximize=False, capturable=False, differentiable=False, fused=None,
+                 decoupled_weight_decay=False):
+        if amsgrad or maximize or decoupled_weight_decay:
+            raise NotImplementedError("amsgrad/maximize/decoupled_weight_decay are not used by the reference")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad, maximize=maximize,
+                        foreach=foreach, capturable=capturable, differentiable=differentiable, fused=fused,
+                        decoupled_weight_decay=decoupled_weight_decay)
+        super().__init__(params, defaults)
+        if len(self.param_groups) != 1:
+            raise NotImplementedError("FusedAdam supports one parameter group (as the reference uses)")
+        self._engine = None
+        self._nstl_step = 0
+        self.last_norm = None
+
+    # --------------------------------------------------------------- arena
+    def _bind(self):
+        params = self.param_groups[0]["params"]
+        if self._engine is None:
+            from ..engine import Seq2SeqEngine  # noqa: F401
+            eng = _find_engine(params)
+            if eng is None:
+                raise RuntimeError("FusedAdam needs the parameters of a Seq2Seq whose engine is built "
+                                   "(run one forward first, or build_model on a GPU)")
+            names = {id(p): n for n, p in eng._params}
+            if set(names) != {id(p) for p in params}:
+                raise RuntimeError("FusedAdam must own exactly the Seq2Seq parameters")
+            self._engine = eng
+            self.m = torch.zeros_like(eng.p32)
+            self.v = torch.zeros_like(eng.p32)
+            self.partial = torch.empty(N_PARTIAL, dtype=torch.float32, device=eng.device)
+            self.norm = torch.zeros(1, dtype=torch.float32, device=eng.device)
+            for p in params:
+                old = self.state.get(p, {})
+                views = self._state_views(p)
+                if "exp_avg" in old:  # state loaded before the arena existed
+                    views["exp_avg"].copy_(old["exp_avg"].to(eng.device))
+                    views["exp_avg_sq"].copy_(old["exp_avg_sq"].to(eng.device))
+                self.state[p] = views
+        return self._engine
+
+    def _state_views(self, p):
+        eng = self._engine
+        o, k, shp = eng.offsets[eng.name_of[id(p)]]
+        return {"step": torch.tensor(float(self._nstl_step)), "exp_avg": self.m[o:o + k].view(shp),
+                "exp_avg_sq": self.v[o:o + k].view(shp)}
+
+    # ---------------------------------------------------------------- step
+    @torch.no_grad()
+    def step(self, closure=None, max_norm=None):
+        """One Adam step; with ``max_norm`` the global-norm clip (clip_grad_norm_)
+        is fused in front.  Returns the loss of ``closure`` (torch semantics)."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        eng = self._bind()
+        eng.ensure_bound()
+        g = self.param_groups[0]
+        self._nstl_step += 1
+        st = K.stream_of(eng.device)
+        a = K.AdamArgs()
+        a.p, a.g, a.m, a.v = eng.p32.data_ptr(), eng.g32.data_ptr(), self.m.data_ptr(), self.v.data_ptr()
+        if eng.p16 is not eng.p32:
+            a.p_lowp, a.lowp_dtype = eng.p16.data_ptr(), K.dtype_code(eng.p16.dtype)
+        a.n = eng.numel
+        a.lr, a.eps, a.weight_decay = g["lr"], g["eps"], g["weight_decay"]
+        a.beta1, a.beta2 = g["betas"]
+        a.step = self._nstl_step
+        if max_norm is not None:
+            K.sumsq(eng.g32, eng.numel, self.partial, N_PARTIAL, stream=st)
+            a.sumsq_partial, a.n_partial, a.max_norm = self.partial.data_ptr(), N_PARTIAL, float(max_norm)
+            a.norm_out = self.norm.data_ptr()
+            self.last_norm = self.norm
+        K.adam_step(a, stream=st)
+        return loss
+
+    def zero_grad(self, set_to_none=True):
+        """The next backward overwrites the gradient arena (no memset; p.grad stays
+        a view of the arena rather than becoming None)."""
+        eng = self._engine if self._engine is not None else _find_engine(self.param_groups[0]["params"])
+        if eng is not None:
+            eng.zero_grad()
+        else:
+            super().zero_grad(set_to_none)
+
+    # ------------------------------------------------------------ state io
+    def state_dict(self):
+        if self._engine is not None:
+            for p in self.param_groups[0]["params"]:
+                self.state[p]["step"] = torch.tensor(float(self._nstl_step))
+        sd = super().state_dict()
+        for s in sd["state"].values():
+            for k, v in list(s.items()):
+                if torch.is_tensor(v) and k != "step":
+                    s[k] = v.clone()
+        return sd
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        params = self.param_groups[0]["params"]
+        loaded = {p: dict(self.state[p]) for p in params if p in self.state}
+        steps = [float(s["step"]) for s in loaded.values() if "step" in s]
+        self._nstl_step = int(max(steps)) if steps else 0
+        if self._engine is None and _find_engine(params) is None:
+            return  # engine not built yet: keep torch-style state; bound on first step
+        eng = self._bind()
+        with torch.no_grad():
+            for p in params:
+                views = self._state_views(p)
+                if p in loaded and "exp_avg" in loaded[p]:
+                    views["exp_avg"].copy_(loaded[p]["exp_avg"].to(eng.device))
+                    views["exp_avg_sq"].copy_(loaded[p]["exp_avg_sq"].to(eng.device))
+                self.state[p] = views
+
+
+def _find_engine(params):
+    for p in params:
+        eng = getattr(p, "_nstl_engine", None)
+        if eng is not None:
+            return eng()
+    return None
+

@@ -214,6 +214,7 @@ class OracleTrainer:
         loss = loss_fn(pred, trg, *self.loss_args)
         loss.backward()
         grads = [self.p[k].grad for k in self.keys]
+        self.last_grads = {k: self.p[k].grad.detach().clone() for k in self.keys}
         with torch.no_grad():
             total = clip_grad_norm(grads, self.clip)
             self.step_count += 1
