@@ -30,6 +30,10 @@ BF16_DENSE_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (MI355X_M
 PEAK_HBM_GBS = 8000.0
 
 
+def log(msg):
+    print("[bench] " + msg, file=sys.stderr, flush=True)
+
+
 def frames_flops(W, T, D, n_attn=24):
     """Algorithmic train FLOPs per frame: 6W + 12*T*D*24."""
     return 6 * W + 12 * T * D * n_attn
@@ -38,7 +42,11 @@ def frames_flops(W, T, D, n_attn=24):
 def cpu_baseline(cfg, T, budget_s=25.0):
     """fp32 oracle step (reference semantics) on the host cores, bounded sample."""
     from oracle import model_ref
+    # the GPU box's affinity mask shows the whole machine; the job's CPU share is
+    # what OMP_NUM_THREADS says there (16)
     cores = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(cores)
     B = 2
     params = model_ref.seeded_params(model_ref.param_shapes(cfg["input_dim"], cfg["hidden_dim"], cfg["n_layers"],
@@ -47,11 +55,14 @@ def cpu_baseline(cfg, T, budget_s=25.0):
     g = torch.Generator().manual_seed(0)
     src = torch.randn(B, T, cfg["input_dim"], generator=g)
     trg = torch.randn(B, T, cfg["output_dim"], generator=g) * 20
+    t0 = time.perf_counter()
     tr.step(src, trg)  # warm-up
+    log("cpu baseline warm-up step %.1fs (%d threads)" % (time.perf_counter() - t0, cores))
     n, t0 = 0, time.perf_counter()
     while n < 2 or (time.perf_counter() - t0 < budget_s * 0.5 and n < 5):
         tr.step(src, trg)
         n += 1
+        log("cpu baseline step %d done at %.1fs" % (n, time.perf_counter() - t0))
     dt = time.perf_counter() - t0
     return {"value": round(n * B * T / dt, 2), "unit": "frames/s", "cores": cores, "kind": "port",
             "sample": "228M fp32 oracle step (fwd+loss+bwd+clip+Adam, dropout 0.3), B=%d x T=%d frames, %d timed steps"
@@ -100,9 +111,11 @@ def main():
         opt.step(max_norm=2.0)
         return loss
 
-    for _ in range(args.warmup):
+    t_w = time.perf_counter()
+    for i in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        log("warm-up step %d done at %.2fs" % (i, time.perf_counter() - t_w))
 
     # live per-launch timing of the dominant kernel (GEMM) inside the timed region
     gemm_events = []
@@ -132,6 +145,7 @@ def main():
         tt = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = tt.item()
+    log("timed %d steps in %.3fs" % (args.steps, elapsed))
     loss_v = loss.item()
     if not (loss_v == loss_v):
         raise RuntimeError("non-finite loss %r" % loss_v)

@@ -108,6 +108,8 @@ typedef struct nstl_ln_args {
   float* ds;               /* f32 [rows][D] (may alias dout) */
   void* dbranch;           /* dtype: ds * masks / (1-p)^n_masks, may be NULL */
   float* dgamma_part; float* dbeta_part; int n_part;   /* [n_part][D] */
+  float* dbranch_part;     /* optional [n_part][D]: column sums of dbranch (the bias
+                              gradient of the Linear that produced y) */
 } nstl_ln_args;
 int nstl_ln_fwd(const nstl_ln_args* args, void* stream);
 int nstl_ln_bwd(const nstl_ln_args* args, void* stream);

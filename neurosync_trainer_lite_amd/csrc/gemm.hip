@@ -12,6 +12,8 @@
 // Tile 128x128, BK = 128 bytes of reduction index (64 bf16 / 32 f32), 4 waves
 // (2x2) each owning 64x64 = 4x4 MFMA 16x16 tiles, register-staged double-
 // buffered LDS (one barrier per K tile), XCD-aware tile order.
+#include <stdlib.h>
+
 #include "../../include/nstl.h"
 #include "common.h"
 #include "status.h"
@@ -35,6 +37,117 @@ struct GemmParams {
   const float* rope_cos; const float* rope_sin; int rope_T, rope_dim, rope_cols;
   float* ws; int k_chunk;  // split-K: partial slabs [z][M][N]
 };
+
+// Epilogue over a wave's MT x 4 grid of 16x16 accumulators whose origin is
+// (row0, col0).  Each 16 x 64 slab goes through the wave's own LDS scratch
+// (16 x 68 f32) and comes back as 4 consecutive columns per lane: 16-byte
+// (f32) / 8-byte (bf16) stores, RoPE pairs lane-local.  Ops: alpha, split-K
+// slab, bias / ReLU+dropout / RoPE / dReLU+dropout, beta*C.
+constexpr int EPI_LD = 68;  // floats per scratch row (64 + 4 pad)
+
+NSTL_DEV void epi_store4(const GemmParams& p, int i, int j, f32x4 v) {
+  const int epi = p.epi;
+  if (p.ws != nullptr) {
+    float* w = p.ws + ((int64_t)blockIdx.y * p.M + i) * p.N + j;
+    if (j + 3 < p.N && (p.N & 3) == 0) {
+      *(f32x4*)w = (f32x4){v[0], v[1], v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j + e < p.N) w[e] = v[e];
+    }
+    return;
+  }
+  if (p.bias != nullptr && epi != NSTL_EPI_NONE && epi != NSTL_EPI_DRELU_DROP) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += j + e < p.N ? p.bias[j + e] : 0.f;
+  }
+  if (epi == NSTL_EPI_BIAS_RELU_DROP) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = fmaxf(v[e], 0.f);
+      if (p.thresh) v[e] = nstl_keep(p.seed, (uint64_t)i * p.N + j + e, p.thresh) ? v[e] * p.inv_keep : 0.f;
+    }
+  } else if (epi == NSTL_EPI_BIAS_ROPE) {
+    if (j < p.rope_cols) {
+      const int t = i % p.rope_T, half = p.rope_dim >> 1;
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const int pair = ((j + e) % p.rope_dim) >> 1;
+        const float c = p.rope_cos[t * half + pair], sn = p.rope_sin[t * half + pair];
+        const float x0 = v[e], x1 = v[e + 1];
+        v[e] = x0 * c - x1 * sn;
+        v[e + 1] = x0 * sn + x1 * c;
+      }
+    }
+  } else if (epi == NSTL_EPI_DRELU_DROP) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (j + e < p.N) {
+        const int64_t x = (int64_t)i * p.ld_aux + j + e;
+        const float av = p.aux_f32 ? ((const float*)p.aux)[x] : (float)((const bf16*)p.aux)[x];
+        v[e] = av > 0.f ? v[e] * p.inv_keep : 0.f;
+      }
+    }
+  }
+  const int64_t o = (int64_t)i * p.ldc + j;
+  const bool vec = j + 3 < p.N && (p.ldc & 3) == 0;
+  if (p.c_f32) {
+    float* c = (float*)p.C + o;
+    if (vec) {
+      if (p.beta != 0.f) {
+        const f32x4 old = *(const f32x4*)c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += p.beta * old[e];
+      }
+      *(f32x4*)c = (f32x4){v[0], v[1], v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j + e < p.N) c[e] = p.beta != 0.f ? v[e] + p.beta * c[e] : v[e];
+    }
+  } else {
+    bf16* c = (bf16*)p.C + o;
+    if (vec) {
+      if (p.beta != 0.f) {
+        const bf16x4 old = *(const bf16x4*)c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += p.beta * (float)old[e];
+      }
+      *(bf16x4*)c = (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j + e < p.N) c[e] = (bf16)(p.beta != 0.f ? v[e] + p.beta * (float)c[e] : v[e]);
+    }
+  }
+}
+
+// HALF slabs at a time: an unrolled (statically indexed) copy of the
+// accumulators into the wave's scratch, then a runtime loop that never touches
+// `acc` (so the big epilogue body is not replicated and acc stays in registers).
+template <int MT, int HALF>
+NSTL_DEV void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[MT][4], int row0, int col0, int lane, float* scr) {
+#pragma unroll
+  for (int ph = 0; ph < MT / HALF; ++ph) {
+#pragma unroll
+    for (int a = 0; a < HALF; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          scr[(a * 16 + 4 * (lane >> 4) + r) * EPI_LD + 16 * b + (lane & 15)] = acc[ph * HALF + a][b][r] * p.alpha;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 1
+    for (int pass = 0; pass < HALF * 4; ++pass) {
+      const int rr = pass * 4 + (lane >> 4), cc = (lane & 15) * 4;
+      const f32x4 x = *(const f32x4*)(scr + rr * EPI_LD + cc);
+      const int i = row0 + ph * HALF * 16 + rr;
+      if (i < p.M && col0 + cc < p.N) epi_store4(p, i, col0 + cc, x);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
 
 template <typename T, bool KMAJ, int RB>
 struct Stager {
@@ -146,59 +259,115 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmParams p) {
     __syncthreads();
   }
 
-  // ---------------- epilogue ----------------
-  const int epi = p.epi;
+  // the K loop ended on a barrier: the staging buffers are free for the epilogue
+  gemm_epilogue<4, 2>(p, acc, m0 + wm * 64, n0 + wn * 64, lane, (float*)&smem[0][0][0] + wave * 32 * EPI_LD);
+}
+
+
+// ===========================================================================
+// 256x256 tile, 8 waves (2 x 4, each 128 x 64), BK = 64 bf16, LDS-DMA
+// (global_load_lds_dwordx4) staging into two 64 KB buffers, one barrier per K
+// tile.  A 128^2 tile moves (128+128)*2 B per 2*128^2 FLOP = 64 FLOP/B through
+// L2, which at the MFMA rate needs ~39 TB/s (> the ~34.5 TB/s aggregate L2);
+// 256^2 halves that.  The DMA writes LDS lane-linearly (1 KB per wave
+// instruction), so the bank swizzle is applied to the per-lane SOURCE address
+// and undone by the same ImgK / ImgMN read mapping.
+// Preconditions (checked on the host): bf16, K % 64 == 0, 16-byte aligned rows.
+constexpr int BIG = 256, BIG_NT = 512, BIG_TILE = 32768;
+
+template <bool KMAJ, int RB>
+NSTL_DEV void glds_stage(char* img, const char* base, int64_t ld, int row0, int rows_total, int k0, int wave,
+                         int lane) {
+  // 32 wave-instructions of 1 KB per 32 KB tile, 4 per wave
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const int j = n0 + wn * 64 + b * 16 + (lane & 15);
-    const bool jok = j < p.N;
-    float bj = 0.f;
-    if (p.bias != nullptr && jok && epi != NSTL_EPI_NONE && epi != NSTL_EPI_DRELU_DROP) bj = p.bias[j];
+  for (int s = 0; s < 4; ++s) {
+    const int q = wave * 4 + s;
+    const char* src;
+    if (KMAJ) {  // 128-byte rows: 8 rows per KB
+      const int row = 8 * q + (lane >> 3), pc = lane & 7;
+      const int lc = pc ^ ((row >> 1) & 7);
+      const int gi = min(row0 + row, rows_total - 1);
+      src = base + ((int64_t)gi * ld + k0 + lc * 8) * 2;
+    } else {     // RB-byte rows (512): 2 rows per KB
+      constexpr int CPR = RB / 16;
+      constexpr int RPK = 1024 / RB;
+      const int row = RPK * q + lane / CPR, pc = lane % CPR;
+      const int x = (row & 3) | (((row >> 3) & 1) << 2);
+      const int lc = pc ^ (x << 1);
+      const int gi = min(row0 + lc * 8, ((rows_total - 1) / 8) * 8);
+      src = base + ((int64_t)(k0 + row) * ld + gi) * 2;
+    }
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)(img + q * 1024), 16, 0, 0);
+  }
+}
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(BIG_NT, 2) void gemm256_kernel(GemmParams p) {
+  constexpr int BK = 64;
+  constexpr int MN_RB = BIG * 2;  // 512-byte rows for MN-major images
+  constexpr int A_RB = AK ? 128 : MN_RB;
+  constexpr int B_RB = BKM ? 128 : MN_RB;
+  constexpr int SMEM = 8 * 64 * EPI_LD * 4 > 4 * BIG_TILE ? 8 * 64 * EPI_LD * 4 : 4 * BIG_TILE;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nt_m = (p.M + BIG - 1) / BIG, nt_n = (p.N + BIG - 1) / BIG;
+  const int id = xcd_remap(blockIdx.x, nt_m * nt_n);
+  const int tm = id / nt_n, tn = id % nt_n;
+  const int m0 = tm * BIG, n0 = tn * BIG;
+  const int kz0 = blockIdx.y * p.k_chunk;
+  const int kz1 = min(p.K, kz0 + p.k_chunk);
+  const int nk = (kz1 - kz0) / BK;
+
+  f32x4 acc[8][4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
+  for (int a = 0; a < 8; ++a)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = m0 + wm * 64 + a * 16 + 4 * (lane >> 4) + r;
-        float v = acc[a][b][r] * p.alpha;
-        if (p.ws != nullptr) {  // split-K partial
-          if (jok && i < p.M) p.ws[((int64_t)blockIdx.y * p.M + i) * p.N + j] = v;
-          continue;
-        }
-        v += bj;
-        if (epi == NSTL_EPI_BIAS_RELU_DROP) {
-          v = fmaxf(v, 0.f);
-          if (p.thresh) v = nstl_keep(p.seed, (uint64_t)i * p.N + j, p.thresh) ? v * p.inv_keep : 0.f;
-        } else if (epi == NSTL_EPI_BIAS_ROPE) {
-          const float partner = __shfl_xor(v, 1);
-          if (j < p.rope_cols) {
-            const int t = i % p.rope_T;
-            const int half = p.rope_dim >> 1;
-            const int pair = (j % p.rope_dim) >> 1;
-            const float c = p.rope_cos[t * half + pair], s = p.rope_sin[t * half + pair];
-            v = (j & 1) ? (partner * s + v * c) : (v * c - partner * s);
-          }
-        } else if (epi == NSTL_EPI_DRELU_DROP) {
-          if (jok && i < p.M) {
-            const int64_t e = (int64_t)i * p.ld_aux + j;
-            const float av = p.aux_f32 ? ((const float*)p.aux)[e] : (float)((const bf16*)p.aux)[e];
-            v = av > 0.f ? v * p.inv_keep : 0.f;
-          }
-        }
-        if (jok && i < p.M) {
-          const int64_t e = (int64_t)i * p.ldc + j;
-          if (p.c_f32) {
-            float* c = (float*)p.C + e;
-            if (p.beta != 0.f) v += p.beta * *c;
-            *c = v;
-          } else {
-            bf16* c = (bf16*)p.C + e;
-            if (p.beta != 0.f) v += p.beta * (float)*c;
-            *c = (bf16)v;
-          }
-        }
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    glds_stage<AK, A_RB>(smem, p.A, p.lda, m0, p.M, kz0, wave, lane);
+    glds_stage<BKM, B_RB>(smem + BIG_TILE, p.B, p.ldb, n0, p.N, kz0, wave, lane);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      const int k1 = kz0 + (kt + 1) * BK;
+      glds_stage<AK, A_RB>(smem + (cur ^ 1) * 2 * BIG_TILE, p.A, p.lda, m0, p.M, k1, wave, lane);
+      glds_stage<BKM, B_RB>(smem + (cur ^ 1) * 2 * BIG_TILE + BIG_TILE, p.B, p.ldb, n0, p.N, k1, wave, lane);
+    }
+    const char* Ai = smem + cur * 2 * BIG_TILE;
+    const char* Bi = Ai + BIG_TILE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 fb[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (BKM)
+          frag_row<ImgK<128>>(fb[t], Bi, wn * 64 + t * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4));
+        else
+          frag_col<ImgMN<B_RB>>(fb[t], Bi, wn * 64 + t * 16, kk * 32, lane);
+      }
+      // one A fragment live at a time: read it, then its 4 MFMAs
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        bf16x8 fa;
+        if (AK)
+          frag_row<ImgK<128>>(fa, Ai, wm * 128 + a * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4));
+        else
+          frag_col<ImgMN<A_RB>>(fa, Ai, wm * 128 + a * 16, kk * 32, lane);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) mma16(acc[a][b], fa, fb[b]);
       }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
+  gemm_epilogue<8, 4>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, (float*)&smem[0] + wave * 64 * EPI_LD);
 }
 
 // split-K combine: C = sum_z ws[z] (+bias) (+beta*C)
@@ -224,6 +393,21 @@ __global__ void splitk_reduce(const float* ws, int splits, int M, int N, char* C
   }
 }
 
+int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t st) {
+  const int nt = ((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
+  dim3 grid(nt, splits), block(BIG_NT);
+  if (a->a_kmajor && a->b_kmajor)
+    hipLaunchKernelGGL((gemm256_kernel<true, true>), grid, block, 0, st, p);
+  else if (a->a_kmajor && !a->b_kmajor)
+    hipLaunchKernelGGL((gemm256_kernel<true, false>), grid, block, 0, st, p);
+  else if (!a->a_kmajor && !a->b_kmajor)
+    hipLaunchKernelGGL((gemm256_kernel<false, false>), grid, block, 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<false, true>), grid, block, 0, st, p);
+  NSTL_LAUNCH_CHECK("nstl_gemm (256)");
+  return 0;
+}
+
 template <typename T>
 int launch_typed(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t st) {
   const int nt = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
@@ -238,6 +422,15 @@ int launch_typed(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t
     hipLaunchKernelGGL((gemm_kernel<T, false, true>), grid, block, 0, st, p);
   NSTL_LAUNCH_CHECK("nstl_gemm");
   return 0;
+}
+
+// NSTL_GEMM_SMALL=1 forces the 128x128 kernel (A/B comparisons, debugging)
+bool getenv_small_gemm() {
+  static const int v = [] {
+    const char* e = getenv("NSTL_GEMM_SMALL");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v != 0;
 }
 
 }  // namespace
@@ -289,7 +482,13 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   p.rope_T = a->rope_T; p.rope_dim = a->rope_dim; p.rope_cols = a->rope_cols;
   p.ws = nullptr;
 
-  const int BKe = 128 / esz;
+  // the 256x256 LDS-DMA kernel: bf16, K a multiple of its 64-deep K tile, and at
+  // least 32 of its tiles (measured on the 228M step's shapes, tools/bench_gemm.py;
+  // smaller/odd problems take the 128 kernel)
+  const int64_t big_tiles = (int64_t)((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
+  const bool big = a->dtype == NSTL_BF16 && a->K % 64 == 0 && a->M >= BIG && a->N >= BIG && big_tiles >= 32 &&
+                   !getenv_small_gemm();
+  const int BKe = big ? 64 : 128 / esz;
   int splits = a->split_k > 1 ? a->split_k : 1;
   if (splits > 1) {
     NSTL_CHECK_ARG(a->epilogue == NSTL_EPI_NONE || a->epilogue == NSTL_EPI_BIAS,
@@ -305,7 +504,8 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   if (splits == 1) p.ws = nullptr;
 
   hipStream_t st = (hipStream_t)stream;
-  int rc = a->dtype == NSTL_BF16 ? launch_typed<bf16>(a, p, splits, st) : launch_typed<float>(a, p, splits, st);
+  int rc = big ? launch_big(a, p, splits, st)
+               : a->dtype == NSTL_BF16 ? launch_typed<bf16>(a, p, splits, st) : launch_typed<float>(a, p, splits, st);
   if (rc) return rc;
   if (p.ws != nullptr) {
     const int64_t total = (int64_t)a->M * a->N;

@@ -60,7 +60,7 @@ struct LnParams {
   char* s_out; char* out; float* mean; float* rstd;
   char* rot_out; const float* rope_cos; const float* rope_sin; int rope_T;
   const char* s_in; const float* dout; float* ds; char* dbranch;
-  float* dgp; float* dbp;
+  float* dgp; float* dbp; float* dyp;
 };
 
 NSTL_DEV float branch_scale(const LnParams& p, uint64_t idx) {
@@ -130,12 +130,13 @@ template <typename T, int VPL>
 __global__ __launch_bounds__(NT) void ln_bwd_kernel(LnParams p) {
   const int lane = threadIdx.x & 63;
   const int c0 = lane * VPL;
-  float gam[VPL], dg[VPL], db[VPL];
+  float gam[VPL], dg[VPL], db[VPL], dyb[VPL];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
     gam[j] = p.gamma[c0 + j];
     dg[j] = 0.f;
     db[j] = 0.f;
+    dyb[j] = 0.f;
   }
   for (int row = blockIdx.x * (NT / 64) + (threadIdx.x >> 6); row < p.rows; row += gridDim.x * (NT / 64)) {
     const int64_t base = (int64_t)row * p.D + c0;
@@ -163,27 +164,34 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(LnParams p) {
 #pragma unroll
         for (int j = 0; j < VPL; ++j) d[j] *= branch_scale(p, (uint64_t)base + j);
       }
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) d[j] = to_f32(from_f32<T>(d[j]));  // sum what is stored
       store_row<T, VPL>((T*)p.dbranch + base, d);
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) dyb[j] += d[j];
     }
   }
   // per-block partials: reduce the 4 waves through LDS
-  __shared__ float red[2][NT / 64][1024];
+  __shared__ float red[3][NT / 64][1024];
   const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
     red[0][w][c0 + j] = dg[j];
     red[1][w][c0 + j] = db[j];
+    red[2][w][c0 + j] = dyb[j];
   }
   __syncthreads();
   for (int c = threadIdx.x; c < p.D; c += NT) {
-    float a = 0.f, b = 0.f;
+    float a = 0.f, b = 0.f, y = 0.f;
 #pragma unroll
     for (int k = 0; k < NT / 64; ++k) {
       a += red[0][k][c];
       b += red[1][k][c];
+      y += red[2][k][c];
     }
     p.dgp[(int64_t)blockIdx.x * p.D + c] = a;
     p.dbp[(int64_t)blockIdx.x * p.D + c] = b;
+    if (p.dyp) p.dyp[(int64_t)blockIdx.x * p.D + c] = y;
   }
 }
 
@@ -223,7 +231,7 @@ int fill(LnParams& p, const nstl_ln_args* a) {
   p.s_out = (char*)a->s_out; p.out = (char*)a->out; p.mean = a->mean; p.rstd = a->rstd;
   p.rot_out = (char*)a->rot_out; p.rope_cos = a->rope_cos; p.rope_sin = a->rope_sin; p.rope_T = a->rope_T;
   p.s_in = (const char*)a->s_in; p.dout = a->dout; p.ds = a->ds; p.dbranch = (char*)a->dbranch;
-  p.dgp = a->dgamma_part; p.dbp = a->dbeta_part;
+  p.dgp = a->dgamma_part; p.dbp = a->dbeta_part; p.dyp = a->dbranch_part;
   return 0;
 }
 

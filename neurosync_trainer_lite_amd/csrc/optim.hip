@@ -115,6 +115,40 @@ __global__ void copy2d_kernel(int src_bf16, const void* src, int64_t src_ld, int
 }
 
 constexpr int COLSUM_ROWS = 256;
+// Column sums, stage 1: block = 256-row chunk x 256 columns; each thread owns
+// 8 contiguous columns (one 16-byte load per row) of one of 8 row groups.
+template <typename T>
+__global__ __launch_bounds__(NT) void colsum_vec_kernel(const T* x, int64_t ld, int rows, int cols, float* partial) {
+  constexpr int EPV = 16 / sizeof(T);     // elements per 16-byte load
+  constexpr int CT = 256 / EPV;           // column threads per block row
+  constexpr int RG = NT / CT;             // row groups
+  const int ct = threadIdx.x % CT, rg = threadIdx.x / CT;
+  const int c0 = blockIdx.x * 256 + ct * EPV;
+  const int r0 = blockIdx.y * COLSUM_ROWS, r1 = min(rows, r0 + COLSUM_ROWS);
+  float acc[EPV];
+#pragma unroll
+  for (int j = 0; j < EPV; ++j) acc[j] = 0.f;
+  if (c0 < cols) {
+    for (int r = r0 + rg; r < r1; r += RG) {
+      const uint4 u = *(const uint4*)(x + (int64_t)r * ld + c0);
+      const T* e = (const T*)&u;
+#pragma unroll
+      for (int j = 0; j < EPV; ++j) acc[j] += to_f32(e[j]);
+    }
+  }
+  __shared__ float red[RG][256];
+#pragma unroll
+  for (int j = 0; j < EPV; ++j) red[rg][ct * EPV + j] = acc[j];
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (threadIdx.x < 256 && c < cols) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < RG; ++g) s += red[g][threadIdx.x];
+    partial[(int64_t)blockIdx.y * cols + c] = s;
+  }
+}
+
 template <typename T>
 __global__ void colsum_kernel(const T* x, int64_t ld, int rows, int cols, float* partial) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -125,12 +159,26 @@ __global__ void colsum_kernel(const T* x, int64_t ld, int rows, int cols, float*
   partial[(int64_t)blockIdx.y * cols + j] = s;
 }
 
-__global__ void reduce_rows_kernel(const float* part, int n_part, int cols, float* out, float beta) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= cols) return;
+// out[j] = beta*out[j] + sum_k part[k][j]: block = 64 columns x 4 row groups
+__global__ __launch_bounds__(NT) void reduce_rows_kernel(const float* part, int n_part, int cols, float* out,
+                                                         float beta) {
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int k = 0; k < n_part; ++k) s += part[(int64_t)k * cols + j];
-  out[j] = beta != 0.f ? beta * out[j] + s : s;
+  if (j < cols) {
+    int k = rg;
+    for (; k + 12 < n_part; k += 16)
+      s += (part[(int64_t)k * cols + j] + part[(int64_t)(k + 4) * cols + j]) +
+           (part[(int64_t)(k + 8) * cols + j] + part[(int64_t)(k + 12) * cols + j]);
+    for (; k < n_part; k += 4) s += part[(int64_t)k * cols + j];
+  }
+  __shared__ float red[4][64];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && j < cols) {
+    const float t = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    out[j] = beta != 0.f ? beta * out[j] + t : t;
+  }
 }
 
 template <typename TI, typename TO>
@@ -215,21 +263,31 @@ extern "C" int nstl_colsum(int dtype, const void* x, int64_t ld, int rows, int c
                            float beta, void* stream) {
   NSTL_CHECK_ARG(x && partial && out && rows > 0 && cols > 0 && ld >= cols, "nstl_colsum: bad args");
   const int nchunk = (rows + COLSUM_ROWS - 1) / COLSUM_ROWS;
-  dim3 grid((cols + NT - 1) / NT, nchunk);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == NSTL_BF16)
-    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(NT), 0, st, (const bf16*)x, ld, rows, cols, partial);
-  else
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(NT), 0, st, (const float*)x, ld, rows, cols, partial);
+  const int epv = dtype == NSTL_BF16 ? 8 : 4;
+  const bool vec = cols % epv == 0 && ld % epv == 0 && ((uintptr_t)x % 16) == 0;
+  if (vec) {
+    dim3 grid((cols + 255) / 256, nchunk);
+    if (dtype == NSTL_BF16)
+      hipLaunchKernelGGL(colsum_vec_kernel<bf16>, grid, dim3(NT), 0, st, (const bf16*)x, ld, rows, cols, partial);
+    else
+      hipLaunchKernelGGL(colsum_vec_kernel<float>, grid, dim3(NT), 0, st, (const float*)x, ld, rows, cols, partial);
+  } else {
+    dim3 grid((cols + NT - 1) / NT, nchunk);
+    if (dtype == NSTL_BF16)
+      hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(NT), 0, st, (const bf16*)x, ld, rows, cols, partial);
+    else
+      hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(NT), 0, st, (const float*)x, ld, rows, cols, partial);
+  }
   NSTL_LAUNCH_CHECK("nstl_colsum");
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + NT - 1) / NT), dim3(NT), 0, st, partial, nchunk, cols, out, beta);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + 63) / 64), dim3(NT), 0, st, partial, nchunk, cols, out, beta);
   NSTL_LAUNCH_CHECK("nstl_colsum reduce");
   return 0;
 }
 
 extern "C" int nstl_reduce_rows(const float* part, int n_part, int cols, float* out, float beta, void* stream) {
   NSTL_CHECK_ARG(part && out && n_part > 0 && cols > 0, "nstl_reduce_rows: bad args");
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + NT - 1) / NT), dim3(NT), 0, (hipStream_t)stream, part, n_part,
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + 63) / 64), dim3(NT), 0, (hipStream_t)stream, part, n_part,
                      cols, out, beta);
   NSTL_LAUNCH_CHECK("nstl_reduce_rows");
   return 0;

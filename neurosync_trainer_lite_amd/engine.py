@@ -102,7 +102,7 @@ class _Buffers:
             self.demb = e(M, D)
             self.dpred = torch.zeros(M, 64, dtype=dt, device=dev)
             self.n_part = max(1, min(256, M // 4))
-            self.ln_part = e(2, self.n_part, D, dtype=f32)
+            self.ln_part = e(3, self.n_part, D, dtype=f32)
             self.col_part = e((M + 255) // 256, max(Fd, 3 * D, 64), dtype=f32)
             self.ws = e(eng.splitk_ws_elems(M), dtype=f32)
 
@@ -281,9 +281,18 @@ class Seq2SeqEngine:
 
     @staticmethod
     def splits(n, k, m):
-        tiles = ((n + 127) // 128) * ((k + 127) // 128)
-        s = max(1, min(16, 512 // max(1, tiles)))
-        while s > 1 and m // s < 1024:
+        """split-K for a weight-gradient GEMM C[n,k] = sum over m tokens.  Mirrors the
+        kernel choice in nstl_gemm: >= 32 tiles of 256^2 -> the 256 kernel, aim for
+        ~256 blocks; else the 128 kernel, aim for ~512 blocks (tools/bench_gemm.py)."""
+        t256 = ((n + 255) // 256) * ((k + 255) // 256)
+        if t256 >= 32 and n >= 256 and k >= 256:
+            target, tiles = 256, t256
+        else:
+            target, tiles = 512, ((n + 127) // 128) * ((k + 127) // 128)
+        s = 1
+        while s * 2 * tiles <= target and s < 16:
+            s *= 2
+        while s > 1 and (m // s < 1024 or m % (64 * s)):
             s //= 2
         return s
 
@@ -294,15 +303,17 @@ class Seq2SeqEngine:
         K.gemm(x, W, out, x.shape[0], W.shape[0], W.shape[1], epilogue=epi, bias=bias, rope=rope,
                rope_cols=rope_cols, p_drop=p_drop, seed=seed, stream=self.st)
 
-    def _dw(self, dy, x, wname, rows, bf, ws):
-        """grad(W) (+)= dy^T x ; grad(b) (+)= colsum(dy)."""
+    def _dw(self, dy, x, wname, rows, bf, ws, bias=True):
+        """grad(W) (+)= dy^T x ; grad(b) (+)= colsum(dy) (unless the bias gradient
+        was already produced by the LayerNorm backward that wrote dy)."""
         G = self.gw(wname, rows)
         n, k = G.shape
         m = dy.shape[0]
         s = self.splits(n, k, m)
         K.gemm(dy, x, G, n, k, m, a_kmajor=False, b_kmajor=False, beta=bf, split_k=s, workspace=ws, stream=self.st)
-        bname = wname.replace(".weight", ".bias")
-        K.colsum(dy, dy.stride(0), m, n, self.cur.col_part, self.gb(bname, rows), bf, stream=self.st)
+        if bias:
+            bname = wname.replace(".weight", ".bias")
+            K.colsum(dy, dy.stride(0), m, n, self.cur.col_part, self.gb(bname, rows), bf, stream=self.st)
 
     def _dx(self, dy, wname, rows, out, beta, epi=K.EPI_NONE, aux=None, p_drop=0.0):
         """out (+)= dy W  (W: [N][K] read as [r][j])."""
@@ -325,7 +336,9 @@ class Seq2SeqEngine:
             a.rot_out, a.rope_cos, a.rope_sin, a.rope_T = rot.data_ptr(), cs.data_ptr(), sn.data_ptr(), T
         K.ln_fwd(a, stream=self.st)
 
-    def _ln_bwd(self, s_in, stats, prefix, dres_in, dres_out, dbranch, n_masks, seeds, bf):
+    def _ln_bwd(self, s_in, stats, prefix, dres_in, dres_out, dbranch, n_masks, seeds, bf, bias_of=None):
+        """LayerNorm(+dropout+residual) backward; with `bias_of`, the column sums of
+        dbranch become grad(bias) of that Linear (its output was the LN branch)."""
         bb = self.cur
         a = K.LnArgs()
         a.dtype = K.dtype_code(self.dt)
@@ -336,9 +349,13 @@ class Seq2SeqEngine:
         a.mean, a.rstd = stats[0].data_ptr(), stats[1].data_ptr()
         a.s_in, a.dout, a.ds, a.dbranch = s_in.data_ptr(), dres_in.data_ptr(), dres_out.data_ptr(), K.ptr(dbranch)
         a.dgamma_part, a.dbeta_part, a.n_part = bb.ln_part[0].data_ptr(), bb.ln_part[1].data_ptr(), bb.n_part
+        if bias_of is not None:
+            a.dbranch_part = bb.ln_part[2].data_ptr()
         K.ln_bwd(a, stream=self.st)
         K.reduce_rows(bb.ln_part[0], bb.n_part, self.D, self.gb(prefix + ".weight"), bf, stream=self.st)
         K.reduce_rows(bb.ln_part[1], bb.n_part, self.D, self.gb(prefix + ".bias"), bf, stream=self.st)
+        if bias_of is not None:
+            K.reduce_rows(bb.ln_part[2], bb.n_part, self.D, self.gb(bias_of), bf, stream=self.st)
 
     def _attn(self, q, k, v, o, lse, seed, T, B):
         a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
@@ -500,8 +517,9 @@ class Seq2SeqEngine:
     def _attn_block_bwd(self, bb, pre, x_in, qkv, o, lse, st, s1, norm, seeds, T, bf):
         """Backward through x1 = LN(x_in + drop(drop(out_linear(attn(x_in))))) (self-attention)."""
         D, ws = self.D, bb.ws
-        self._ln_bwd(s1, st, pre + norm, bb.dres, bb.dres, bb.dy, 2, seeds[0:2], bf)
-        self._dw(bb.dy, o, pre + "self_attn.out_linear.weight", 1, bf, ws)
+        self._ln_bwd(s1, st, pre + norm, bb.dres, bb.dres, bb.dy, 2, seeds[0:2], bf,
+                     bias_of=pre + "self_attn.out_linear.bias")
+        self._dw(bb.dy, o, pre + "self_attn.out_linear.weight", 1, bf, ws, bias=False)
         self._dx(bb.dy, pre + "self_attn.out_linear.weight", 1, bb.dattn, 0.0)
         self._attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, bb.dattn,
                        bb.dqkv[:, :D], bb.dqkv[:, D:2 * D], bb.dqkv[:, 2 * D:], seeds[2], T, bb.B)
@@ -511,8 +529,9 @@ class Seq2SeqEngine:
     def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf):
         """Backward through x_out = LN(x_in + drop(FFN(x_in)))."""
         ws = self.cur.ws
-        self._ln_bwd(s_out, st, pre + norm, bb.dres, bb.dres, bb.dy, 1, (seed_drop, 0), bf)
-        self._dw(bb.dy, h, pre + "ffn.linear2.weight", 1, bf, ws)
+        self._ln_bwd(s_out, st, pre + norm, bb.dres, bb.dres, bb.dy, 1, (seed_drop, 0), bf,
+                     bias_of=pre + "ffn.linear2.bias")
+        self._dw(bb.dy, h, pre + "ffn.linear2.weight", 1, bf, ws, bias=False)
         self._dx(bb.dy, pre + "ffn.linear2.weight", 1, bb.dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p)
         self._dw(bb.dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws)
         self._dx(bb.dh, pre + "ffn.linear1.weight", 1, bb.dres, 1.0)
@@ -534,9 +553,10 @@ class Seq2SeqEngine:
         x_in = bb.xdec0 if l == 0 else bb.d_x3[l - 1]
         self._ffn_bwd(bb, pre, bb.d_x2[l], bb.d_h[l], bb.d_s3[l], st[4:6], "norm3", sd("drop3"), bf)
         # cross attention block: x2 = LN(x1 + drop(drop(out(attn(q(x1), kv(mem))))))
-        self._ln_bwd(bb.d_s2[l], st[2:4], pre + "norm2", bb.dres, bb.dres, bb.dy, 2, (sd("xresid"), sd("drop2x")), bf)
         m = pre + "multihead_attn."
-        self._dw(bb.dy, bb.d_oc[l], m + "out_linear.weight", 1, bf, ws)
+        self._ln_bwd(bb.d_s2[l], st[2:4], pre + "norm2", bb.dres, bb.dres, bb.dy, 2, (sd("xresid"), sd("drop2x")), bf,
+                     bias_of=m + "out_linear.bias")
+        self._dw(bb.dy, bb.d_oc[l], m + "out_linear.weight", 1, bf, ws, bias=False)
         self._dx(bb.dy, m + "out_linear.weight", 1, bb.dattn, 0.0)
         kvc = bb.d_kvc[l]
         self._attn_bwd(bb.d_qc[l], kvc[:, :D], kvc[:, D:], bb.d_oc[l], bb.d_lsec[l], bb.dattn,

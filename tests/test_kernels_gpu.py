@@ -417,3 +417,65 @@ def test_small_kernels():
     back = torch.zeros_like(y)
     K.rope(r, D, back, D, 2 * T, D, cs, sn, T, D, inverse=True, accumulate=True)
     check(back, y, 1e-6, "rope inverse")
+
+
+# ---------------------------------------------------------------------------
+# 256x256 LDS-DMA kernel (selected for bf16 problems with >= 64 of its tiles)
+@pytest.mark.parametrize("M,N,Kd", [(2048, 2048, 512), (2000, 2304, 256), (4096, 1024, 1024)])
+def test_gemm256_forward(M, N, Kd):
+    dt = torch.bfloat16
+    A, W, b = rnd(M, Kd, dtype=dt, seed=80), rnd(N, Kd, dtype=dt, scale=0.05, seed=81), rnd(N, seed=82)
+    C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    K.gemm(A, W, C, M, N, Kd, epilogue=K.EPI_BIAS, bias=b)
+    torch.cuda.synchronize()
+    check(C, f64(A) @ f64(W).T + f64(b), 1e-5, "gemm256 NT")
+
+
+@pytest.mark.parametrize("M,N,Kd", [(2048, 2048, 512), (4096, 1024, 2048)])
+def test_gemm256_dx(M, N, Kd):
+    dt = torch.bfloat16
+    dY, W = rnd(M, N, dtype=dt, seed=83), rnd(N, Kd, dtype=dt, seed=84)
+    C0 = rnd(M, Kd, seed=85)
+    C = C0.clone()
+    K.gemm(dY, W, C, M, Kd, N, a_kmajor=True, b_kmajor=False, beta=1.0)
+    torch.cuda.synchronize()
+    check(C, f64(C0) + f64(dY) @ f64(W), 1e-5, "gemm256 dX")
+
+
+@pytest.mark.parametrize("Mt,N,Kd,split", [(4096, 512, 512, 16), (2048, 2048, 512, 1), (8192, 768, 512, 8)])
+def test_gemm256_dw(Mt, N, Kd, split):
+    dt = torch.bfloat16
+    dY, X = rnd(Mt, N, dtype=dt, seed=86), rnd(Mt, Kd, dtype=dt, seed=87)
+    C0 = rnd(N, Kd, seed=88)
+    C = C0.clone()
+    ws = torch.empty(split * N * Kd, dtype=torch.float32, device=DEV)
+    K.gemm(dY, X, C, N, Kd, Mt, a_kmajor=False, b_kmajor=False, beta=1.0, split_k=split, workspace=ws)
+    torch.cuda.synchronize()
+    check(C, f64(C0) + f64(dY).T @ f64(X), 1e-5, "gemm256 dW")
+
+
+def test_gemm256_epilogues():
+    """RoPE / ReLU-dropout / dReLU epilogues through the 256 kernel (bf16 out)."""
+    dt, B, T, D = torch.bfloat16, 16, 128, 1024
+    M = B * T
+    X, W, b = rnd(M, 256, dtype=dt, seed=89), rnd(3 * D, 256, dtype=dt, scale=0.05, seed=90), rnd(3 * D, seed=91)
+    cs, sn = rotation_tables(T, 64, DEV)
+    C = torch.empty(M, 3 * D, dtype=dt, device=DEV)
+    K.gemm(X, W, C, M, 3 * D, 256, epilogue=K.EPI_BIAS_ROPE, bias=b, rope=(cs, sn, T, 64), rope_cols=2 * D)
+    y = f64(X) @ f64(W).T + f64(b)
+    ref = y.clone()
+    c, s = f64(cs), f64(sn)
+    z = y[:, :2 * D].reshape(B, T, 2 * D // 64, 64).permute(0, 2, 1, 3)
+    e, o = z[..., 0::2], z[..., 1::2]
+    r = torch.empty_like(z)
+    r[..., 0::2] = e * c - o * s
+    r[..., 1::2] = e * s + o * c
+    ref[:, :2 * D] = r.permute(0, 2, 1, 3).reshape(M, 2 * D)
+    check(C, ref, 8e-3, "gemm256 rope")
+    H = torch.empty(M, 3 * D, dtype=dt, device=DEV)
+    K.gemm(X, W, H, M, 3 * D, 256, epilogue=K.EPI_BIAS_RELU_DROP, bias=b, p_drop=0.3, seed=5)
+    h = f64(H)
+    pos = torch.relu(y) > 1e-2
+    kept = h[pos] != 0
+    assert abs(kept.double().mean().item() - 0.7) < 0.01
+    torch.testing.assert_close(h[pos][kept], (torch.relu(y)[pos][kept] / 0.7), rtol=1e-2, atol=1e-3)
