@@ -1,18 +1,21 @@
 // Multi-head attention forward/backward for the NeuroSync Seq2Seq
 // (replaces F.scaled_dot_product_attention, utils/model.py:126-127, and its
 // autograd backward; RoPE (apply_rope_qk, :60-83) is applied to q/k by the
-// projection GEMM epilogue, and rotated back here on dq/dk).
+// projection epilogue, and rotated back here on dq/dk).
 //
 // Shapes are short: T <= 256 frames, dh = 64.  A whole (batch, head) key/value
 // sequence fits in LDS, so there is no online softmax and no cross-workgroup
 // reduction:
 //   forward : workgroup = (b, h, 64 query rows); each wave 16 rows; scores for
-//             all keys live in MFMA accumulators; exact softmax; P round-trips
-//             through a per-wave LDS image to become the A operand of P.V.
+//             all keys live in MFMA accumulators; exact softmax; P^T is staged
+//             through a per-wave LDS image (one 8-byte write per lane and key
+//             tile) and read back with transpose reads as the A operand of P.V.
 //   backward: workgroup = (b, h); phase 1 waves own 16-key tiles and accumulate
 //             dK, dV over all queries; phase 2 waves own 16-query tiles and
 //             accumulate dQ (scores/probabilities recomputed from the saved LSE).
-// Dropout keep-mask is a counter hash of (b, h, q, k): regenerated, never stored.
+// Q/K/V/dO tiles arrive by LDS-DMA (global_load_lds_dwordx4, all in flight
+// together; bank swizzle applied on the source address).  Dropout keep-mask is a
+// counter hash of (b, h, key, query): regenerated in backward, never stored.
 #include <algorithm>
 
 #include "../../include/nstl.h"
@@ -41,14 +44,20 @@ struct AttnParams {
   uint32_t thresh; float inv_keep; uint64_t seed;
 };
 
-// Copy rows [0, nrows) of a (b, h) slice (64 elements per row) into an LDS image.
-template <typename T, class Img>
-NSTL_DEV void load_rows(char* img, const char* g, int64_t ld, int64_t row0, int col0, int nrows, int tid) {
-  constexpr int CPR = DH * (int)sizeof(T) / 16;
-  for (int c = tid; c < nrows * CPR; c += NT) {
-    const int row = c / CPR, ch = c % CPR;
-    const uint4 v = *(const uint4*)(g + (((row0 + row) * ld + col0) * (int64_t)sizeof(T)) + ch * 16);
-    *(uint4*)(img + Img::off(row, ch * 16)) = v;
+// LDS-DMA rows [0, nrows) of a (b, h) slice (64 elements per row) into an
+// ImgK<RB> image.  One wave instruction moves 1 KB = 1024/RB rows; the image
+// swizzle is applied to the per-lane source chunk.
+template <int RB>
+NSTL_DEV void dma_rows(char* img, const char* g, int64_t ld_bytes, int nrows, int wave, int lane) {
+  constexpr int RPK = 1024 / RB, CPR = RB / 16;
+  const int ninst = nrows / RPK;
+  for (int q = wave; q < ninst; q += NT / 64) {
+    const int row = q * RPK + lane / CPR, pc = lane % CPR;
+    const int x = RB == 128 ? ((row >> 1) & 7) : (row & 15);
+    const int lc = pc ^ x;
+    const char* src = g + row * ld_bytes + lc * 16;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)(img + q * 1024), 16, 0, 0);
   }
 }
 
@@ -57,31 +66,44 @@ NSTL_DEV void store_elem(char* base, int64_t e, float v) {
   ((T*)base)[e] = from_f32<T>(v);
 }
 
-NSTL_DEV uint64_t drop_idx(int bh, int T, int q, int k) { return ((uint64_t)bh * T + q) * T + k; }
+// dropout element index: key-major so that (q, q+1) form a hash pair
+NSTL_DEV uint64_t drop_idx(int bh, int T, int q, int k) { return ((uint64_t)bh * T + k) * T + q; }
+
+// four consecutive values of one lane as an 8-byte (bf16) / 16-byte (f32) LDS write
+NSTL_DEV void put4(char* dst, float a, float b, float c, float d, bf16) {
+  *(bf16x4*)dst = (bf16x4){(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+}
+NSTL_DEV void put4(char* dst, float a, float b, float c, float d, float) {
+  *(f32x4*)dst = (f32x4){a, b, c, d};
+}
 
 // ----------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
-  constexpr int RBK = DH * (int)sizeof(T);  // 128 (bf16) / 256 (f32)
+  constexpr int ESZ = (int)sizeof(T);
+  constexpr int RBK = DH * ESZ;   // 128 (bf16) / 256 (f32)
+  constexpr int RBP = 16 * ESZ;   // P^T image rows: 16 queries
   typedef ImgK<RBK> Img;
+  typedef ImgPlain<RBP> ImgP;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int T_ = p.T, nkt = T_ / 16;
-  const int RBP = T_ * (int)sizeof(T) + 16;
   char* Kimg = smem;
   char* Vimg = Kimg + T_ * RBK;
   char* Qimg = Vimg + T_ * RBK;
   char* Pimg = Qimg + 64 * RBK;
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int qb0 = blockIdx.x * 64;
   const int nq = min(64, T_ - qb0);
   const int64_t tok0 = (int64_t)b * T_;
 
-  load_rows<T, Img>(Kimg, p.k, p.k_ld, tok0, h * DH, T_, tid);
-  load_rows<T, Img>(Vimg, p.v, p.v_ld, tok0, h * DH, T_, tid);
-  load_rows<T, Img>(Qimg, p.q, p.q_ld, tok0 + qb0, h * DH, nq, tid);
+  dma_rows<RBK>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
+  dma_rows<RBK>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
+  dma_rows<RBK>(Qimg, p.q + ((tok0 + qb0) * p.q_ld + h * DH) * ESZ, p.q_ld * ESZ, nq, w, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int q0 = w * 16;  // local row base of this wave
@@ -94,11 +116,11 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
     for (int kt = 0; kt < 16; ++kt) {
       s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
       if (kt < nkt) {
-        Frag fk;
-        frag_row<Img>(fk, Kimg, kt * 16 + (lane & 15), 8 * g);
-        mma16(s[kt], fq[0], fk);
-        frag_row<Img>(fk, Kimg, kt * 16 + (lane & 15), 32 + 8 * g);
-        mma16(s[kt], fq[1], fk);
+        Frag fk0, fk1;
+        frag_row<Img>(fk0, Kimg, kt * 16 + (lane & 15), 8 * g);
+        frag_row<Img>(fk1, Kimg, kt * 16 + (lane & 15), 32 + 8 * g);
+        mma16(s[kt], fq[0], fk0);
+        mma16(s[kt], fq[1], fk1);
       }
     }
     const float c2 = p.scale * LOG2E;
@@ -128,19 +150,25 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
       sm += __shfl_xor(sm, 8);
       sum[r] = sm;
     }
-    // dropout + write P (unnormalised) into this wave's image [16 rows][T keys]
-    char* Pw = Pimg + w * 16 * RBP;
+    // dropout + P^T (unnormalised) into this wave's image [T keys][16 rows]
+    char* Pw = Pimg + w * max(T_, 64) * RBP;  // also holds the 16 x 64 O tile
+    const int qrow = qb0 + q0 + 4 * g;  // this lane's first query (even)
 #pragma unroll
     for (int kt = 0; kt < 16; ++kt) {
       if (kt < nkt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 4 * g + r, key = kt * 16 + (lane & 15);
-          float pv = s[kt][r];
-          if (p.thresh)
-            pv = nstl_keep(p.seed, drop_idx(bh, T_, qb0 + q0 + row, key), p.thresh) ? pv * p.inv_keep : 0.f;
-          *(T*)(Pw + row * RBP + key * (int)sizeof(T)) = from_f32<T>(pv);
+        const int key = kt * 16 + (lane & 15);
+        float v0 = s[kt][0], v1 = s[kt][1], v2 = s[kt][2], v3 = s[kt][3];
+        if (p.thresh) {
+          bool k0, k1, k2, k3;
+          const uint64_t idx = drop_idx(bh, T_, qrow, key);
+          nstl_keep2(p.seed, idx, p.thresh, k0, k1);
+          nstl_keep2(p.seed, idx + 2, p.thresh, k2, k3);
+          v0 = k0 ? v0 * p.inv_keep : 0.f;
+          v1 = k1 ? v1 * p.inv_keep : 0.f;
+          v2 = k2 ? v2 * p.inv_keep : 0.f;
+          v3 = k3 ? v3 * p.inv_keep : 0.f;
         }
+        put4(Pw + key * RBP + 4 * g * ESZ, v0, v1, v2, v3, T());
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -149,7 +177,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
     for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int ks = 0; ks < nkt / 2; ++ks) {
       Frag fp;
-      frag_row<ImgPlain<0>>(fp, Pw + (lane & 15) * RBP, 0, ks * 32 + 8 * g);
+      frag_col<ImgP>(fp, Pw, 0, ks * 32, lane);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         Frag fv;
@@ -157,14 +185,28 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
         mma16(o[dt], fp, fv);
       }
     }
+    // O: stage 16 x 64 through the (now free) P^T image, store 16-byte rows
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    char* Ow = Pw;  // [16 rows][64 d] of T = 64 * RBP bytes
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int q = qb0 + q0 + 4 * g + r;
       const float inv = 1.f / sum[r];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        store_elem<T>(p.o, (tok0 + q) * p.o_ld + h * DH + dt * 16 + (lane & 15), o[dt][r] * inv);
-      if ((lane & 15) == 0) p.lse[(int64_t)bh * T_ + q] = mx[r] * p.scale + logf(sum[r]);
+        *(T*)(Ow + (4 * g + r) * RBK + (dt * 16 + (lane & 15)) * ESZ) = from_f32<T>(o[dt][r] * inv);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int CPR = RBK / 16;
+#pragma unroll
+    for (int c = lane; c < 16 * CPR; c += 64) {
+      const int row = c / CPR, ch = c % CPR;
+      const uint4 val = *(const uint4*)(Ow + row * RBK + ch * 16);
+      *(uint4*)(p.o + ((tok0 + qb0 + q0 + row) * p.o_ld + h * DH) * ESZ + ch * 16) = val;
+    }
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        p.lse[(int64_t)bh * T_ + qb0 + q0 + 4 * g + r] = mx[r] * p.scale + logf(sum[r]);
     }
   }
 }
@@ -179,9 +221,10 @@ NSTL_DEV float rope_back(float v, int t, int d, const float* cs, const float* sn
 template <typename T>
 __global__ __launch_bounds__(NT) void attn_bwd_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
-  constexpr int RBK = DH * (int)sizeof(T);
+  constexpr int ESZ = (int)sizeof(T);
+  constexpr int RBK = DH * ESZ;
   typedef ImgK<RBK> Img;
-  constexpr int RBS = 32 * (int)sizeof(T) + 16;  // per-wave scratch rows (32 elems + pad)
+  constexpr int RBS = 16 * ESZ;     // per-wave scratch rows: 16 entries
   typedef ImgPlain<RBS> ImgS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int T_ = p.T, nkt = T_ / 16;
@@ -193,30 +236,49 @@ __global__ __launch_bounds__(NT) void attn_bwd_kernel(AttnParams p) {
   float* dq_s = lse_s + T_;
   char* scratch = (char*)(dq_s + T_);
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
   const int64_t tok0 = (int64_t)b * T_;
 
-  load_rows<T, Img>(Qimg, p.q, p.q_ld, tok0, h * DH, T_, tid);
-  load_rows<T, Img>(Kimg, p.k, p.k_ld, tok0, h * DH, T_, tid);
-  load_rows<T, Img>(Vimg, p.v, p.v_ld, tok0, h * DH, T_, tid);
-  load_rows<T, Img>(Dimg, p.dout, p.dout_ld, tok0, h * DH, T_, tid);
-  // D_q = rowsum(dO * O), one wave per row group
-  for (int row = w; row < T_; row += NT / 64) {
-    const int64_t eo = (tok0 + row) * p.o_ld + h * DH + lane;
-    const int64_t ed = (tok0 + row) * p.dout_ld + h * DH + lane;
-    float v = to_f32(((const T*)p.o)[eo]) * to_f32(((const T*)p.dout)[ed]);
-    v = wave_sum(v);
-    if (lane == 0) {
-      dq_s[row] = v;
-      lse_s[row] = p.lse[(int64_t)bh * T_ + row];
+  dma_rows<RBK>(Qimg, p.q + (tok0 * p.q_ld + h * DH) * ESZ, p.q_ld * ESZ, T_, w, lane);
+  dma_rows<RBK>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
+  dma_rows<RBK>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
+  dma_rows<RBK>(Dimg, p.dout + (tok0 * p.dout_ld + h * DH) * ESZ, p.dout_ld * ESZ, T_, w, lane);
+  // D_q = rowsum(dO * O): 256/T threads per row, each a run of 16-byte chunks;
+  // the O loads are issued together, dO is read once the DMA has landed
+  constexpr int EPC = 16 / ESZ;
+  const int tpr = NT / T_;                 // threads per row (1..8)
+  const int row = tid / tpr, part = tid % tpr;
+  const int nch = (DH / EPC) / tpr;        // chunks per thread
+  uint4 ov[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    if (c < nch) ov[c] = *(const uint4*)(p.o + ((tok0 + row) * p.o_ld + h * DH + (part * nch + c) * EPC) * ESZ);
+  if (tid < T_) lse_s[tid] = p.lse[(int64_t)bh * T_ + tid];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (c < nch) {
+        const int ch = part * nch + c;
+        const uint4 dv = *(const uint4*)(Dimg + Img::off(row, ch * 16));
+        const T* oe = (const T*)&ov[c];
+        const T* de = (const T*)&dv;
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) acc += to_f32(oe[e]) * to_f32(de[e]);
+      }
     }
+    for (int o = 1; o < tpr; o <<= 1) acc += __shfl_xor(acc, o);
+    if (part == 0) dq_s[row] = acc;
   }
   __syncthreads();
 
   const float c2 = p.scale * LOG2E;
-  char* S1 = scratch + w * 2 * 16 * RBS;  // Pd^T / dS image A
-  char* S2 = S1 + 16 * RBS;               // dS^T image
+  char* S1 = scratch + w * 2 * 32 * RBS;  // [32 rows][16] images
+  char* S2 = S1 + 32 * RBS;
 
   // ---------------- phase 1: dK, dV for 16-key tiles ----------------
   for (int kt = w; kt < nkt; kt += 4) {
@@ -242,27 +304,32 @@ __global__ __launch_bounds__(NT) void attn_bwd_kernel(AttnParams p) {
         mma16(dpt, fv[0], fb);
         frag_row<Img>(fb, Dimg, qt * 16 + (lane & 15), 32 + 8 * g);
         mma16(dpt, fv[1], fb);
+        // accumulator: row = key (4g + r), col = query
         const int q = qt * 16 + (lane & 15);
         const float lq = lse_s[q] * LOG2E, dqv = dq_s[q];
+        float pd[4], ds[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int kr = 4 * g + r, key = kt * 16 + kr;
+          const int key = kt * 16 + 4 * g + r;
           const float pv = exp2f(st[r] * c2 - lq);
-          float pd = pv, dpd = dpt[r];
+          float pdr = pv, dpd = dpt[r];
           if (p.thresh) {
             const bool keep = nstl_keep(p.seed, drop_idx(bh, T_, q, key), p.thresh);
-            pd = keep ? pv * p.inv_keep : 0.f;
+            pdr = keep ? pv * p.inv_keep : 0.f;
             dpd = keep ? dpd * p.inv_keep : 0.f;
           }
-          const float ds = pv * (dpd - dqv);
-          *(T*)(S1 + ImgS::off(kr, (u * 16 + (lane & 15)) * (int)sizeof(T))) = from_f32<T>(pd);
-          *(T*)(S2 + ImgS::off(kr, (u * 16 + (lane & 15)) * (int)sizeof(T))) = from_f32<T>(ds);
+          pd[r] = pdr;
+          ds[r] = pv * (dpd - dqv);
         }
+        // transposed images [query][key]: this lane's 4 keys are contiguous
+        const int qr = u * 16 + (lane & 15);
+        put4(S1 + qr * RBS + 4 * g * ESZ, pd[0], pd[1], pd[2], pd[3], T());
+        put4(S2 + qr * RBS + 4 * g * ESZ, ds[0], ds[1], ds[2], ds[3], T());
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       Frag fa1, fa2;
-      frag_row<ImgS>(fa1, S1, lane & 15, 8 * g);
-      frag_row<ImgS>(fa2, S2, lane & 15, 8 * g);
+      frag_col<ImgS>(fa1, S1, 0, 0, lane);  // A(i = key, r = query)
+      frag_col<ImgS>(fa2, S2, 0, 0, lane);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         Frag fb;
@@ -317,20 +384,28 @@ __global__ __launch_bounds__(NT) void attn_bwd_kernel(AttnParams p) {
         mma16(dp, fo[0], fb);
         frag_row<Img>(fb, Vimg, kt * 16 + (lane & 15), 32 + 8 * g);
         mma16(dp, fo[1], fb);
+        // accumulator: row = query (4g + r), col = key
         const int key = kt * 16 + (lane & 15);
+        bool keep[4] = {true, true, true, true};
+        if (p.thresh) {
+          const uint64_t idx = drop_idx(bh, T_, qt * 16 + 4 * g, key);
+          nstl_keep2(p.seed, idx, p.thresh, keep[0], keep[1]);
+          nstl_keep2(p.seed, idx + 2, p.thresh, keep[2], keep[3]);
+        }
+        float ds[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int qr = 4 * g + r, q = qt * 16 + qr;
           const float pv = exp2f(s[r] * c2 - lq[r]);
           float dpd = dp[r];
-          if (p.thresh) dpd = nstl_keep(p.seed, drop_idx(bh, T_, q, key), p.thresh) ? dpd * p.inv_keep : 0.f;
-          const float ds = pv * (dpd - dqv[r]);
-          *(T*)(S2 + ImgS::off(qr, (u * 16 + (lane & 15)) * (int)sizeof(T))) = from_f32<T>(ds);
+          if (p.thresh) dpd = keep[r] ? dpd * p.inv_keep : 0.f;
+          ds[r] = pv * (dpd - dqv[r]);
         }
+        // transposed image [key][query]
+        put4(S2 + (u * 16 + (lane & 15)) * RBS + 4 * g * ESZ, ds[0], ds[1], ds[2], ds[3], T());
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       Frag fa;
-      frag_row<ImgS>(fa, S2, lane & 15, 8 * g);
+      frag_col<ImgS>(fa, S2, 0, 0, lane);  // A(i = query, r = key)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         Frag fb;
@@ -354,10 +429,10 @@ __global__ __launch_bounds__(NT) void attn_bwd_kernel(AttnParams p) {
 }
 
 size_t fwd_lds_bytes(int T, int esz) {
-  return (size_t)(2 * T + 64) * DH * esz + 4 * 16 * (size_t)(T * esz + 16);
+  return (size_t)(2 * T + 64) * DH * esz + 4 * (size_t)std::max(T, 64) * 16 * esz;
 }
 size_t bwd_lds_bytes(int T, int esz) {
-  return (size_t)4 * T * DH * esz + 2 * T * 4 + 4 * 2 * 16 * (size_t)(32 * esz + 16);
+  return (size_t)4 * T * DH * esz + 2 * T * 4 + 4 * 2 * 32 * 16 * (size_t)esz;
 }
 
 int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
@@ -369,11 +444,14 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   NSTL_CHECK_ARG(a->B > 0 && a->H > 0, "nstl_attn: empty batch");
   NSTL_CHECK_ARG(a->q && a->k && a->v && a->o && a->lse, "nstl_attn: null tensor");
   const int vec = a->dtype == NSTL_F32 ? 4 : 8;
-  NSTL_CHECK_ARG(a->q_ld % vec == 0 && a->k_ld % vec == 0 && a->v_ld % vec == 0, "nstl_attn: ld alignment");
+  NSTL_CHECK_ARG(a->q_ld % vec == 0 && a->k_ld % vec == 0 && a->v_ld % vec == 0 && a->o_ld % vec == 0,
+                 "nstl_attn: ld alignment");
+  NSTL_CHECK_ARG(((uintptr_t)a->q | (uintptr_t)a->k | (uintptr_t)a->v | (uintptr_t)a->o) % 16 == 0,
+                 "nstl_attn: tensors must be 16-byte aligned");
   NSTL_CHECK_ARG(a->p_drop >= 0.f && a->p_drop < 1.f, "nstl_attn: p_drop out of range");
   if (bwd) {
     NSTL_CHECK_ARG(a->dout && a->dq && a->dk && a->dv, "nstl_attn_bwd: null gradient tensor");
-    NSTL_CHECK_ARG(a->dout_ld % vec == 0, "nstl_attn_bwd: dout_ld alignment");
+    NSTL_CHECK_ARG(a->dout_ld % vec == 0 && (uintptr_t)a->dout % 16 == 0, "nstl_attn_bwd: dout alignment");
     NSTL_CHECK_ARG(!(a->rope_q || a->rope_k) || (a->rope_cos && a->rope_sin), "nstl_attn_bwd: rope tables");
   }
   p.q = (const char*)a->q; p.q_ld = a->q_ld;

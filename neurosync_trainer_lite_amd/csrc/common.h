@@ -118,21 +118,36 @@ NSTL_DEV void frag_col(f32x8& f, const char* img, int col16, int r0, int lane) {
 // ---------------------------------------------------------------------------
 // Counter-based dropout RNG: keep(seed, idx) is a pure function of its inputs,
 // so forward and backward regenerate the same mask without storing it.
-NSTL_DEV uint32_t nstl_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z = z ^ (z >> 31);
-  return (uint32_t)(z >> 32);
+// One 32-bit fmix (murmur3 finaliser) of the seed-keyed pair index gives two
+// 16-bit uniforms: elements 2k and 2k+1 take the low / high half.  The drop
+// probability is quantised to 1/65536 (0.3 -> 0.300003).
+NSTL_DEV uint32_t nstl_fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
-// p in [0,1): keep with probability 1-p.
+NSTL_DEV uint32_t nstl_pair_hash(uint64_t seed, uint64_t idx) {
+  const uint32_t s = (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x27D4EB2Fu) ^ ((uint32_t)(idx >> 33) * 0x165667B1u);
+  return nstl_fmix32((uint32_t)(idx >> 1) * 0x9E3779B1u ^ s);
+}
 NSTL_DEV bool nstl_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
-  return nstl_hash(seed, idx) >= thresh;
+  const uint32_t h = nstl_pair_hash(seed, idx);
+  return ((idx & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thresh;
 }
+// keep decisions for the pair (idx, idx+1), idx even: one hash
+NSTL_DEV void nstl_keep2(uint64_t seed, uint64_t idx, uint32_t thresh, bool& k0, bool& k1) {
+  const uint32_t h = nstl_pair_hash(seed, idx);
+  k0 = (h & 0xFFFFu) >= thresh;
+  k1 = (h >> 16) >= thresh;
+}
+// threshold on a 16-bit uniform; 0 = no dropout
 static inline uint32_t nstl_drop_thresh(float p) {
-  double t = (double)p * 4294967296.0;
-  if (t <= 0) return 0;
-  if (t >= 4294967295.0) return 0xFFFFFFFFu;
+  double t = (double)p * 65536.0 + 0.5;
+  if (p <= 0.f) return 0;
+  if (t >= 65536.0) return 65536u;
   return (uint32_t)t;
 }
 

@@ -64,9 +64,22 @@ NSTL_DEV void epi_store4(const GemmParams& p, int i, int j, f32x4 v) {
   }
   if (epi == NSTL_EPI_BIAS_RELU_DROP) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = fmaxf(v[e], 0.f);
-      if (p.thresh) v[e] = nstl_keep(p.seed, (uint64_t)i * p.N + j + e, p.thresh) ? v[e] * p.inv_keep : 0.f;
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    if (p.thresh) {
+      // (i*N + j) is even when N is even (j is a multiple of 4): two pair hashes
+      const uint64_t idx = (uint64_t)i * p.N + j;
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        bool k0, k1;
+        if ((idx & 1) == 0) {
+          nstl_keep2(p.seed, idx + e, p.thresh, k0, k1);
+        } else {
+          k0 = nstl_keep(p.seed, idx + e, p.thresh);
+          k1 = nstl_keep(p.seed, idx + e + 1, p.thresh);
+        }
+        v[e] = k0 ? v[e] * p.inv_keep : 0.f;
+        v[e + 1] = k1 ? v[e + 1] * p.inv_keep : 0.f;
+      }
     }
   } else if (epi == NSTL_EPI_BIAS_ROPE) {
     if (j < p.rope_cols) {
@@ -314,8 +327,16 @@ __global__ __launch_bounds__(BIG_NT, 2) void gemm256_kernel(GemmParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int nt_m = (p.M + BIG - 1) / BIG, nt_n = (p.N + BIG - 1) / BIG;
+  // XCD-contiguous id ranges, then grouped order (GROUP_M row tiles per group,
+  // column-fastest inside): an XCD's 32 co-resident blocks cover ~4 x 8 tiles,
+  // sharing 4 A panels and 8 B panels in its L2.
   const int id = xcd_remap(blockIdx.x, nt_m * nt_n);
-  const int tm = id / nt_n, tn = id % nt_n;
+  constexpr int GROUP_M = 4;
+  const int per_group = GROUP_M * nt_n;
+  const int first_m = (id / per_group) * GROUP_M;
+  const int gm = min(nt_m - first_m, GROUP_M);
+  const int in_g = id % per_group;
+  const int tm = first_m + in_g % gm, tn = in_g / gm;
   const int m0 = tm * BIG, n0 = tn * BIG;
   const int kz0 = blockIdx.y * p.k_chunk;
   const int kz1 = min(p.K, kz0 + p.k_chunk);
@@ -352,16 +373,23 @@ __global__ __launch_bounds__(BIG_NT, 2) void gemm256_kernel(GemmParams p) {
         else
           frag_col<ImgMN<B_RB>>(fb[t], Bi, wn * 64 + t * 16, kk * 32, lane);
       }
-      // one A fragment live at a time: read it, then its 4 MFMAs
+      // A fragments double-buffered in registers: the read of fragment a+1 is
+      // issued before the 4 MFMAs of fragment a
+      bf16x8 fa[2];
+      if (AK)
+        frag_row<ImgK<128>>(fa[0], Ai, wm * 128 + (lane & 15), kk * 32 + 8 * (lane >> 4));
+      else
+        frag_col<ImgMN<A_RB>>(fa[0], Ai, wm * 128, kk * 32, lane);
 #pragma unroll
       for (int a = 0; a < 8; ++a) {
-        bf16x8 fa;
-        if (AK)
-          frag_row<ImgK<128>>(fa, Ai, wm * 128 + a * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4));
-        else
-          frag_col<ImgMN<A_RB>>(fa, Ai, wm * 128 + a * 16, kk * 32, lane);
+        if (a + 1 < 8) {
+          if (AK)
+            frag_row<ImgK<128>>(fa[(a + 1) & 1], Ai, wm * 128 + (a + 1) * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4));
+          else
+            frag_col<ImgMN<A_RB>>(fa[(a + 1) & 1], Ai, wm * 128 + (a + 1) * 16, kk * 32, lane);
+        }
 #pragma unroll
-        for (int b = 0; b < 4; ++b) mma16(acc[a][b], fa, fb[b]);
+        for (int b = 0; b < 4; ++b) mma16(acc[a][b], fa[a & 1], fb[b]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

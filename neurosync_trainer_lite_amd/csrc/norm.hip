@@ -63,11 +63,14 @@ struct LnParams {
   float* dgp; float* dbp; float* dyp;
 };
 
-NSTL_DEV float branch_scale(const LnParams& p, uint64_t idx) {
-  float m = 1.f;
-  if (p.n_masks >= 1) m = nstl_keep(p.seed1, idx, p.thresh) ? p.inv_keep : 0.f;
-  if (p.n_masks >= 2) m = nstl_keep(p.seed2, idx, p.thresh) ? m * p.inv_keep : 0.f;
-  return m;
+// dropout scale of the element pair (idx, idx+1), idx even: 1 or 2 stacked masks
+NSTL_DEV void branch_scale2(const LnParams& p, uint64_t idx, float& m0, float& m1) {
+  bool a0, a1, b0 = true, b1 = true;
+  nstl_keep2(p.seed1, idx, p.thresh, a0, a1);
+  if (p.n_masks >= 2) nstl_keep2(p.seed2, idx, p.thresh, b0, b1);
+  const float s = p.n_masks >= 2 ? p.inv_keep * p.inv_keep : p.inv_keep;
+  m0 = (a0 && b0) ? s : 0.f;
+  m1 = (a1 && b1) ? s : 0.f;
 }
 
 template <typename T, int VPL>
@@ -81,7 +84,12 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnParams p) {
   load_row<T, VPL>((const T*)p.y + base, s);
   if (p.thresh && p.n_masks > 0) {
 #pragma unroll
-    for (int j = 0; j < VPL; ++j) s[j] *= branch_scale(p, (uint64_t)base + j);
+    for (int j = 0; j < VPL; j += 2) {
+      float m0, m1;
+      branch_scale2(p, (uint64_t)base + j, m0, m1);
+      s[j] *= m0;
+      s[j + 1] *= m1;
+    }
   }
   if (p.x) {
     float xv[VPL];
@@ -162,7 +170,12 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(LnParams p) {
     if (p.dbranch) {
       if (p.thresh && p.n_masks > 0) {
 #pragma unroll
-        for (int j = 0; j < VPL; ++j) d[j] *= branch_scale(p, (uint64_t)base + j);
+        for (int j = 0; j < VPL; j += 2) {
+          float m0, m1;
+          branch_scale2(p, (uint64_t)base + j, m0, m1);
+          d[j] *= m0;
+          d[j + 1] *= m1;
+        }
       }
 #pragma unroll
       for (int j = 0; j < VPL; ++j) d[j] = to_f32(from_f32<T>(d[j]));  // sum what is stored
