@@ -175,6 +175,21 @@ int nstl_cast(int src_dtype, const void* src, int dst_dtype, void* dst, int64_t 
 int nstl_autocorr(const float* y, int64_t n_samples, int frame_length, int hop_length, int n_lags,
                   double* out, int n_frames, void* stream);
 
+/* Combined per-clip audio features: extract_and_combine_features after the
+ * load (utils/audio/extraction/extract_features.py:6-46 with
+ * extract_features_utils.py:5-44,54-128): MFCC(23, CMVN) + delta + delta2
+ * (Savitzky-Golay width 9, mode 'interp') and autocorrelation lags 1..187,
+ * STFT frames (n_fft = int(0.01667 sr), hop n_fft/2) reduced by frame pairs.
+ * y: f32 [n_samples] peak-normalised audio at sr; out: f32 [n_out_frames][ld_out],
+ * columns 0..255 = [mfcc | d | dd | autocorr].  n_out_frames must equal
+ * nstl_features_frames(); the caller rejects clips with fewer than 9 frames
+ * (extract_features.py:19-21), the library returns hipErrorInvalidValue.
+ * Workspace (caller-owned): nstl_features_workspace_bytes(). */
+int nstl_features(const float* y, int64_t n_samples, int sr, float* out, int64_t ld_out, int n_out_frames,
+                  void* workspace, int64_t workspace_bytes, void* stream);
+int64_t nstl_features_workspace_bytes(int64_t n_samples, int sr);
+int nstl_features_frames(int64_t n_samples, int sr);
+
 const char* nstl_last_error_string(void);
 int nstl_version(void);
 

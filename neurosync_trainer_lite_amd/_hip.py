@@ -86,7 +86,8 @@ class AdamArgs(ctypes.Structure):
 EXPORTS = [
     "nstl_gemm", "nstl_gemm_workspace_bytes", "nstl_attn_fwd", "nstl_attn_bwd", "nstl_ln_fwd", "nstl_ln_bwd",
     "nstl_reduce_rows", "nstl_colsum", "nstl_rope", "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step",
-    "nstl_cast", "nstl_copy2d", "nstl_autocorr", "nstl_last_error_string", "nstl_version",
+    "nstl_cast", "nstl_copy2d", "nstl_autocorr", "nstl_features", "nstl_features_workspace_bytes",
+    "nstl_features_frames", "nstl_last_error_string", "nstl_version",
 ]
 
 _lib = None
@@ -118,6 +119,11 @@ def lib():
         L.nstl_cast.argtypes = [_i32, _vp, _i32, _vp, _i64, _vp]
         L.nstl_copy2d.argtypes = [_i32, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp]
         L.nstl_autocorr.argtypes = [_vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp]
+        L.nstl_features.argtypes = [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _i64, _vp]
+        L.nstl_features_workspace_bytes.argtypes = [_i64, _i32]
+        L.nstl_features_workspace_bytes.restype = _i64
+        L.nstl_features_frames.argtypes = [_i64, _i32]
+        L.nstl_features_frames.restype = _i32
         L.nstl_last_error_string.restype = ctypes.c_char_p
         L.nstl_version.restype = _i32
         _lib = L
@@ -181,10 +187,10 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     check(lib().nstl_gemm(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_gemm")
 
 
-def attn_args(dtype, B, T, H, q, q_ld, k, k_ld, v, v_ld, o, o_ld, lse, p_drop, seed):
+def attn_args(dtype, B, T, H, q, q_ld, k, k_ld, v, v_ld, o, o_ld, lse, p_drop, seed, dh=64):
     a = AttnArgs()
     a.dtype = dtype
-    a.B, a.T, a.H, a.dh = B, T, H, 64
+    a.B, a.T, a.H, a.dh = B, T, H, dh
     a.q, a.q_ld, a.k, a.k_ld, a.v, a.v_ld = q, q_ld, k, k_ld, v, v_ld
     a.o, a.o_ld, a.lse = o, o_ld, lse
     a.p_drop, a.seed = p_drop, seed & 0xFFFFFFFFFFFFFFFF
@@ -252,3 +258,18 @@ def copy2d(src, src_ld, dst, dst_ld, rows, cols, dst_cols, scale=None, stream=No
 def autocorr(y, frame_length, hop_length, n_lags, out, n_frames, stream=None):
     check(lib().nstl_autocorr(y.data_ptr(), y.numel(), frame_length, hop_length, n_lags, out.data_ptr(), n_frames,
                               stream if stream is not None else stream_of()), "nstl_autocorr")
+
+
+def features_frames(n_samples, sr):
+    return lib().nstl_features_frames(n_samples, sr)
+
+
+def features_workspace_bytes(n_samples, sr):
+    return lib().nstl_features_workspace_bytes(n_samples, sr)
+
+
+def features(y, sr, out, workspace, stream=None):
+    """y: f32 [S] on the device -> out f32 [F60, >=256] (see include/nstl.h)."""
+    check(lib().nstl_features(y.data_ptr(), y.numel(), sr, out.data_ptr(), out.stride(0), out.shape[0],
+                              workspace.data_ptr(), workspace.numel() * workspace.element_size(),
+                              stream if stream is not None else stream_of()), "nstl_features")

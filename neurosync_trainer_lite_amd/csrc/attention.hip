@@ -39,7 +39,7 @@ struct AttnParams {
   char* dk; int64_t dk_ld;
   char* dv; int64_t dv_ld;
   const float* rope_cos; const float* rope_sin; int rope_q, rope_k;
-  int B, T, H;
+  int B, T, H, dh;
   float scale;
   uint32_t thresh; float inv_keep; uint64_t seed;
 };
@@ -435,12 +435,232 @@ size_t bwd_lds_bytes(int T, int esz) {
   return (size_t)4 * T * DH * esz + 2 * T * 4 + 4 * 2 * 32 * 16 * (size_t)esz;
 }
 
+// ---------------------------------------------------------------------------
+// Generic path: any even head_dim that is a multiple of 8 (<= 512) and any T
+// (<= 4096).  One wave per query row (forward, dq) or per key row (dk, dv);
+// the wave's own row is staged in LDS as f32, the other operand's rows stream
+// from global memory (L2-resident per (b, h)), softmax rows live in LDS.  It
+// serves the shapes the MFMA kernels above do not (e.g. BASELINE C1: 4 heads
+// of 256) with the same dropout stream (drop_idx / nstl_keep), scale, LSE and
+// RoPE^T conventions, so the two paths are interchangeable.
+// ---------------------------------------------------------------------------
+constexpr int G_MAX_DH = 512, G_MAX_T = 4096;
+
+NSTL_DEV void load8(const bf16* g, float* v) {
+  const bf16x8 x = *(const bf16x8*)g;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = (float)x[k];
+}
+NSTL_DEV void load8(const float* g, float* v) {
+  const f32x4 a = *(const f32x4*)g, b = *(const f32x4*)(g + 4);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = a[k];
+    v[4 + k] = b[k];
+  }
+}
+
+// dot(global row g[0..dh), LDS f32 row s[0..dh))
+template <typename T>
+NSTL_DEV float dot_gs(const T* g, const float* s, int dh) {
+  float acc = 0.f;
+  for (int d = 0; d < dh; d += 8) {
+    float v[8];
+    load8(g + d, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = fmaf(v[k], s[d + k], acc);
+  }
+  return acc;
+}
+
+template <typename T>
+NSTL_DEV float dot_gg(const T* a, const T* b, int dh) {
+  float acc = 0.f;
+  for (int d = 0; d < dh; d += 8) {
+    float x[8], y[8];
+    load8(a + d, x);
+    load8(b + d, y);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = fmaf(x[k], y[k], acc);
+  }
+  return acc;
+}
+
+template <typename T>
+NSTL_DEV const T* row_ptr(const char* base, int64_t ld, int64_t tok, int h, int dh) {
+  return (const T*)base + tok * ld + (int64_t)h * dh;
+}
+
+// RoPE^T on a row held as (d = i*64 + lane): the pair partner is lane ^ 1
+NSTL_DEV float rope_back_g(float v, int t, int d, int dh, const float* cs, const float* sn) {
+  const float partner = __shfl_xor(v, 1);
+  if (d >= dh) return v;
+  const float c = cs[t * (dh / 2) + (d >> 1)], s = sn[t * (dh / 2) + (d >> 1)];
+  return (d & 1) ? (v * c - partner * s) : (v * c + partner * s);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_generic(AttnParams p) {
+  extern __shared__ float gsm[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int T_ = p.T, dh = p.dh, bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int q = blockIdx.x * 4 + w;
+  const bool act = q < T_;
+  float* qs = gsm + w * (dh + T_);
+  float* sc = qs + dh;
+  const int64_t tok0 = (int64_t)b * T_;
+  if (act) {
+    const T* qr = row_ptr<T>(p.q, p.q_ld, tok0 + q, h, dh);
+    for (int d = lane; d < dh; d += 64) qs[d] = to_f32(qr[d]);
+  }
+  __syncthreads();
+  if (act) {
+    float mx = -INFINITY;
+    for (int j = lane; j < T_; j += 64) {
+      const float sv = dot_gs(row_ptr<T>(p.k, p.k_ld, tok0 + j, h, dh), qs, dh) * p.scale;
+      sc[j] = sv;
+      mx = fmaxf(mx, sv);
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int j = lane; j < T_; j += 64) sum += expf(sc[j] - mx);
+    sum = wave_sum(sum);
+    const float lse = mx + logf(sum);
+    for (int j = lane; j < T_; j += 64) {
+      float pv = expf(sc[j] - lse);
+      if (p.thresh) pv = nstl_keep(p.seed, drop_idx(bh, T_, q, j), p.thresh) ? pv * p.inv_keep : 0.f;
+      sc[j] = pv;
+    }
+    if (lane == 0) p.lse[(int64_t)bh * T_ + q] = lse;
+  }
+  __syncthreads();
+  if (act) {
+    for (int d = lane; d < dh; d += 64) {
+      float acc = 0.f;
+      for (int j = 0; j < T_; ++j) acc = fmaf(sc[j], to_f32(row_ptr<T>(p.v, p.v_ld, tok0 + j, h, dh)[d]), acc);
+      store_elem<T>(p.o, (tok0 + q) * p.o_ld + (int64_t)h * dh + d, acc);
+    }
+  }
+}
+
+// dq (one wave per query row)
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_dq_generic(AttnParams p) {
+  extern __shared__ float gsm[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int T_ = p.T, dh = p.dh, bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int q = blockIdx.x * 4 + w;
+  const bool act = q < T_;
+  float* qs = gsm + w * (2 * dh + T_);
+  float* dos = qs + dh;
+  float* sc = dos + dh;
+  const int64_t tok0 = (int64_t)b * T_;
+  float Dq = 0.f;
+  if (act) {
+    const T* qr = row_ptr<T>(p.q, p.q_ld, tok0 + q, h, dh);
+    const T* dr = row_ptr<T>(p.dout, p.dout_ld, tok0 + q, h, dh);
+    const T* orow = row_ptr<T>(p.o, p.o_ld, tok0 + q, h, dh);
+    for (int d = lane; d < dh; d += 64) {
+      qs[d] = to_f32(qr[d]);
+      const float g = to_f32(dr[d]);
+      dos[d] = g;
+      Dq = fmaf(g, to_f32(orow[d]), Dq);
+    }
+    Dq = wave_sum(Dq);
+  }
+  __syncthreads();
+  if (act) {
+    const float lse = p.lse[(int64_t)bh * T_ + q];
+    for (int j = lane; j < T_; j += 64) {
+      const float pv = expf(dot_gs(row_ptr<T>(p.k, p.k_ld, tok0 + j, h, dh), qs, dh) * p.scale - lse);
+      float dp = dot_gs(row_ptr<T>(p.v, p.v_ld, tok0 + j, h, dh), dos, dh);
+      if (p.thresh) dp = nstl_keep(p.seed, drop_idx(bh, T_, q, j), p.thresh) ? dp * p.inv_keep : 0.f;
+      sc[j] = pv * (dp - Dq);
+    }
+  }
+  __syncthreads();
+  if (act) {
+    for (int d0 = 0; d0 < dh; d0 += 64) {
+      const int d = d0 + lane;
+      float acc = 0.f;
+      if (d < dh)
+        for (int j = 0; j < T_; ++j) acc = fmaf(sc[j], to_f32(row_ptr<T>(p.k, p.k_ld, tok0 + j, h, dh)[d]), acc);
+      float v = acc * p.scale;
+      if (p.rope_q) v = rope_back_g(v, q, d, dh, p.rope_cos, p.rope_sin);
+      if (d < dh) store_elem<T>(p.dq, (tok0 + q) * p.dq_ld + (int64_t)h * dh + d, v);
+    }
+  }
+}
+
+// dk, dv (one wave per key row)
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_generic(AttnParams p) {
+  extern __shared__ float gsm[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int T_ = p.T, dh = p.dh, bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int j = blockIdx.x * 4 + w;
+  const bool act = j < T_;
+  float* ks = gsm + w * (2 * dh + 2 * T_);
+  float* vs = ks + dh;
+  float* pd = vs + dh;
+  float* ds = pd + T_;
+  const int64_t tok0 = (int64_t)b * T_;
+  if (act) {
+    const T* kr = row_ptr<T>(p.k, p.k_ld, tok0 + j, h, dh);
+    const T* vr = row_ptr<T>(p.v, p.v_ld, tok0 + j, h, dh);
+    for (int d = lane; d < dh; d += 64) {
+      ks[d] = to_f32(kr[d]);
+      vs[d] = to_f32(vr[d]);
+    }
+  }
+  __syncthreads();
+  if (act) {
+    for (int i = lane; i < T_; i += 64) {
+      const T* dr = row_ptr<T>(p.dout, p.dout_ld, tok0 + i, h, dh);
+      const float pv = expf(dot_gs(row_ptr<T>(p.q, p.q_ld, tok0 + i, h, dh), ks, dh) * p.scale -
+                            p.lse[(int64_t)bh * T_ + i]);
+      float dp = dot_gs(dr, vs, dh);
+      const float Di = dot_gg(dr, row_ptr<T>(p.o, p.o_ld, tok0 + i, h, dh), dh);
+      float pdv = pv;
+      if (p.thresh) {
+        const bool keep = nstl_keep(p.seed, drop_idx(bh, T_, i, j), p.thresh);
+        pdv = keep ? pv * p.inv_keep : 0.f;
+        dp = keep ? dp * p.inv_keep : 0.f;
+      }
+      pd[i] = pdv;
+      ds[i] = pv * (dp - Di);
+    }
+  }
+  __syncthreads();
+  if (act) {
+    for (int d0 = 0; d0 < dh; d0 += 64) {
+      const int d = d0 + lane;
+      float av = 0.f, ak = 0.f;
+      if (d < dh)
+        for (int i = 0; i < T_; ++i) {
+          av = fmaf(pd[i], to_f32(row_ptr<T>(p.dout, p.dout_ld, tok0 + i, h, dh)[d]), av);
+          ak = fmaf(ds[i], to_f32(row_ptr<T>(p.q, p.q_ld, tok0 + i, h, dh)[d]), ak);
+        }
+      float vk = ak * p.scale;
+      if (p.rope_k) vk = rope_back_g(vk, j, d, dh, p.rope_cos, p.rope_sin);
+      if (d < dh) {
+        store_elem<T>(p.dk, (tok0 + j) * p.dk_ld + (int64_t)h * dh + d, vk);
+        store_elem<T>(p.dv, (tok0 + j) * p.dv_ld + (int64_t)h * dh + d, av);
+      }
+    }
+  }
+}
+
+bool use_fast(const nstl_attn_args* a) {
+  return a->dh == DH && a->T % 32 == 0 && a->T <= (a->dtype == NSTL_BF16 ? 256 : 128);
+}
+
 int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   NSTL_CHECK_ARG(a != nullptr, "nstl_attn: null args");
   NSTL_CHECK_ARG(a->dtype == NSTL_F32 || a->dtype == NSTL_BF16, "nstl_attn: bad dtype");
-  NSTL_CHECK_ARG(a->dh == DH, "nstl_attn: head_dim must be 64 (got %d)", a->dh);
-  NSTL_CHECK_ARG(a->T > 0 && a->T % 32 == 0, "nstl_attn: T must be a positive multiple of 32 (got %d)", a->T);
-  NSTL_CHECK_ARG(a->T <= (a->dtype == NSTL_BF16 ? 256 : 128), "nstl_attn: T=%d too long for this dtype", a->T);
+  NSTL_CHECK_ARG(a->dh > 0 && a->dh % 8 == 0 && a->dh <= G_MAX_DH,
+                 "nstl_attn: head_dim must be a multiple of 8 up to %d (got %d)", G_MAX_DH, a->dh);
+  NSTL_CHECK_ARG(a->T > 0 && a->T <= G_MAX_T, "nstl_attn: T must be in [1, %d] (got %d)", G_MAX_T, a->T);
   NSTL_CHECK_ARG(a->B > 0 && a->H > 0, "nstl_attn: empty batch");
   NSTL_CHECK_ARG(a->q && a->k && a->v && a->o && a->lse, "nstl_attn: null tensor");
   const int vec = a->dtype == NSTL_F32 ? 4 : 8;
@@ -465,7 +685,7 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   p.dv = (char*)a->dv; p.dv_ld = a->dv_ld;
   p.rope_cos = a->rope_cos; p.rope_sin = a->rope_sin;
   p.rope_q = a->rope_q; p.rope_k = a->rope_k;
-  p.B = a->B; p.T = a->T; p.H = a->H;
+  p.B = a->B; p.T = a->T; p.H = a->H; p.dh = a->dh;
   p.scale = 1.0f / sqrtf((float)a->dh);
   p.thresh = nstl_drop_thresh(a->p_drop);
   p.inv_keep = 1.0f / (1.0f - a->p_drop);
@@ -489,10 +709,17 @@ extern "C" int nstl_attn_fwd(const nstl_attn_args* a, void* stream) {
   int rc = fill(p, a, false);
   if (rc) return rc;
   const int esz = a->dtype == NSTL_F32 ? 4 : 2;
+  hipStream_t st = (hipStream_t)stream;
+  if (!use_fast(a)) {
+    dim3 grid((a->T + 3) / 4, a->B * a->H);
+    const size_t lds = 4 * (size_t)(a->dh + a->T) * 4;
+    if (a->dtype == NSTL_BF16) return launch(attn_fwd_generic<bf16>, grid, lds, st, p, "nstl_attn_fwd generic");
+    return launch(attn_fwd_generic<float>, grid, lds, st, p, "nstl_attn_fwd generic");
+  }
   dim3 grid((a->T + 63) / 64, a->B * a->H);
   const size_t lds = fwd_lds_bytes(a->T, esz);
-  if (a->dtype == NSTL_BF16) return launch(attn_fwd_kernel<bf16>, grid, lds, (hipStream_t)stream, p, "nstl_attn_fwd");
-  return launch(attn_fwd_kernel<float>, grid, lds, (hipStream_t)stream, p, "nstl_attn_fwd");
+  if (a->dtype == NSTL_BF16) return launch(attn_fwd_kernel<bf16>, grid, lds, st, p, "nstl_attn_fwd");
+  return launch(attn_fwd_kernel<float>, grid, lds, st, p, "nstl_attn_fwd");
 }
 
 extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
@@ -500,8 +727,19 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
   int rc = fill(p, a, true);
   if (rc) return rc;
   const int esz = a->dtype == NSTL_F32 ? 4 : 2;
+  hipStream_t st = (hipStream_t)stream;
+  if (!use_fast(a)) {
+    dim3 grid((a->T + 3) / 4, a->B * a->H);
+    const size_t lq = 4 * (size_t)(2 * a->dh + a->T) * 4, lkv = 4 * (size_t)(2 * a->dh + 2 * a->T) * 4;
+    if (a->dtype == NSTL_BF16) {
+      if ((rc = launch(attn_bwd_dq_generic<bf16>, grid, lq, st, p, "nstl_attn_bwd generic dq"))) return rc;
+      return launch(attn_bwd_dkv_generic<bf16>, grid, lkv, st, p, "nstl_attn_bwd generic dkv");
+    }
+    if ((rc = launch(attn_bwd_dq_generic<float>, grid, lq, st, p, "nstl_attn_bwd generic dq"))) return rc;
+    return launch(attn_bwd_dkv_generic<float>, grid, lkv, st, p, "nstl_attn_bwd generic dkv");
+  }
   dim3 grid(a->B * a->H);
   const size_t lds = bwd_lds_bytes(a->T, esz);
-  if (a->dtype == NSTL_BF16) return launch(attn_bwd_kernel<bf16>, grid, lds, (hipStream_t)stream, p, "nstl_attn_bwd");
-  return launch(attn_bwd_kernel<float>, grid, lds, (hipStream_t)stream, p, "nstl_attn_bwd");
+  if (a->dtype == NSTL_BF16) return launch(attn_bwd_kernel<bf16>, grid, lds, st, p, "nstl_attn_bwd");
+  return launch(attn_bwd_kernel<float>, grid, lds, st, p, "nstl_attn_bwd");
 }

@@ -123,6 +123,7 @@ class Seq2SeqEngine:
         self.out_dim = dec.fc_output.out_features
         self.L = len(enc.transformer_encoder)
         self.H = enc.transformer_encoder[0].self_attn.num_heads
+        self.dh = self.D // self.H
         self.Fd = enc.transformer_encoder[0].ffn.linear1.out_features
         self.dropout = model.dropout_p
         self._check_shapes()
@@ -133,12 +134,13 @@ class Seq2SeqEngine:
         self.grads_fresh = True
         self.grad_reducer = None   # parallel.GradAllReducer when data-parallel
         self.grad_scale_t = None   # device f32 [1]: loss-gradient pre-scale (1/world)
+        self.seed_salt = 0         # data-parallel rank: distinct dropout streams per replica
 
     # ------------------------------------------------------------------ setup
     def _check_shapes(self):
         D, H = self.D, self.H
-        if D % H or D // H != 64:
-            raise ValueError("MI355X kernels need head_dim == 64 (hidden_dim=%d, num_heads=%d)" % (D, H))
+        if D % H or (D // H) % 8 or D // H > 512:
+            raise ValueError("head_dim must be a multiple of 8 up to 512 (hidden_dim=%d, num_heads=%d)" % (D, H))
         if D % 128 or D > 1024:
             raise ValueError("hidden_dim must be a multiple of 128 and <= 1024 (got %d)" % D)
         if self.out_dim > 64:
@@ -359,16 +361,18 @@ class Seq2SeqEngine:
 
     def _attn(self, q, k, v, o, lse, seed, T, B):
         a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
-                        v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed)
+                        v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed,
+                        dh=self.dh)
         K.attn_fwd(a, stream=self.st)
 
     def _attn_bwd(self, q, k, v, o, lse, do, dq, dk, dv, seed, T, B):
         a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
-                        v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed)
+                        v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed,
+                        dh=self.dh)
         a.dout, a.dout_ld = do.data_ptr(), do.stride(0)
         a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dq.data_ptr(), dq.stride(0), dk.data_ptr(), dk.stride(0),
                                                         dv.data_ptr(), dv.stride(0))
-        cs, sn = self.rope(T, 64)
+        cs, sn = self.rope(T, self.dh)
         a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
         K.attn_bwd(a, stream=self.st)
 
@@ -379,7 +383,7 @@ class Seq2SeqEngine:
         sd = lambda s: _seed(self.base_seed, True, l, s)
         qkv, o, lse = bb.layer(bb.e_qkv, l), bb.layer(bb.e_o, l), bb.layer(bb.e_lse, l)
         self._gemm_fwd(x, pre + "self_attn.q_linear.weight", qkv, K.EPI_BIAS_ROPE, rows=3,
-                       rope=(*self.rope(T, 64), T, 64), rope_cols=2 * D)
+                       rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=2 * D)
         self._attn(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, sd("attn"), T, B)
         self._gemm_fwd(o, pre + "self_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         st = bb.layer(bb.e_stats, l)
@@ -400,16 +404,16 @@ class Seq2SeqEngine:
         st = L_(bb.d_stats)
         qkv = L_(bb.d_qkv)
         self._gemm_fwd(x, pre + "self_attn.q_linear.weight", qkv, K.EPI_BIAS_ROPE, rows=3,
-                       rope=(*self.rope(T, 64), T, 64), rope_cols=2 * D)
+                       rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=2 * D)
         self._attn(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], L_(bb.d_o), L_(bb.d_lse), sd("attn"), T, B)
         self._gemm_fwd(L_(bb.d_o), pre + "self_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         x1 = L_(bb.d_x1)
         self._ln(x, bb.y, x1, st[0:2], pre + "norm1", 2, (sd("resid"), sd("drop1")), L_(bb.d_s1))
         qc, kvc = L_(bb.d_qc), L_(bb.d_kvc)
         self._gemm_fwd(x1, pre + "multihead_attn.q_linear.weight", qc, K.EPI_BIAS_ROPE,
-                       rope=(*self.rope(T, 64), T, 64), rope_cols=D)
+                       rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D)
         self._gemm_fwd(mem, pre + "multihead_attn.k_linear.weight", kvc, K.EPI_BIAS_ROPE, rows=2,
-                       rope=(*self.rope(T, 64), T, 64), rope_cols=D)
+                       rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D)
         self._attn(qc, kvc[:, :D], kvc[:, D:], L_(bb.d_oc), L_(bb.d_lsec), sd("xattn"), T, B)
         self._gemm_fwd(L_(bb.d_oc), pre + "multihead_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         x2 = L_(bb.d_x2)
@@ -457,10 +461,17 @@ class Seq2SeqEngine:
         self._gemm_fwd(bb.xf, "decoder.fc_output.weight", pred, K.EPI_BIAS)
         return pred
 
+    def draw_seed(self):
+        """Dropout seed of one forward: torch's RNG (so torch.manual_seed reproduces
+        a run) mixed with the replica's rank."""
+        if self.p <= 0:
+            return 0
+        return (int(torch.randint(0, 2 ** 62, (1,)).item()) + self.seed_salt * 0x9E3779B97F4A7C15) % (1 << 62)
+
     def forward(self, src, training, save):
         B, T, _ = src.shape
         self._prologue(training)
-        self.base_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self.p > 0 else 0
+        self.base_seed = self.draw_seed()
         bb = self.bufs(B, T, save)
         mem = self.encode(bb, src, T)
         pred = self.decode(bb, mem, T, xdec0=bb.xdec0)

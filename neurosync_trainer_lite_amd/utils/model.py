@@ -161,7 +161,7 @@ class Encoder(nn.Module):
             raise RuntimeError("Encoder must belong to a Seq2Seq to run")
         with torch.no_grad():
             eng._prologue(self.training)
-            eng.base_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if eng.p > 0 else 0
+            eng.base_seed = eng.draw_seed()
             B, T, _ = x.shape
             bb = eng.bufs(B, T, False)
             mem = eng.encode(bb, x, T)
@@ -191,7 +191,7 @@ class Decoder(nn.Module):
             raise RuntimeError("Decoder must belong to a Seq2Seq to run")
         with torch.no_grad():
             eng._prologue(self.training)
-            eng.base_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if eng.p > 0 else 0
+            eng.base_seed = eng.draw_seed()
             B, T, D = encoder_outputs.shape
             bb = eng.bufs(B, T, False)
             mem = bb.mem

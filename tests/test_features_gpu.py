@@ -1,0 +1,106 @@
+"""GPU feature path (nstl_features / nstl_autocorr) against the CPU oracle and
+the reference-generated autocorrelation fixture; the drop-in
+extract_audio_features on a WAV file; batched clip inference vs the reference's
+per-chunk loop; a full-width C1 training run through train.main."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import data_ref
+from tests.golden.make_goldens_helpers import synth_audio
+
+pytestmark = pytest.mark.gpu
+
+
+def _features(y, sr=88200):
+    from neurosync_trainer_lite_amd.utils.audio.extraction.extract_features import extract_audio_features_device
+    out = extract_audio_features_device(y, sr, device=torch.device("cuda:0"))
+    torch.cuda.synchronize()
+    return None if out is None else out.double().cpu().numpy()
+
+
+def test_autocorr_matches_reference_fixture(golden):
+    g = golden("features_autocorr.npz")
+    cases = [(synth_audio(1.0, 3), g["ac_3"]), (synth_audio(0.73, 4), g["ac_4"])]
+    y = synth_audio(0.5, 5)
+    y[:3000] = 0
+    y[-3000:] = 0
+    cases.append((y, g["ac_silent_edges"]))
+    for y, want in cases:
+        got = _features(y)[:, 69:]
+        # f64 lags, f32 output
+        np.testing.assert_allclose(got, want, rtol=2e-6, atol=2e-7)
+
+
+@pytest.mark.parametrize("seconds,seed", [(1.0, 3), (0.73, 4), (2.5, 6), (0.09, 7)])
+def test_features_match_oracle(seconds, seed):
+    y = synth_audio(seconds, seed)
+    want = data_ref.extract_features(y)
+    got = _features(y)
+    assert got.shape == want.shape == ((1 + len(y) // 735 + 1) // 2, 256)
+    # MFCC branch (librosa restated; parity vs librosa itself unpinned): CMVN'd
+    # coefficients and deltas are O(1); f32 DFT-GEMM/mel/DCT vs the f64 oracle
+    np.testing.assert_allclose(got[:, :69], want[:, :69], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(got[:, 69:], want[:, 69:], rtol=2e-6, atol=2e-7)
+
+
+def test_features_short_clip_rejected():
+    assert _features(np.zeros(1470 + 7 * 735, np.float32) + 0.1) is None  # 8 frames
+    assert _features(synth_audio(9 * 735 / 88200 + 1470 / 88200, 8)) is not None
+
+
+def test_extract_audio_features_from_wav(tmp_path):
+    from neurosync_trainer_lite_amd.utils.audio.extraction.extract_features import extract_audio_features
+    from neurosync_trainer_lite_amd.utils.audio.load_audio import write_wav
+    y = synth_audio(1.5, 9)
+    p = tmp_path / "a.wav"
+    write_wav(str(p), y, 88200, bits=32)
+    feats, yy = extract_audio_features(str(p))
+    assert feats.dtype == np.float64 and feats.shape == ((1 + len(y) // 735 + 1) // 2, 256)
+    want = data_ref.extract_features(yy)
+    np.testing.assert_allclose(feats[:, 69:], want[:, 69:], rtol=2e-6, atol=2e-7)
+    np.testing.assert_allclose(feats[:, :69], want[:, :69], atol=2e-3)
+
+
+def test_batched_inference_matches_per_chunk_loop():
+    from neurosync_trainer_lite_amd.config import training_config
+    from neurosync_trainer_lite_amd.utils.audio.processing import audio_processing as ap
+    from neurosync_trainer_lite_amd.utils.model_utils import build_model
+    from oracle import model_ref
+    from tests.test_host_cpu import _reference_process
+    cfg = dict(training_config)
+    cfg.update(hidden_dim=128, num_heads=2, n_layers=2, use_amp=False)
+    dev = torch.device("cuda:0")
+    model = build_model(cfg, dev)
+    model.load_state_dict(model_ref.seeded_params(model_ref.param_shapes(256, 128, 2, 61), 3), strict=True)
+    model.eval()
+    feats = np.random.default_rng(0).standard_normal((700, 256))
+
+    def decode(chunk):
+        return ap.decode_audio_chunk(chunk, model, dev)
+
+    want = _reference_process(feats, decode, 128, 16)
+    got = ap.process_audio_features(feats, model, dev, cfg)
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6)
+
+
+def test_c1_train_main_full_width(tmp_path, monkeypatch):
+    """C1 shape (L4/H4/D1024) through the drop-in entry point: GPU feature
+    extraction (no cache), dataset, 1 epoch, checkpoint, validation clip."""
+    from neurosync_trainer_lite_amd import train as tr
+    from neurosync_trainer_lite_amd.config import training_config
+    from tests.test_train_plumbing import make_corpus
+    monkeypatch.chdir(tmp_path)
+    clip = make_corpus(str(tmp_path), cache_features=False)
+    cfg = dict(training_config)
+    cfg.update(n_layers=4, num_heads=4, hidden_dim=1024, n_epochs=1, batch_size=128,
+               audio_path=os.path.join(clip, "audio.wav"),
+               ground_truth_path=os.path.join(clip, "synth_iPhone_cal.csv"))
+    steps = tr.main(cfg)
+    assert steps > 0
+    assert os.path.exists(os.path.join(clip, "audio_features.csv"))
+    assert os.path.exists("out/model.pth") and os.path.exists(cfg["checkpoint_path"])
+    stats = open("dataset/validation_plots/stats/comparison_stats_epoch_1.txt").read()
+    assert "Mean Squared Error (MSE)" in stats

@@ -158,29 +158,32 @@ def rope_back_ref(g, cs, sn):
     return r
 
 
-@pytest.mark.parametrize("dt,T", [(torch.float32, 32), (torch.float32, 128), (torch.bfloat16, 64),
-                                  (torch.bfloat16, 128), (torch.bfloat16, 256)])
-def test_attention_fwd_bwd(dt, T):
-    B, H, dh = 2, 3, 64
+@pytest.mark.parametrize("dt,T,dh", [(torch.float32, 32, 64), (torch.float32, 128, 64), (torch.bfloat16, 64, 64),
+                                     (torch.bfloat16, 128, 64), (torch.bfloat16, 256, 64),
+                                     # generic kernels: ragged T, head_dim != 64 (BASELINE C1: 4 x 256)
+                                     (torch.float32, 48, 64), (torch.bfloat16, 100, 128),
+                                     (torch.float32, 128, 256), (torch.bfloat16, 128, 256), (torch.float32, 7, 24)])
+def test_attention_fwd_bwd(dt, T, dh):
+    B, H = 2, 3
     M, D = B * T, H * dh
     qkv = rnd(M, 3 * D, dtype=dt, seed=20)
     o = torch.empty(M, D, dtype=dt, device=DEV)
     lse = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
     code = K.dtype_code(dt)
     a = K.attn_args(code, B, T, H, qkv.data_ptr(), 3 * D, qkv[:, D:].data_ptr(), 3 * D, qkv[:, 2 * D:].data_ptr(),
-                    3 * D, o.data_ptr(), D, lse.data_ptr(), 0.0, 0)
+                    3 * D, o.data_ptr(), D, lse.data_ptr(), 0.0, 0, dh=dh)
     K.attn_fwd(a)
     torch.cuda.synchronize()
     q = f64(qkv[:, :D]).view(B, T, H, dh).transpose(1, 2).requires_grad_(True)
     k = f64(qkv[:, D:2 * D]).view(B, T, H, dh).transpose(1, 2).requires_grad_(True)
     v = f64(qkv[:, 2 * D:]).view(B, T, H, dh).transpose(1, 2).requires_grad_(True)
-    ro, rl = attn_ref(q, k, v, 1 / 8.0)
+    ro, rl = attn_ref(q, k, v, dh ** -0.5)
     tol = 5e-6 if dt == torch.float32 else 1e-2
     check(o, ro.transpose(1, 2).reshape(M, D), tol, "attn out")
     check(lse, rl.reshape(-1), 1e-5 if dt == torch.float32 else 1e-2, "attn lse")
     do = rnd(M, D, dtype=dt, seed=21)
     dqkv = torch.zeros(M, 3 * D, dtype=dt, device=DEV)
-    cs, sn = rotation_tables(T, 64, DEV)
+    cs, sn = rotation_tables(T, dh, DEV)
     a.dout, a.dout_ld = do.data_ptr(), D
     a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dqkv.data_ptr(), 3 * D, dqkv[:, D:].data_ptr(), 3 * D,
                                                     dqkv[:, 2 * D:].data_ptr(), 3 * D)
@@ -199,23 +202,24 @@ def test_attention_fwd_bwd(dt, T):
     check(dqkv[:, 2 * D:], rdv, tolb, "dv")
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_attention_dropout_consistency(dt):
-    """T=64 with V = I reveals the keep-mask through the output; check the rate, then
-    check fwd and bwd against a reference that uses exactly that mask."""
-    B, H, T, dh, p = 2, 2, 64, 64, 0.3
+@pytest.mark.parametrize("dt,T", [(torch.float32, 64), (torch.bfloat16, 64), (torch.float32, 40),
+                                  (torch.bfloat16, 40)])
+def test_attention_dropout_consistency(dt, T):
+    """dh = T with V = I reveals the keep-mask through the output; check the rate, then
+    check fwd and bwd against a reference that uses exactly that mask (T=40: generic kernels)."""
+    B, H, dh, p = 2, 2, T, 0.3
     M, D = B * T, H * dh
     qkv = rnd(M, 3 * D, dtype=dt, scale=0.5, seed=30)
-    eye = torch.eye(64, dtype=dt, device=DEV)
+    eye = torch.eye(T, dtype=dt, device=DEV)
     vI = eye.repeat(B, H)  # [B*T, H*dh], V[b,t,h,:] = e_t
     o = torch.empty(M, D, dtype=torch.float32 if dt == torch.float32 else dt, device=DEV)
     lse = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
     code = K.dtype_code(dt)
     a = K.attn_args(code, B, T, H, qkv.data_ptr(), 3 * D, qkv[:, D:].data_ptr(), 3 * D, vI.data_ptr(), D,
-                    o.data_ptr(), D, lse.data_ptr(), p, 777)
+                    o.data_ptr(), D, lse.data_ptr(), p, 777, dh=dh)
     K.attn_fwd(a)
     torch.cuda.synchronize()
-    Pd = f64(o).view(B, T, H, 64).transpose(1, 2)  # = P * mask / (1-p)
+    Pd = f64(o).view(B, T, H, dh).transpose(1, 2)  # = P * mask / (1-p)
     mask = (Pd != 0).double()
     frac = mask.mean().item()
     assert abs(frac - 0.7) < 0.03, frac
@@ -223,10 +227,10 @@ def test_attention_dropout_consistency(dt):
     k = f64(qkv[:, D:2 * D]).view(B, T, H, dh).transpose(1, 2).requires_grad_(True)
     v = rnd(M, D, dtype=dt, seed=31)
     vv = f64(v).view(B, T, H, dh).transpose(1, 2).requires_grad_(True)
-    ro, _ = attn_ref(q, k, vv, 1 / 8.0, mask, p)
+    ro, _ = attn_ref(q, k, vv, dh ** -0.5, mask, p)
     o2 = torch.empty(M, D, dtype=dt, device=DEV)
     a2 = K.attn_args(code, B, T, H, qkv.data_ptr(), 3 * D, qkv[:, D:].data_ptr(), 3 * D, v.data_ptr(), D,
-                     o2.data_ptr(), D, lse.data_ptr(), p, 777)
+                     o2.data_ptr(), D, lse.data_ptr(), p, 777, dh=dh)
     K.attn_fwd(a2)
     tol = 5e-6 if dt == torch.float32 else 1e-2
     check(o2, ro.transpose(1, 2).reshape(M, D), tol, "attn dropout out")
@@ -247,8 +251,11 @@ def test_attention_rejects_bad_shapes():
     t = torch.zeros(64, 3 * 64, device=DEV)
     lse = torch.zeros(64, device=DEV)
     a = K.attn_args(K.F32, 1, 48, 1, t.data_ptr(), 192, t.data_ptr(), 192, t.data_ptr(), 192, t.data_ptr(), 64,
-                    lse.data_ptr(), 0.0, 0)
-    with pytest.raises(RuntimeError, match="multiple of 32"):
+                    lse.data_ptr(), 0.0, 0, dh=60)
+    with pytest.raises(RuntimeError, match="head_dim"):
+        K.attn_fwd(a)
+    a.dh, a.T = 64, 5000
+    with pytest.raises(RuntimeError, match="T must be"):
         K.attn_fwd(a)
 
 

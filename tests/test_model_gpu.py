@@ -168,3 +168,26 @@ def test_state_dict_and_optimizer_round_trip(tmp_path):
     model2.eval()
     with torch.no_grad():
         assert torch.equal(model(src), model2(src))
+
+
+@pytest.mark.parametrize("D,H,L,T", [(256, 1, 1, 48), (512, 2, 1, 100)])
+def test_fp32_step_generic_attention_matches_oracle(D, H, L, T):
+    """Head dims 256 (BASELINE C1's 1024/4) and ragged T take the generic
+    attention kernels: same step parity bar as the MFMA path."""
+    cfg, model, crit, opt, params = make(D, H, L, 31, amp=False)
+    keys = list(params.keys())
+    oracle = model_ref.OracleTrainer(params, H)
+    g = torch.Generator().manual_seed(3)
+    src = torch.randn(2, T, 256, generator=g)
+    trg = torch.randn(2, T, 61, generator=g) * 20
+    model.train()
+    opt.zero_grad()
+    pred = model(src.to(DEV))
+    loss = crit(pred, trg.to(DEV))
+    loss.backward()
+    o_loss, o_norm, o_pred = oracle.step(src, trg)
+    named = dict(model.named_parameters())
+    worst = max(rel(named[k].grad, gk) for k, gk in oracle_grads(oracle, keys).items())
+    assert worst < 1e-4, worst
+    assert (pred.detach().cpu() - o_pred).abs().max().item() < 1e-3
+    assert abs(loss.item() - o_loss.item()) < 1e-5 * abs(o_loss.item())
