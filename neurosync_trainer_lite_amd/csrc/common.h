@@ -53,7 +53,8 @@ template <int RB> struct ImgK {
   static NSTL_DEV int off(int row, int byte) {
     const int chunk = byte >> 4;
     int x;
-    if constexpr (RB == 128) x = (row >> 1) & 7;
+    if constexpr (RB == 64) x = 0;  // 16 rows x 64 B = one contiguous KB: conflict-free as is
+    else if constexpr (RB == 128) x = (row >> 1) & 7;
     else x = row & 15;
     return row * RB + (((chunk ^ x) << 4) | (byte & 15));
   }

@@ -15,6 +15,8 @@
 #include <stdlib.h>
 
 #include "../../include/nstl.h"
+#include <string>
+
 #include "common.h"
 #include "status.h"
 
@@ -35,7 +37,8 @@ struct GemmParams {
   const char* aux; int64_t ld_aux; int aux_f32;
   float inv_keep; uint32_t thresh; uint64_t seed;
   const float* rope_cos; const float* rope_sin; int rope_T, rope_dim, rope_cols;
-  float* ws; int k_chunk;  // split-K: partial slabs [z][M][N]
+  float* ws;
+  int debug_skip_epilogue; int k_chunk;  // split-K: partial slabs [z][M][N]
 };
 
 // Epilogue over a wave's MT x 4 grid of 16x16 accumulators whose origin is
@@ -45,19 +48,10 @@ struct GemmParams {
 // slab, bias / ReLU+dropout / RoPE / dReLU+dropout, beta*C.
 constexpr int EPI_LD = 68;  // floats per scratch row (64 + 4 pad)
 
-NSTL_DEV void epi_store4(const GemmParams& p, int i, int j, f32x4 v) {
+// bias / ReLU+dropout / RoPE / dReLU+dropout on four consecutive columns
+// j..j+3 of row i (no alpha, beta or store)
+NSTL_DEV f32x4 epi_math4(const GemmParams& p, int i, int j, f32x4 v) {
   const int epi = p.epi;
-  if (p.ws != nullptr) {
-    float* w = p.ws + ((int64_t)blockIdx.y * p.M + i) * p.N + j;
-    if (j + 3 < p.N && (p.N & 3) == 0) {
-      *(f32x4*)w = (f32x4){v[0], v[1], v[2], v[3]};
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (j + e < p.N) w[e] = v[e];
-    }
-    return;
-  }
   if (p.bias != nullptr && epi != NSTL_EPI_NONE && epi != NSTL_EPI_DRELU_DROP) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] += j + e < p.N ? p.bias[j + e] : 0.f;
@@ -94,15 +88,36 @@ NSTL_DEV void epi_store4(const GemmParams& p, int i, int j, f32x4 v) {
       }
     }
   } else if (epi == NSTL_EPI_DRELU_DROP) {
+    const int64_t x = (int64_t)i * p.ld_aux + j;
+    float av[4];
+    if (!p.aux_f32 && j + 3 < p.N && (p.ld_aux & 3) == 0) {
+      const bf16x4 a4 = *(const bf16x4*)((const bf16*)p.aux + x);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (j + e < p.N) {
-        const int64_t x = (int64_t)i * p.ld_aux + j + e;
-        const float av = p.aux_f32 ? ((const float*)p.aux)[x] : (float)((const bf16*)p.aux)[x];
-        v[e] = av > 0.f ? v[e] * p.inv_keep : 0.f;
-      }
+      for (int e = 0; e < 4; ++e) av[e] = (float)a4[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        av[e] = j + e < p.N ? (p.aux_f32 ? ((const float*)p.aux)[x + e] : (float)((const bf16*)p.aux)[x + e]) : 0.f;
     }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = av[e] > 0.f ? v[e] * p.inv_keep : 0.f;
   }
+  return v;
+}
+
+NSTL_DEV void epi_store4(const GemmParams& p, int i, int j, f32x4 v) {
+  if (p.ws != nullptr) {
+    float* w = p.ws + ((int64_t)blockIdx.y * p.M + i) * p.N + j;
+    if (j + 3 < p.N && (p.N & 3) == 0) {
+      *(f32x4*)w = (f32x4){v[0], v[1], v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j + e < p.N) w[e] = v[e];
+    }
+    return;
+  }
+  v = epi_math4(p, i, j, v);
   const int64_t o = (int64_t)i * p.ldc + j;
   const bool vec = j + 3 < p.N && (p.ldc & 3) == 0;
   if (p.c_f32) {
@@ -398,6 +413,405 @@ __global__ __launch_bounds__(BIG_NT, 2) void gemm256_kernel(GemmParams p) {
   gemm_epilogue<8, 4>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, (float*)&smem[0] + wave * 64 * EPI_LD);
 }
 
+// ===========================================================================
+// 256x256 tile, 8 waves (2 x 4, each 128 x 64), BK = 32, a ring of FIVE 32 KB
+// LDS-DMA stages (160 KB), two wave groups staggered by one barrier.
+//
+// Step s of a wave = R(s) | barrier | M(s) | barrier, where
+//   R(s): ds_read its 12 fragments of tile s, stage tile s+3 (LDS-DMA);
+//   M(s): s_waitcnt lgkmcnt(0), 32 MFMAs.
+// Waves 4-7 (wm = 1) take one extra barrier up front, so on every SIMD one wave
+// runs M while its partner (wm = 0 <-> 1, same SIMD) runs R: the matrix pipe
+// alternates between the two waves instead of draining at every barrier.
+// With barriers numbered B(k): group 0 runs R0(s) B(2s) M0(s) B(2s+1), group 1
+// runs R1(s) B(2s+1) M1(s) B(2s+2).
+//   RAW: tile T is read after B(2T-1) (group 0) / B(2T) (group 1); every wave
+//        retires its share of tile T before it reaches B(2T-1): group 0 at the
+//        end of M0(T-1), group 1 at the end of R1(T-1) -> vmcnt(8) (tiles T+1,
+//        T+2 may still fly).
+//   WAR: tile T overwrites the slot of tile T-5, whose last reads retire before
+//        B(2T-8); tile T is staged in R(T-3), after B(2T-7) / B(2T-6).
+constexpr int R_BK = 32, R_SLOT = 32768, R_STAGES = 5;
+
+template <bool KMAJ>
+NSTL_DEV void glds_stage32(char* img, const char* base, int64_t ld, int row0, int rows_total, int k0, int wave,
+                           int lane) {
+  // 16 KB operand tile = 16 wave-instructions of 1 KB, 2 per wave
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int q = wave * 2 + s;
+    const char* src;
+    if (KMAJ) {  // 64-byte rows (32 k), 16 rows per KB, identity image
+      const int row = 16 * q + (lane >> 2), ch = lane & 3;
+      const int gi = min(row0 + row, rows_total - 1);
+      src = base + ((int64_t)gi * ld + k0 + ch * 8) * 2;
+    } else {     // 512-byte rows (256 m/n), 2 rows per KB, ImgMN<512>
+      const int row = 2 * q + (lane >> 5), pc = lane & 31;
+      const int x = (row & 3) | (((row >> 3) & 1) << 2);
+      const int lc = pc ^ (x << 1);
+      const int gi = min(row0 + lc * 8, ((rows_total - 1) / 8) * 8);
+      src = base + ((int64_t)(k0 + row) * ld + gi) * 2;
+    }
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)(img + q * 1024), 16, 0, 0);
+  }
+}
+
+template <bool AK, bool BKM>
+NSTL_DEV void ring_stage(char* slot, const GemmParams& p, int m0, int n0, int k0, int wave, int lane) {
+  glds_stage32<AK>(slot, p.A, p.lda, m0, p.M, k0, wave, lane);
+  glds_stage32<BKM>(slot + R_SLOT / 2, p.B, p.ldb, n0, p.N, k0, wave, lane);
+}
+
+#define NSTL_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+// LDS fragment reads as inline asm: the compiler cannot prove a ds_read does
+// not alias an in-flight LDS-DMA write to another ring slot and would put an
+// s_waitcnt vmcnt(0) in front of every K-step's first read, draining the
+// prefetch.  Ordering is by the explicit vmcnt/barrier protocol above, and
+// the consumer waits with an explicit lgkmcnt(0) + sched_barrier.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x2_t __attribute__((ext_vector_type(2)));
+NSTL_DEV uint32_t lds_u32(const char* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+NSTL_DEV void asm_frag_k64(bf16x8& f, uint32_t img, int row, int r) {
+  // ImgK<64>: identity image, 64-byte rows
+  i32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(img + row * 64 + r * 2));
+  f = __builtin_bit_cast(bf16x8, v);
+}
+NSTL_DEV void asm_frag_mn512(bf16x8& f, uint32_t img, int col16, int lane) {
+  // ImgMN<512> transpose reads (see frag_col), r0 = 0
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int rb = 8 * g;
+  const int byte = (col16 + 4 * pp) * 2;
+  i32x2_t v0, v1;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v0) : "v"(img + ImgMN<512>::off(rb + q, byte)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v1) : "v"(img + ImgMN<512>::off(rb + 4 + q, byte)));
+  const bf16x4 b0 = __builtin_bit_cast(bf16x4, v0), b1 = __builtin_bit_cast(bf16x4, v1);
+  f = (bf16x8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+}
+
+// this wave's share of tile t+1 has landed; later tiles (issued up to t+3) fly on
+NSTL_DEV void retire_next(int t, int nk) {
+  const int ahead = min(nk, t + 4) - (t + 2);
+  if (ahead >= 2) NSTL_VMCNT(8);
+  else if (ahead == 1) NSTL_VMCNT(4);
+  else NSTL_VMCNT(0);
+}
+
+// ---------------------------------------------------------------------------
+// Epilogues of the ring kernel.  acc[a][b] holds, in lane l, row 16a + (l&15)
+// and columns 16b + 4(l>>4) + 0..3 of the wave's 128 x 64 block, so the raw
+// accumulators go to the wave's LDS scratch with one 16-byte write per group
+// (f32, two passes of 64 rows).  A compact loop reads row-major chunks back
+// and stores 16 bytes per lane: a wave instruction writes 8 rows x 128 B
+// (bf16) / 4 rows x 256 B (f32), whole cache lines.  (Storing the 4-column
+// groups straight from the accumulators writes 32-byte pieces: ~2x slower.)
+//
+// The epilogue kind is a template parameter (EM_*), so each instantiation
+// carries only its own elementwise code: the generic, branchy form measured
+// ~800 VALU + 600 SALU instructions per wave per tile (≈5 µs per 256^2 tile,
+// VALU-issue bound).  vmcnt counts loads and stores together, so any input
+// load (RoPE cos/sin, the dReLU operand, old C) is issued one iteration ahead,
+// before the current store, and the bias (fixed per lane) once per tile.
+enum { EM_GENERIC = 0, EM_BF16 = 1, EM_RELU_DROP = 2, EM_ROPE = 3, EM_DRELU = 4, EM_F32 = 5, EM_WS = 6 };
+
+constexpr int RING_EPI_RB = 64 * 4 + 16;          // padded f32 scratch row
+constexpr int RING_EPI_WAVE = 64 * RING_EPI_RB;   // 17 KB per wave (8 waves: 136 KB)
+
+NSTL_DEV void stage_half(const f32x4 (&acc)[8][4], int half, float alpha, int lane, char* scr) {
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      *(f32x4*)(scr + (16 * a + (lane & 15)) * RING_EPI_RB + (16 * b + 4 * (lane >> 4)) * 4) =
+          acc[half * 4 + a][b] * alpha;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int EM>
+NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, int col0, int lane, char* scr) {
+  constexpr bool F32OUT = EM == EM_F32 || EM == EM_WS;
+  constexpr int ESZ = F32OUT ? 4 : 2;
+  constexpr int CW = 16 / ESZ;   // columns per lane per store (8 bf16 / 4 f32)
+  constexpr int LPR = 64 / CW;   // lanes per 64-column row (8 / 16)
+  constexpr int RPI = 64 / LPR;  // rows per wave instruction (8 / 4)
+  constexpr int NIT = 64 / RPI;  // iterations per 64-row pass
+  char* const C = EM == EM_WS ? (char*)(p.ws + (int64_t)blockIdx.y * p.M * p.N) : p.C;
+  const int64_t ldc = EM == EM_WS ? p.N : p.ldc;
+  const int c = (lane % LPR) * CW, j = col0 + c;
+  const bool colok = j < p.N;
+  const bool vec = j + CW <= p.N && (ldc % CW) == 0;
+  const bool use_beta = EM == EM_F32 && p.beta != 0.f;
+  float bias[CW];
+#pragma unroll
+  for (int e = 0; e < CW; ++e) bias[e] = 0.f;
+  if ((EM == EM_BF16 || EM == EM_RELU_DROP || EM == EM_ROPE) && p.bias != nullptr) {
+#pragma unroll
+    for (int e = 0; e < CW; ++e) bias[e] = j + e < p.N ? p.bias[j + e] : 0.f;
+  }
+  const bool rope_col = EM == EM_ROPE && j < p.rope_cols;
+  const int rhalf = p.rope_dim >> 1;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    stage_half(acc, half, p.alpha, lane, scr);
+    const int r0 = lane / LPR;
+    const int ib = row0 + half * 64 + r0;
+    // inputs of iteration it, loaded one iteration ahead
+    float in_a[CW], in_b[CW];
+    auto prefetch = [&](int i, float* xa, float* xb) {
+      if (i >= p.M || !colok) return;
+      if (EM == EM_ROPE && rope_col) {
+        const int t = i % p.rope_T;
+#pragma unroll
+        for (int e = 0; e < CW; e += 2) {
+          const int pr = ((j + e) % p.rope_dim) >> 1;
+          xa[e] = p.rope_cos[t * rhalf + pr];
+          xa[e + 1] = p.rope_sin[t * rhalf + pr];
+        }
+      } else if (EM == EM_DRELU) {
+        const bf16* ap = (const bf16*)p.aux + (int64_t)i * p.ld_aux + j;
+        if (vec && (p.ld_aux % CW) == 0) {
+          const bf16x8 a8 = *(const bf16x8*)ap;
+#pragma unroll
+          for (int e = 0; e < CW; ++e) xa[e] = (float)a8[e % 8];
+        } else {
+#pragma unroll
+          for (int e = 0; e < CW; ++e) xa[e] = j + e < p.N ? (float)ap[e] : 0.f;
+        }
+      } else if (EM == EM_F32 && use_beta) {
+        const float* cp = (const float*)C + (int64_t)i * ldc + j;
+        if (vec) {
+          const f32x4 o = *(const f32x4*)cp;
+#pragma unroll
+          for (int e = 0; e < CW; ++e) xb[e] = o[e % 4];
+        } else {
+#pragma unroll
+          for (int e = 0; e < CW; ++e) xb[e] = j + e < p.N ? cp[e] : 0.f;
+        }
+      }
+    };
+#pragma unroll
+    for (int e = 0; e < CW; ++e) in_a[e] = in_b[e] = 0.f;
+    prefetch(ib, in_a, in_b);
+#pragma unroll 2
+    for (int it = 0; it < NIT; ++it) {
+      const int i = ib + it * RPI;
+      const char* src = scr + (it * RPI + r0) * RING_EPI_RB + c * 4;
+      float v[CW];
+      {
+        const f32x4 v0 = *(const f32x4*)src;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v0[e];
+        if (CW == 8) {
+          const f32x4 v1 = *(const f32x4*)(src + 16);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[(4 + e) % CW] = v1[e];
+        }
+      }
+      float na[CW], nb[CW];
+#pragma unroll
+      for (int e = 0; e < CW; ++e) na[e] = nb[e] = 0.f;
+      if (it + 1 < NIT) prefetch(i + RPI, na, nb);
+      if (i < p.M && colok) {
+#pragma unroll
+        for (int e = 0; e < CW; ++e) v[e] += bias[e];
+        if (EM == EM_RELU_DROP) {
+#pragma unroll
+          for (int e = 0; e < CW; ++e) v[e] = fmaxf(v[e], 0.f);
+          if (p.thresh) {
+            const uint64_t idx = (uint64_t)i * p.N + j;  // even: N even, j % 8 == 0
+#pragma unroll
+            for (int e = 0; e < CW; e += 2) {
+              bool k0, k1;
+              nstl_keep2(p.seed, idx + e, p.thresh, k0, k1);
+              v[e] = k0 ? v[e] * p.inv_keep : 0.f;
+              v[e + 1] = k1 ? v[e + 1] * p.inv_keep : 0.f;
+            }
+          }
+        } else if (EM == EM_ROPE) {
+          if (rope_col) {
+#pragma unroll
+            for (int e = 0; e < CW; e += 2) {
+              const float x0 = v[e], x1 = v[e + 1], cs = in_a[e], sn = in_a[e + 1];
+              v[e] = x0 * cs - x1 * sn;
+              v[e + 1] = x0 * sn + x1 * cs;
+            }
+          }
+        } else if (EM == EM_DRELU) {
+#pragma unroll
+          for (int e = 0; e < CW; ++e) v[e] = in_a[e] > 0.f ? v[e] * p.inv_keep : 0.f;
+        } else if (EM == EM_F32) {
+          if (use_beta) {
+#pragma unroll
+            for (int e = 0; e < CW; ++e) v[e] += p.beta * in_b[e];
+          }
+        }
+        char* dst = C + ((int64_t)i * ldc + j) * ESZ;
+        if (vec) {
+          if (ESZ == 4)
+            *(f32x4*)dst = (f32x4){v[0], v[1 % CW], v[2 % CW], v[3 % CW]};
+          else
+            *(bf16x8*)dst = (bf16x8){(bf16)v[0], (bf16)v[1 % CW], (bf16)v[2 % CW], (bf16)v[3 % CW],
+                                     (bf16)v[4 % CW], (bf16)v[5 % CW], (bf16)v[6 % CW], (bf16)v[7 % CW]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < CW; ++e)
+            if (j + e < p.N) {
+              if (ESZ == 4) ((float*)dst)[e] = v[e];
+              else ((bf16*)dst)[e] = (bf16)v[e];
+            }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < CW; ++e) {
+        in_a[e] = na[e];
+        in_b[e] = nb[e];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+// generic fallback (any epilogue op, beta, dtype): per 4-column group epi_store4
+NSTL_DEV void ring_epi_generic(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, int col0, int lane,
+                               char* scr) {
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    stage_half(acc, half, p.alpha, lane, scr);
+#pragma unroll 1
+    for (int it = 0; it < 16; ++it) {
+      const int r = it * 4 + (lane >> 4), c = (lane & 15) * 4;
+      const int i = row0 + half * 64 + r;
+      if (i < p.M && col0 + c < p.N) epi_store4(p, i, col0 + c, *(const f32x4*)(scr + r * RING_EPI_RB + c * 4));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+template <bool AK, bool BKM, int EM>
+__global__ __launch_bounds__(BIG_NT, 1) void gemm256r_kernel(GemmParams p) {
+  constexpr int SMEM = R_STAGES * R_SLOT;
+  static_assert(8 * RING_EPI_WAVE <= SMEM, "epilogue scratch must fit in the ring");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nt_m = (p.M + BIG - 1) / BIG, nt_n = (p.N + BIG - 1) / BIG;
+  // XCD-contiguous id ranges, then grouped order (GROUP_M row tiles per group,
+  // column-fastest inside): an XCD's 32 co-resident blocks cover ~4 x 8 tiles
+  const int id = xcd_remap(blockIdx.x, nt_m * nt_n);
+  constexpr int GROUP_M = 4;
+  const int per_group = GROUP_M * nt_n;
+  const int first_m = (id / per_group) * GROUP_M;
+  const int gm = min(nt_m - first_m, GROUP_M);
+  const int in_g = id % per_group;
+  const int tm = first_m + in_g % gm, tn = in_g / gm;
+  const int m0 = tm * BIG, n0 = tn * BIG;
+  const int kz0 = blockIdx.y * p.k_chunk;
+  const int kz1 = min(p.K, kz0 + p.k_chunk);
+  const int nk = (kz1 - kz0) / R_BK;
+  const uint32_t smem_u32 = lds_u32(smem);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // prologue: tiles 0..2 in flight, tile 0 landed everywhere
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+    if (s < nk) ring_stage<AK, BKM>(smem + s * R_SLOT, p, m0, n0, kz0 + s * R_BK, wave, lane);
+  if (nk >= 3) NSTL_VMCNT(8);
+  else if (nk == 2) NSTL_VMCNT(4);
+  else NSTL_VMCNT(0);
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // the stagger
+
+  int slot = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // ---- R(kt)
+    const uint32_t Ai = smem_u32 + slot * R_SLOT;
+    const uint32_t Bi = Ai + R_SLOT / 2;
+    bf16x8 fb[4], fa[8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (BKM) asm_frag_k64(fb[t], Bi, wn * 64 + t * 16 + (lane & 15), 8 * (lane >> 4));
+      else asm_frag_mn512(fb[t], Bi, wn * 64 + t * 16, lane);
+    }
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      if (AK) asm_frag_k64(fa[a], Ai, wm * 128 + a * 16 + (lane & 15), 8 * (lane >> 4));
+      else asm_frag_mn512(fa[a], Ai, wm * 128 + a * 16, lane);
+    }
+    if (kt + 3 < nk) {
+      int s3 = slot + 3;
+      if (s3 >= R_STAGES) s3 -= R_STAGES;
+      ring_stage<AK, BKM>(smem + s3 * R_SLOT, p, m0, n0, kz0 + (kt + 3) * R_BK, wave, lane);
+    }
+    if (wm == 1) retire_next(kt, nk);
+    __builtin_amdgcn_s_barrier();
+    // ---- M(kt)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    // operands swapped: acc[a][b] takes C^T's register layout, i.e. lane l owns
+    // row 16a + (l & 15) and the four consecutive columns 16b + 4(l >> 4) + 0..3
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mma16(acc[a][b], fb[b], fa[a]);
+    __builtin_amdgcn_s_setprio(0);
+    if (wm == 0) retire_next(kt, nk);
+    __builtin_amdgcn_s_barrier();
+    slot = slot + 1 == R_STAGES ? 0 : slot + 1;
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger
+  if (p.debug_skip_epilogue == 1) {  // timing experiments only (NSTL_GEMM_DEBUG=skip_epi)
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(acc[a][b]));
+    return;
+  }
+  __syncthreads();  // every wave is done with the ring: it becomes scratch
+  char* scr = smem + wave * RING_EPI_WAVE;
+  const int row0 = m0 + wm * 128, col0 = n0 + wn * 64;
+  if (EM == EM_GENERIC) ring_epi_generic(p, acc, row0, col0, lane, scr);
+  else ring_epi<EM>(p, acc, row0, col0, lane, scr);
+}
+
+// which lean epilogue fits this call (EM_GENERIC when none does)
+int ring_epi_mode(const nstl_gemm_args* a, const GemmParams& p) {
+  if (p.ws != nullptr) return EM_WS;
+  if (p.c_f32) return a->epilogue == NSTL_EPI_NONE ? EM_F32 : EM_GENERIC;
+  if (p.beta != 0.f) return EM_GENERIC;
+  switch (a->epilogue) {
+    case NSTL_EPI_NONE:
+    case NSTL_EPI_BIAS: return EM_BF16;
+    case NSTL_EPI_BIAS_RELU_DROP: return (a->N % 2 == 0) ? EM_RELU_DROP : EM_GENERIC;
+    case NSTL_EPI_BIAS_ROPE: return EM_ROPE;
+    case NSTL_EPI_DRELU_DROP: return a->dtype == NSTL_BF16 ? EM_DRELU : EM_GENERIC;
+  }
+  return EM_GENERIC;
+}
+
+template <bool AK, bool BKM>
+void launch_ring_em(int em, dim3 grid, dim3 block, hipStream_t st, const GemmParams& p) {
+  switch (em) {
+    case EM_BF16: hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, EM_BF16>), grid, block, 0, st, p); break;
+    case EM_RELU_DROP: hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, EM_RELU_DROP>), grid, block, 0, st, p); break;
+    case EM_ROPE: hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, EM_ROPE>), grid, block, 0, st, p); break;
+    case EM_DRELU: hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, EM_DRELU>), grid, block, 0, st, p); break;
+    case EM_F32: hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, EM_F32>), grid, block, 0, st, p); break;
+    case EM_WS: hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, EM_WS>), grid, block, 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm256r_kernel<AK, BKM, EM_GENERIC>), grid, block, 0, st, p); break;
+  }
+}
+
 // split-K combine: C = sum_z ws[z] (+bias) (+beta*C)
 __global__ void splitk_reduce(const float* ws, int splits, int M, int N, char* C, int64_t ldc, int c_f32,
                               float beta, const float* bias) {
@@ -421,9 +835,27 @@ __global__ void splitk_reduce(const float* ws, int splits, int M, int N, char* C
   }
 }
 
+// NSTL_GEMM_RING=0 selects the two-stage BK=64 kernel (A/B comparisons)
+bool getenv_ring() {
+  static const int v = [] {
+    const char* e = getenv("NSTL_GEMM_RING");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return v != 0;
+}
+
 int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t st) {
   const int nt = ((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
   dim3 grid(nt, splits), block(BIG_NT);
+  if (getenv_ring()) {
+    const int em = ring_epi_mode(a, p);
+    if (a->a_kmajor && a->b_kmajor) launch_ring_em<true, true>(em, grid, block, st, p);
+    else if (a->a_kmajor && !a->b_kmajor) launch_ring_em<true, false>(em, grid, block, st, p);
+    else if (!a->a_kmajor && !a->b_kmajor) launch_ring_em<false, false>(em, grid, block, st, p);
+    else launch_ring_em<false, true>(em, grid, block, st, p);
+    NSTL_LAUNCH_CHECK("nstl_gemm (256 ring)");
+    return 0;
+  }
   if (a->a_kmajor && a->b_kmajor)
     hipLaunchKernelGGL((gemm256_kernel<true, true>), grid, block, 0, st, p);
   else if (a->a_kmajor && !a->b_kmajor)
@@ -450,6 +882,15 @@ int launch_typed(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t
     hipLaunchKernelGGL((gemm_kernel<T, false, true>), grid, block, 0, st, p);
   NSTL_LAUNCH_CHECK("nstl_gemm");
   return 0;
+}
+
+// NSTL_GEMM_DEBUG=skip_epi: the ring kernel stores nothing (timing experiments only)
+int getenv_debug_skip_epi() {
+  static const int v = [] {
+    const char* e = getenv("NSTL_GEMM_DEBUG");
+    return !e ? 0 : std::string(e) == "skip_epi" ? 1 : std::string(e) == "skip_store" ? 2 : 0;
+  }();
+  return v;
 }
 
 // NSTL_GEMM_SMALL=1 forces the 128x128 kernel (A/B comparisons, debugging)
@@ -509,6 +950,7 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   p.rope_cos = a->rope_cos; p.rope_sin = a->rope_sin;
   p.rope_T = a->rope_T; p.rope_dim = a->rope_dim; p.rope_cols = a->rope_cols;
   p.ws = nullptr;
+  p.debug_skip_epilogue = getenv_debug_skip_epi();
 
   // the 256x256 LDS-DMA kernel: bf16, K a multiple of its 64-deep K tile, and at
   // least 32 of its tiles (measured on the 228M step's shapes, tools/bench_gemm.py;
