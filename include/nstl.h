@@ -84,6 +84,7 @@ typedef struct nstl_attn_args {
   void* dv; int64_t dv_ld;
   const float* rope_cos; const float* rope_sin;  /* [T][dh/2]; non-null: dq,dk rotated back */
   int rope_q, rope_k;
+  float* dsum;                /* backward scratch [B*H*T] f32: rowsum(dO * O) */
 } nstl_attn_args;
 int nstl_attn_fwd(const nstl_attn_args* args, void* stream);
 int nstl_attn_bwd(const nstl_attn_args* args, void* stream);

@@ -34,6 +34,7 @@ struct AttnParams {
   const char* v; int64_t v_ld;
   char* o; int64_t o_ld;
   float* lse;
+  float* dsum;
   const char* dout; int64_t dout_ld;
   char* dq; int64_t dq_ld;
   char* dk; int64_t dk_ld;
@@ -47,11 +48,11 @@ struct AttnParams {
 // LDS-DMA rows [0, nrows) of a (b, h) slice (64 elements per row) into an
 // ImgK<RB> image.  One wave instruction moves 1 KB = 1024/RB rows; the image
 // swizzle is applied to the per-lane source chunk.
-template <int RB>
+template <int RB, int NW = NT / 64>
 NSTL_DEV void dma_rows(char* img, const char* g, int64_t ld_bytes, int nrows, int wave, int lane) {
   constexpr int RPK = 1024 / RB, CPR = RB / 16;
   const int ninst = nrows / RPK;
-  for (int q = wave; q < ninst; q += NT / 64) {
+  for (int q = wave; q < ninst; q += NW) {
     const int row = q * RPK + lane / CPR, pc = lane % CPR;
     const int x = RB == 128 ? ((row >> 1) & 7) : (row & 15);
     const int lc = pc ^ x;
@@ -78,8 +79,13 @@ NSTL_DEV void put4(char* dst, float a, float b, float c, float d, float) {
 }
 
 // ----------------------------------------------------------------------------
+// Forward: one workgroup of FWD_NT/64 waves per (b, h) and 16*FWD_NT/64 queries
+// (all of T=128), so K and V are staged once per (b, h); each wave owns 16
+// query rows.
+constexpr int FWD_NT = 512, FWD_QB = 16 * FWD_NT / 64;
+
 template <typename T>
-__global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
+__global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
   constexpr int ESZ = (int)sizeof(T);
   constexpr int RBK = DH * ESZ;   // 128 (bf16) / 256 (f32)
@@ -91,18 +97,19 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnParams p) {
   char* Kimg = smem;
   char* Vimg = Kimg + T_ * RBK;
   char* Qimg = Vimg + T_ * RBK;
-  char* Pimg = Qimg + 64 * RBK;
+  char* Pimg = Qimg + FWD_QB * RBK;
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  const int qb0 = blockIdx.x * 64;
-  const int nq = min(64, T_ - qb0);
+  const int qb0 = blockIdx.x * FWD_QB;
+  const int nq = min(FWD_QB, T_ - qb0);
   const int64_t tok0 = (int64_t)b * T_;
+  constexpr int NW = FWD_NT / 64;
 
-  dma_rows<RBK>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
-  dma_rows<RBK>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
-  dma_rows<RBK>(Qimg, p.q + ((tok0 + qb0) * p.q_ld + h * DH) * ESZ, p.q_ld * ESZ, nq, w, lane);
+  dma_rows<RBK, NW>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, NW>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, NW>(Qimg, p.q + ((tok0 + qb0) * p.q_ld + h * DH) * ESZ, p.q_ld * ESZ, nq, w, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -218,221 +225,290 @@ NSTL_DEV float rope_back(float v, int t, int d, const float* cs, const float* sn
   return (d & 1) ? (v * c - partner * s) : (v * c + partner * s);
 }
 
+// A wave's 16 x 64 result tile (lane: rows 4g+r, column dt*16 + (lane&15)) to
+// global memory through the wave's LDS scratch: element writes into a dense
+// [16][64] image, then 16-byte row chunks (2-byte scattered stores write
+// 32-byte pieces of 4 rows per instruction).
 template <typename T>
-__global__ __launch_bounds__(NT) void attn_bwd_kernel(AttnParams p) {
+NSTL_DEV void store_tile16x64(const float (&v)[4][4], char* scr, char* gbase, int64_t ld_elems, int lane) {
+  constexpr int ESZ = (int)sizeof(T), RB = DH * ESZ, CPR = RB / 16;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) *(T*)(scr + (4 * g + r) * RB + (dt * 16 + (lane & 15)) * ESZ) = from_f32<T>(v[dt][r]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int c = lane; c < 16 * CPR; c += 64) {
+    const int row = c / CPR, ch = c % CPR;
+    *(uint4*)(gbase + (int64_t)row * ld_elems * ESZ + ch * 16) = *(const uint4*)(scr + row * RB + ch * 16);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// Backward, as two kernels (8 waves, 128 rows: all of T=128, so each (b, h)
+// operand is staged once) with ~48 KB LDS, 3 resident per CU:
+//   attn_bwd_dq : workgroup = (b, h, 128 queries); K, V of (b, h) in LDS; a wave
+//                 owns 16 queries: D = rowsum(dO * O) (also written to p.dsum
+//                 for the second kernel), dS over all keys, dQ = dS K (RoPE^T).
+//   attn_bwd_dkv: workgroup = (b, h, 128 keys); Q, dO of (b, h) in LDS; a wave
+//                 owns 16 keys: dV = P_drop^T dO, dK = dS^T Q (RoPE^T).
+// A wave's own rows come straight from global memory into MFMA fragments.
+constexpr int BWD_NT = 512, BWD_ROWS = 16 * BWD_NT / 64;  // 8 waves, 128 rows
+
+template <typename T>
+NSTL_DEV void gload_frag(typename FragT<T>::type& f, const T* row, int k0);
+template <>
+NSTL_DEV void gload_frag<bf16>(bf16x8& f, const bf16* row, int k0) {
+  f = *(const bf16x8*)(row + k0);
+}
+template <>
+NSTL_DEV void gload_frag<float>(f32x8& f, const float* row, int k0) {
+  const f32x4 lo = *(const f32x4*)(row + k0), hi = *(const f32x4*)(row + k0 + 4);
+  f = (f32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <typename T>
+__global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
   constexpr int ESZ = (int)sizeof(T);
   constexpr int RBK = DH * ESZ;
   typedef ImgK<RBK> Img;
-  constexpr int RBS = 16 * ESZ;     // per-wave scratch rows: 16 entries
+  constexpr int RBS = 16 * ESZ;
+  typedef ImgPlain<RBS> ImgS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int T_ = p.T, nkt = T_ / 16;
+  char* Kimg = smem;
+  char* Vimg = Kimg + T_ * RBK;
+  char* scratch = Vimg + T_ * RBK;
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int64_t tok0 = (int64_t)b * T_;
+  const int q0 = blockIdx.x * BWD_ROWS + w * 16;
+  dma_rows<RBK, BWD_NT / 64>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, BWD_NT / 64>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
+  const bool act = q0 < T_;
+  Frag fq[2], fo[2];
+  float lq[4], dqv[4];
+  if (act) {
+    const int qr = q0 + (lane & 15);
+    const T* qrow = (const T*)p.q + (tok0 + qr) * p.q_ld + h * DH;
+    const T* drow = (const T*)p.dout + (tok0 + qr) * p.dout_ld + h * DH;
+    const T* orow = (const T*)p.o + (tok0 + qr) * p.o_ld + h * DH;
+    Frag oo[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      gload_frag<T>(fq[u], qrow, 32 * u + 8 * g);
+      gload_frag<T>(fo[u], drow, 32 * u + 8 * g);
+      gload_frag<T>(oo[u], orow, 32 * u + 8 * g);
+    }
+    // D for row (lane & 15): 16 of its products per lane, then across the 4 groups
+    float dpart = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dpart += to_f32(fo[u][e]) * to_f32(oo[u][e]);
+    dpart += __shfl_xor(dpart, 16);
+    dpart += __shfl_xor(dpart, 32);
+    if (g == 0) p.dsum[(int64_t)bh * T_ + qr] = dpart;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dqv[r] = __shfl(dpart, 4 * g + r);
+      lq[r] = p.lse[(int64_t)bh * T_ + q0 + 4 * g + r] * LOG2E;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!act) return;
+
+  const float c2 = p.scale * LOG2E;
+  char* S2 = scratch + w * 2 * 32 * RBS;
+  f32x4 dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < nkt / 2; ++kc) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kt = kc * 2 + u;
+      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      Frag fb;
+      frag_row<Img>(fb, Kimg, kt * 16 + (lane & 15), 8 * g);
+      mma16(s, fq[0], fb);
+      frag_row<Img>(fb, Kimg, kt * 16 + (lane & 15), 32 + 8 * g);
+      mma16(s, fq[1], fb);
+      frag_row<Img>(fb, Vimg, kt * 16 + (lane & 15), 8 * g);
+      mma16(dp, fo[0], fb);
+      frag_row<Img>(fb, Vimg, kt * 16 + (lane & 15), 32 + 8 * g);
+      mma16(dp, fo[1], fb);
+      // accumulator: row = query (4g + r), col = key
+      const int key = kt * 16 + (lane & 15);
+      bool keep[4] = {true, true, true, true};
+      if (p.thresh) {
+        const uint64_t idx = drop_idx(bh, T_, q0 + 4 * g, key);
+        nstl_keep2(p.seed, idx, p.thresh, keep[0], keep[1]);
+        nstl_keep2(p.seed, idx + 2, p.thresh, keep[2], keep[3]);
+      }
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = exp2f(s[r] * c2 - lq[r]);
+        float dpd = dp[r];
+        if (p.thresh) dpd = keep[r] ? dpd * p.inv_keep : 0.f;
+        ds[r] = pv * (dpd - dqv[r]);
+      }
+      // transposed image [key][query]
+      put4(S2 + (u * 16 + (lane & 15)) * RBS + 4 * g * ESZ, ds[0], ds[1], ds[2], ds[3], T());
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    Frag fa;
+    frag_col<ImgS>(fa, S2, 0, 0, lane);  // A(i = query, r = key)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      Frag fb;
+      frag_col<Img>(fb, Kimg, dt * 16, kc * 32, lane);
+      mma16(dq[dt], fa, fb);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  float vq[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = q0 + 4 * g + r;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int d = dt * 16 + (lane & 15);
+      float x = dq[dt][r] * p.scale;
+      if (p.rope_q) x = rope_back(x, q, d, p.rope_cos, p.rope_sin);
+      vq[dt][r] = x;
+    }
+  }
+  store_tile16x64<T>(vq, S2, p.dq + ((tok0 + q0) * p.dq_ld + h * DH) * ESZ, p.dq_ld, lane);
+}
+
+template <typename T>
+__global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
+  typedef typename FragT<T>::type Frag;
+  constexpr int ESZ = (int)sizeof(T);
+  constexpr int RBK = DH * ESZ;
+  typedef ImgK<RBK> Img;
+  constexpr int RBS = 16 * ESZ;
   typedef ImgPlain<RBS> ImgS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int T_ = p.T, nkt = T_ / 16;
   char* Qimg = smem;
-  char* Kimg = Qimg + T_ * RBK;
-  char* Vimg = Kimg + T_ * RBK;
-  char* Dimg = Vimg + T_ * RBK;
+  char* Dimg = Qimg + T_ * RBK;
   float* lse_s = (float*)(Dimg + T_ * RBK);
   float* dq_s = lse_s + T_;
   char* scratch = (char*)(dq_s + T_);
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int64_t tok0 = (int64_t)b * T_;
-
-  dma_rows<RBK>(Qimg, p.q + (tok0 * p.q_ld + h * DH) * ESZ, p.q_ld * ESZ, T_, w, lane);
-  dma_rows<RBK>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
-  dma_rows<RBK>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
-  dma_rows<RBK>(Dimg, p.dout + (tok0 * p.dout_ld + h * DH) * ESZ, p.dout_ld * ESZ, T_, w, lane);
-  // D_q = rowsum(dO * O): 256/T threads per row, each a run of 16-byte chunks;
-  // the O loads are issued together, dO is read once the DMA has landed
-  constexpr int EPC = 16 / ESZ;
-  const int tpr = NT / T_;                 // threads per row (1..8)
-  const int row = tid / tpr, part = tid % tpr;
-  const int nch = (DH / EPC) / tpr;        // chunks per thread
-  uint4 ov[8];
+  const int k0 = blockIdx.x * BWD_ROWS + w * 16;
+  dma_rows<RBK, BWD_NT / 64>(Qimg, p.q + (tok0 * p.q_ld + h * DH) * ESZ, p.q_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, BWD_NT / 64>(Dimg, p.dout + (tok0 * p.dout_ld + h * DH) * ESZ, p.dout_ld * ESZ, T_, w, lane);
+  for (int i = tid; i < T_; i += BWD_NT) {
+    lse_s[i] = p.lse[(int64_t)bh * T_ + i] * LOG2E;
+    dq_s[i] = p.dsum[(int64_t)bh * T_ + i];
+  }
+  const bool act = k0 < T_;
+  Frag fk[2], fv[2];
+  if (act) {
+    const int kr = k0 + (lane & 15);
+    const T* krow = (const T*)p.k + (tok0 + kr) * p.k_ld + h * DH;
+    const T* vrow = (const T*)p.v + (tok0 + kr) * p.v_ld + h * DH;
 #pragma unroll
-  for (int c = 0; c < 8; ++c)
-    if (c < nch) ov[c] = *(const uint4*)(p.o + ((tok0 + row) * p.o_ld + h * DH + (part * nch + c) * EPC) * ESZ);
-  if (tid < T_) lse_s[tid] = p.lse[(int64_t)bh * T_ + tid];
+    for (int u = 0; u < 2; ++u) {
+      gload_frag<T>(fk[u], krow, 32 * u + 8 * g);
+      gload_frag<T>(fv[u], vrow, 32 * u + 8 * g);
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  {
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      if (c < nch) {
-        const int ch = part * nch + c;
-        const uint4 dv = *(const uint4*)(Dimg + Img::off(row, ch * 16));
-        const T* oe = (const T*)&ov[c];
-        const T* de = (const T*)&dv;
-#pragma unroll
-        for (int e = 0; e < EPC; ++e) acc += to_f32(oe[e]) * to_f32(de[e]);
-      }
-    }
-    for (int o = 1; o < tpr; o <<= 1) acc += __shfl_xor(acc, o);
-    if (part == 0) dq_s[row] = acc;
-  }
-  __syncthreads();
+  if (!act) return;
 
   const float c2 = p.scale * LOG2E;
   char* S1 = scratch + w * 2 * 32 * RBS;  // [32 rows][16] images
   char* S2 = S1 + 32 * RBS;
-
-  // ---------------- phase 1: dK, dV for 16-key tiles ----------------
-  for (int kt = w; kt < nkt; kt += 4) {
-    Frag fk[2], fv[2];
-    frag_row<Img>(fk[0], Kimg, kt * 16 + (lane & 15), 8 * g);
-    frag_row<Img>(fk[1], Kimg, kt * 16 + (lane & 15), 32 + 8 * g);
-    frag_row<Img>(fv[0], Vimg, kt * 16 + (lane & 15), 8 * g);
-    frag_row<Img>(fv[1], Vimg, kt * 16 + (lane & 15), 32 + 8 * g);
-    f32x4 dk[4], dv[4];
+  f32x4 dk[4], dv[4];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int qc = 0; qc < nkt / 2; ++qc) {
+  for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int qc = 0; qc < nkt / 2; ++qc) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int qt = qc * 2 + u;
-        f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
-        Frag fb;
-        frag_row<Img>(fb, Qimg, qt * 16 + (lane & 15), 8 * g);
-        mma16(st, fk[0], fb);
-        frag_row<Img>(fb, Qimg, qt * 16 + (lane & 15), 32 + 8 * g);
-        mma16(st, fk[1], fb);
-        frag_row<Img>(fb, Dimg, qt * 16 + (lane & 15), 8 * g);
-        mma16(dpt, fv[0], fb);
-        frag_row<Img>(fb, Dimg, qt * 16 + (lane & 15), 32 + 8 * g);
-        mma16(dpt, fv[1], fb);
-        // accumulator: row = key (4g + r), col = query
-        const int q = qt * 16 + (lane & 15);
-        const float lq = lse_s[q] * LOG2E, dqv = dq_s[q];
-        float pd[4], ds[4];
+    for (int u = 0; u < 2; ++u) {
+      const int qt = qc * 2 + u;
+      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+      Frag fb;
+      frag_row<Img>(fb, Qimg, qt * 16 + (lane & 15), 8 * g);
+      mma16(st, fk[0], fb);
+      frag_row<Img>(fb, Qimg, qt * 16 + (lane & 15), 32 + 8 * g);
+      mma16(st, fk[1], fb);
+      frag_row<Img>(fb, Dimg, qt * 16 + (lane & 15), 8 * g);
+      mma16(dpt, fv[0], fb);
+      frag_row<Img>(fb, Dimg, qt * 16 + (lane & 15), 32 + 8 * g);
+      mma16(dpt, fv[1], fb);
+      // accumulator: row = key (4g + r), col = query
+      const int q = qt * 16 + (lane & 15);
+      const float lq = lse_s[q], dqv = dq_s[q];
+      float pd[4], ds[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kt * 16 + 4 * g + r;
-          const float pv = exp2f(st[r] * c2 - lq);
-          float pdr = pv, dpd = dpt[r];
-          if (p.thresh) {
-            const bool keep = nstl_keep(p.seed, drop_idx(bh, T_, q, key), p.thresh);
-            pdr = keep ? pv * p.inv_keep : 0.f;
-            dpd = keep ? dpd * p.inv_keep : 0.f;
-          }
-          pd[r] = pdr;
-          ds[r] = pv * (dpd - dqv);
-        }
-        // transposed images [query][key]: this lane's 4 keys are contiguous
-        const int qr = u * 16 + (lane & 15);
-        put4(S1 + qr * RBS + 4 * g * ESZ, pd[0], pd[1], pd[2], pd[3], T());
-        put4(S2 + qr * RBS + 4 * g * ESZ, ds[0], ds[1], ds[2], ds[3], T());
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      Frag fa1, fa2;
-      frag_col<ImgS>(fa1, S1, 0, 0, lane);  // A(i = key, r = query)
-      frag_col<ImgS>(fa2, S2, 0, 0, lane);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        Frag fb;
-        frag_col<Img>(fb, Dimg, dt * 16, qc * 32, lane);
-        mma16(dv[dt], fa1, fb);
-        frag_col<Img>(fb, Qimg, dt * 16, qc * 32, lane);
-        mma16(dk[dt], fa2, fb);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int key = kt * 16 + 4 * g + r;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int d = dt * 16 + (lane & 15);
-        float vk = dk[dt][r] * p.scale;
-        if (p.rope_k) vk = rope_back(vk, key, d, p.rope_cos, p.rope_sin);
-        store_elem<T>(p.dk, (tok0 + key) * p.dk_ld + h * DH + d, vk);
-        store_elem<T>(p.dv, (tok0 + key) * p.dv_ld + h * DH + d, dv[dt][r]);
-      }
-    }
-  }
-
-  // ---------------- phase 2: dQ for 16-query tiles ----------------
-  for (int qt = w; qt < nkt; qt += 4) {
-    Frag fq[2], fo[2];
-    frag_row<Img>(fq[0], Qimg, qt * 16 + (lane & 15), 8 * g);
-    frag_row<Img>(fq[1], Qimg, qt * 16 + (lane & 15), 32 + 8 * g);
-    frag_row<Img>(fo[0], Dimg, qt * 16 + (lane & 15), 8 * g);
-    frag_row<Img>(fo[1], Dimg, qt * 16 + (lane & 15), 32 + 8 * g);
-    float lq[4], dqv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      lq[r] = lse_s[qt * 16 + 4 * g + r] * LOG2E;
-      dqv[r] = dq_s[qt * 16 + 4 * g + r];
-    }
-    f32x4 dq[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < nkt / 2; ++kc) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int kt = kc * 2 + u;
-        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-        Frag fb;
-        frag_row<Img>(fb, Kimg, kt * 16 + (lane & 15), 8 * g);
-        mma16(s, fq[0], fb);
-        frag_row<Img>(fb, Kimg, kt * 16 + (lane & 15), 32 + 8 * g);
-        mma16(s, fq[1], fb);
-        frag_row<Img>(fb, Vimg, kt * 16 + (lane & 15), 8 * g);
-        mma16(dp, fo[0], fb);
-        frag_row<Img>(fb, Vimg, kt * 16 + (lane & 15), 32 + 8 * g);
-        mma16(dp, fo[1], fb);
-        // accumulator: row = query (4g + r), col = key
-        const int key = kt * 16 + (lane & 15);
-        bool keep[4] = {true, true, true, true};
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 4 * g + r;
+        const float pv = exp2f(st[r] * c2 - lq);
+        float pdr = pv, dpd = dpt[r];
         if (p.thresh) {
-          const uint64_t idx = drop_idx(bh, T_, qt * 16 + 4 * g, key);
-          nstl_keep2(p.seed, idx, p.thresh, keep[0], keep[1]);
-          nstl_keep2(p.seed, idx + 2, p.thresh, keep[2], keep[3]);
+          const bool keep = nstl_keep(p.seed, drop_idx(bh, T_, q, key), p.thresh);
+          pdr = keep ? pv * p.inv_keep : 0.f;
+          dpd = keep ? dpd * p.inv_keep : 0.f;
         }
-        float ds[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = exp2f(s[r] * c2 - lq[r]);
-          float dpd = dp[r];
-          if (p.thresh) dpd = keep[r] ? dpd * p.inv_keep : 0.f;
-          ds[r] = pv * (dpd - dqv[r]);
-        }
-        // transposed image [key][query]
-        put4(S2 + (u * 16 + (lane & 15)) * RBS + 4 * g * ESZ, ds[0], ds[1], ds[2], ds[3], T());
+        pd[r] = pdr;
+        ds[r] = pv * (dpd - dqv);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      Frag fa;
-      frag_col<ImgS>(fa, S2, 0, 0, lane);  // A(i = query, r = key)
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        Frag fb;
-        frag_col<Img>(fb, Kimg, dt * 16, kc * 32, lane);
-        mma16(dq[dt], fa, fb);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // transposed images [query][key]: this lane's 4 keys are contiguous
+      const int qr = u * 16 + (lane & 15);
+      put4(S1 + qr * RBS + 4 * g * ESZ, pd[0], pd[1], pd[2], pd[3], T());
+      put4(S2 + qr * RBS + 4 * g * ESZ, ds[0], ds[1], ds[2], ds[3], T());
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    Frag fa1, fa2;
+    frag_col<ImgS>(fa1, S1, 0, 0, lane);  // A(i = key, r = query)
+    frag_col<ImgS>(fa2, S2, 0, 0, lane);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = qt * 16 + 4 * g + r;
+    for (int dt = 0; dt < 4; ++dt) {
+      Frag fb;
+      frag_col<Img>(fb, Dimg, dt * 16, qc * 32, lane);
+      mma16(dv[dt], fa1, fb);
+      frag_col<Img>(fb, Qimg, dt * 16, qc * 32, lane);
+      mma16(dk[dt], fa2, fb);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  float vk[4][4], vv[4][4];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int d = dt * 16 + (lane & 15);
-        float vq = dq[dt][r] * p.scale;
-        if (p.rope_q) vq = rope_back(vq, q, d, p.rope_cos, p.rope_sin);
-        store_elem<T>(p.dq, (tok0 + q) * p.dq_ld + h * DH + d, vq);
-      }
+  for (int r = 0; r < 4; ++r) {
+    const int key = k0 + 4 * g + r;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int d = dt * 16 + (lane & 15);
+      float x = dk[dt][r] * p.scale;
+      if (p.rope_k) x = rope_back(x, key, d, p.rope_cos, p.rope_sin);
+      vk[dt][r] = x;
+      vv[dt][r] = dv[dt][r];
     }
   }
+  store_tile16x64<T>(vk, S1, p.dk + ((tok0 + k0) * p.dk_ld + h * DH) * ESZ, p.dk_ld, lane);
+  store_tile16x64<T>(vv, S1, p.dv + ((tok0 + k0) * p.dv_ld + h * DH) * ESZ, p.dv_ld, lane);
 }
 
 size_t fwd_lds_bytes(int T, int esz) {
-  return (size_t)(2 * T + 64) * DH * esz + 4 * (size_t)std::max(T, 64) * 16 * esz;
+  return (size_t)(2 * T + FWD_QB) * DH * esz + (FWD_NT / 64) * (size_t)std::max(T, 64) * 16 * esz;
 }
-size_t bwd_lds_bytes(int T, int esz) {
-  return (size_t)4 * T * DH * esz + 2 * T * 4 + 4 * 2 * 32 * 16 * (size_t)esz;
+size_t bwd_lds_bytes(int T, int esz) {  // either backward kernel
+  return (size_t)2 * T * DH * esz + 2 * T * 4 + (BWD_NT / 64) * 2 * 32 * 16 * (size_t)esz;
 }
 
 // ---------------------------------------------------------------------------
@@ -672,13 +748,18 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   if (bwd) {
     NSTL_CHECK_ARG(a->dout && a->dq && a->dk && a->dv, "nstl_attn_bwd: null gradient tensor");
     NSTL_CHECK_ARG(a->dout_ld % vec == 0 && (uintptr_t)a->dout % 16 == 0, "nstl_attn_bwd: dout alignment");
+    NSTL_CHECK_ARG(a->dq_ld % vec == 0 && a->dk_ld % vec == 0 && a->dv_ld % vec == 0 &&
+                       ((uintptr_t)a->dq | (uintptr_t)a->dk | (uintptr_t)a->dv) % 16 == 0,
+                   "nstl_attn_bwd: dq/dk/dv must be 16-byte aligned");
     NSTL_CHECK_ARG(!(a->rope_q || a->rope_k) || (a->rope_cos && a->rope_sin), "nstl_attn_bwd: rope tables");
+    NSTL_CHECK_ARG(!use_fast(a) || a->dsum, "nstl_attn_bwd: dsum scratch [B*H*T] f32 missing");
   }
   p.q = (const char*)a->q; p.q_ld = a->q_ld;
   p.k = (const char*)a->k; p.k_ld = a->k_ld;
   p.v = (const char*)a->v; p.v_ld = a->v_ld;
   p.o = (char*)a->o; p.o_ld = a->o_ld;
   p.lse = a->lse;
+  p.dsum = a->dsum;
   p.dout = (const char*)a->dout; p.dout_ld = a->dout_ld;
   p.dq = (char*)a->dq; p.dq_ld = a->dq_ld;
   p.dk = (char*)a->dk; p.dk_ld = a->dk_ld;
@@ -694,10 +775,10 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
 }
 
 template <typename K>
-int launch(K kern, dim3 grid, size_t lds, hipStream_t st, const AttnParams& p, const char* what) {
+int launch(K kern, dim3 grid, size_t lds, hipStream_t st, const AttnParams& p, const char* what, int nt = NT) {
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return nstl::fail((int)e, "%s: LDS request %zu: %s", what, lds, hipGetErrorString(e));
-  hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, p);
+  hipLaunchKernelGGL(kern, grid, dim3(nt), lds, st, p);
   NSTL_LAUNCH_CHECK(what);
   return 0;
 }
@@ -716,10 +797,10 @@ extern "C" int nstl_attn_fwd(const nstl_attn_args* a, void* stream) {
     if (a->dtype == NSTL_BF16) return launch(attn_fwd_generic<bf16>, grid, lds, st, p, "nstl_attn_fwd generic");
     return launch(attn_fwd_generic<float>, grid, lds, st, p, "nstl_attn_fwd generic");
   }
-  dim3 grid((a->T + 63) / 64, a->B * a->H);
+  dim3 grid((a->T + FWD_QB - 1) / FWD_QB, a->B * a->H);
   const size_t lds = fwd_lds_bytes(a->T, esz);
-  if (a->dtype == NSTL_BF16) return launch(attn_fwd_kernel<bf16>, grid, lds, st, p, "nstl_attn_fwd");
-  return launch(attn_fwd_kernel<float>, grid, lds, st, p, "nstl_attn_fwd");
+  if (a->dtype == NSTL_BF16) return launch(attn_fwd_kernel<bf16>, grid, lds, st, p, "nstl_attn_fwd", FWD_NT);
+  return launch(attn_fwd_kernel<float>, grid, lds, st, p, "nstl_attn_fwd", FWD_NT);
 }
 
 extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
@@ -738,8 +819,12 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
     if ((rc = launch(attn_bwd_dq_generic<float>, grid, lq, st, p, "nstl_attn_bwd generic dq"))) return rc;
     return launch(attn_bwd_dkv_generic<float>, grid, lkv, st, p, "nstl_attn_bwd generic dkv");
   }
-  dim3 grid(a->B * a->H);
+  dim3 grid((a->T + BWD_ROWS - 1) / BWD_ROWS, a->B * a->H);
   const size_t lds = bwd_lds_bytes(a->T, esz);
-  if (a->dtype == NSTL_BF16) return launch(attn_bwd_kernel<bf16>, grid, lds, st, p, "nstl_attn_bwd");
-  return launch(attn_bwd_kernel<float>, grid, lds, st, p, "nstl_attn_bwd");
+  if (a->dtype == NSTL_BF16) {
+    if ((rc = launch(attn_bwd_dq_kernel<bf16>, grid, lds, st, p, "nstl_attn_bwd dq", BWD_NT))) return rc;
+    return launch(attn_bwd_dkv_kernel<bf16>, grid, lds, st, p, "nstl_attn_bwd dkv", BWD_NT);
+  }
+  if ((rc = launch(attn_bwd_dq_kernel<float>, grid, lds, st, p, "nstl_attn_bwd dq", BWD_NT))) return rc;
+  return launch(attn_bwd_dkv_kernel<float>, grid, lds, st, p, "nstl_attn_bwd dkv", BWD_NT);
 }

@@ -101,6 +101,7 @@ class _Buffers:
             self.dh = e(M, Fd)
             self.demb = e(M, D)
             self.dpred = torch.zeros(M, 64, dtype=dt, device=dev)
+            self.dsum = e(B * eng.H * T, dtype=f32)  # attention backward rowsum(dO * O)
             self.n_part = max(1, min(256, M // 4))
             self.ln_part = e(3, self.n_part, D, dtype=f32)
             self.col_part = e((M + 255) // 256, max(Fd, 3 * D, 64), dtype=f32)
@@ -374,6 +375,7 @@ class Seq2SeqEngine:
                                                         dv.data_ptr(), dv.stride(0))
         cs, sn = self.rope(T, self.dh)
         a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
+        a.dsum = self.cur.dsum.data_ptr()
         K.attn_bwd(a, stream=self.st)
 
     # --------------------------------------------------------------- forward

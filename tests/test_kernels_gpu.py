@@ -188,6 +188,8 @@ def test_attention_fwd_bwd(dt, T, dh):
     a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dqkv.data_ptr(), 3 * D, dqkv[:, D:].data_ptr(), 3 * D,
                                                     dqkv[:, 2 * D:].data_ptr(), 3 * D)
     a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
+    dsum = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
+    a.dsum = dsum.data_ptr()
     K.attn_bwd(a)
     torch.cuda.synchronize()
     # reference uses the kernel's own (rounded) output o for D = rowsum(dO*O) consistency
@@ -238,6 +240,8 @@ def test_attention_dropout_consistency(dt, T):
     dq, dk, dv = (torch.zeros(M, D, dtype=dt, device=DEV) for _ in range(3))
     a2.dout, a2.dout_ld = do.data_ptr(), D
     a2.dq, a2.dq_ld, a2.dk, a2.dk_ld, a2.dv, a2.dv_ld = dq.data_ptr(), D, dk.data_ptr(), D, dv.data_ptr(), D
+    dsum = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
+    a2.dsum = dsum.data_ptr()
     K.attn_bwd(a2)
     torch.cuda.synchronize()
     ro.backward(f64(do).view(B, T, H, dh).transpose(1, 2))
