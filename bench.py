@@ -39,7 +39,18 @@ def frames_flops(W, T, D, n_attn=24):
     return 6 * W + 12 * T * D * n_attn
 
 
-def cpu_baseline(cfg, T, budget_s=25.0):
+def gemm_traffic():
+    """Per-launch HBM bytes of the GEMM family from the committed PMC summary
+    (tools/run_pmc_traffic.sh -> profiles/*_gemm_traffic.json), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_gemm_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], HERE)
+
+
+def cpu_baseline(cfg, T, budget_s=20.0):
     """fp32 oracle step (reference semantics) on the host cores, bounded sample."""
     from oracle import model_ref
     # the GPU box's affinity mask shows the whole machine; the job's CPU share is
@@ -48,7 +59,7 @@ def cpu_baseline(cfg, T, budget_s=25.0):
     if os.environ.get("OMP_NUM_THREADS", "").isdigit():
         cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(cores)
-    B = 2
+    B = 4
     params = model_ref.seeded_params(model_ref.param_shapes(cfg["input_dim"], cfg["hidden_dim"], cfg["n_layers"],
                                                             cfg["output_dim"]), 0)
     tr = model_ref.OracleTrainer(params, cfg["num_heads"], dropout=cfg["dropout"])
@@ -59,7 +70,7 @@ def cpu_baseline(cfg, T, budget_s=25.0):
     tr.step(src, trg)  # warm-up
     log("cpu baseline warm-up step %.1fs (%d threads)" % (time.perf_counter() - t0, cores))
     n, t0 = 0, time.perf_counter()
-    while n < 2 or (time.perf_counter() - t0 < budget_s * 0.5 and n < 5):
+    while n < 3 or time.perf_counter() - t0 < budget_s:
         tr.step(src, trg)
         n += 1
         log("cpu baseline step %d done at %.1fs" % (n, time.perf_counter() - t0))
@@ -127,7 +138,9 @@ def main():
         e0.record(st)
         real_gemm(A, B_, C, M, N, Kd, **kw)
         e1.record(st)
-        gemm_events.append((e0, e1, 2.0 * M * N * Kd))
+        ebytes = 2 if A.dtype == torch.bfloat16 else 4
+        cbytes = 2 if C.dtype == torch.bfloat16 else 4
+        gemm_events.append((e0, e1, 2.0 * M * N * Kd, (M * Kd + N * Kd) * ebytes + M * N * cbytes))
 
     K.gemm = timed_gemm
     if world > 1:
@@ -150,8 +163,10 @@ def main():
     if not (loss_v == loss_v):
         raise RuntimeError("non-finite loss %r" % loss_v)
 
-    gemm_ms = sum(a.elapsed_time(b) for a, b, _ in gemm_events)
-    gemm_flops = sum(f for _, _, f in gemm_events)
+    gemm_ms = sum(a.elapsed_time(b) for a, b, _, _ in gemm_events)
+    gemm_flops = sum(f for _, _, f, _ in gemm_events)
+    gemm_alg_bytes = sum(x for _, _, _, x in gemm_events) / max(1, len(gemm_events))
+    traffic, traffic_src = gemm_traffic()
     n_launch = len(gemm_events)
     achieved_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
     ms_step = elapsed / args.steps * 1e3
@@ -176,9 +191,13 @@ def main():
             "config": {"workload": "228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam)",
                        "model": "NeuroSync Seq2Seq 228M", "global_batch": B * world, "seq_len": T,
                        "frames_per_step": B * T * world, "parallelism": "dp%d" % world},
-            "roofline": {"bound": "mfma", "kernel": "nstl gemm_kernel (all launches in timed region)",
+            "roofline": {"bound": "mfma", "kernel": "nstl GEMM family (gemm256r_kernel + gemm_kernel), all launches "
+                                                    "in the timed region",
                          "achieved": round(achieved_tf, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": round(gemm_alg_bytes),
                          "launches": n_launch, "avg_launch_us": round(gemm_ms * 1e3 / max(1, n_launch), 2),
                          "gemm_share_of_step": round(gemm_ms / (elapsed * 1e3), 3)},
             "step_tflops_per_gpu": round(step_tf, 1),

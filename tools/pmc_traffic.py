@@ -1,0 +1,52 @@
+"""Aggregate rocprofv3 FETCH_SIZE / WRITE_SIZE passes into the per-launch HBM
+traffic of the GEMM family (the bench's dominant kernel) -> JSON for bench.py.
+
+  python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> <tag>
+
+Corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE is reported in KiB and counts
+a wide coalesced streaming read at exactly half its bytes on gfx950 -> x2;
+WRITE_SIZE (KiB) is exact for 16-byte-per-lane stores.  Both come from the L2's
+memory-side request counters (Infinity-Cache hits included)."""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter):
+    vals = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            if "gemm" not in name or "splitk" in name:
+                continue
+            key = int(r["Dispatch_Id"])
+            vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+    return vals
+
+
+def main():
+    fetch_dir, write_dir, out, tag = sys.argv[1:5]
+    fetch = per_dispatch(fetch_dir, "FETCH_SIZE")
+    write = per_dispatch(write_dir, "WRITE_SIZE")
+    n_f, n_w = len(fetch), len(write)
+    f_kib = sum(fetch.values()) / max(1, n_f)
+    w_kib = sum(write.values()) / max(1, n_w)
+    res = {
+        "tag": tag,
+        "kernel": "nstl GEMM family (gemm256r_kernel / gemm_kernel), every dispatch of the profiled bench run",
+        "dispatches_fetch": n_f, "dispatches_write": n_w,
+        "fetch_size_kib_per_launch_raw": round(f_kib, 1),
+        "write_size_kib_per_launch": round(w_kib, 1),
+        "hbm_bytes_per_launch": round((2.0 * f_kib + w_kib) * 1024.0),
+        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950 FETCH_SIZE counts streaming reads at half their bytes)",
+    }
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
