@@ -88,6 +88,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--feature-steps", type=int, default=10,
+                    help="steps of the feature-inclusive variant (raw audio -> GPU features -> step); 0 = skip")
     args = ap.parse_args()
 
     from neurosync_trainer_lite_amd import _hip as K
@@ -174,6 +176,54 @@ def main():
     value = frames / elapsed
     step_tf = frames_flops(W, T, cfg["hidden_dim"]) * B * T * world / (elapsed / args.steps) / 1e12 / world
 
+    # feature-inclusive variant (BASELINE C2's on-GPU STFT/mel path): per step,
+    # raw 88.2 kHz audio for the step's B*T frames -> nstl_features -> windows
+    feat = None
+    if args.feature_steps > 0:
+        from neurosync_trainer_lite_amd.utils.audio.extraction.extract_features import extract_audio_features_device
+        sr = cfg["sr"]
+        n_samp = int(B * T / 60.0 * sr) + 1470
+        tt = torch.arange(n_samp, device=dev, dtype=torch.float32) / sr
+        gen = torch.Generator(device=dev).manual_seed(7 + rank)
+        audio = (0.6 * torch.sin(2 * 3.14159265 * 180.0 * tt) * (0.55 + 0.45 * torch.sin(2 * 3.14159265 * 4.0 * tt))
+                 + 0.01 * torch.randn(n_samp, device=dev, generator=gen))
+        audio = audio / audio.abs().max()
+
+        def feat_step():
+            f = extract_audio_features_device(audio, sr, device=dev)
+            src_f = f[:B * T].view(B, T, -1)
+            opt.zero_grad()
+            loss_f = crit(model(src_f), trg)
+            loss_f.backward()
+            opt.step(max_norm=2.0)
+            return loss_f
+
+        feat_step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.feature_steps):
+            feat_step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el_f = time.perf_counter() - t1
+        if world > 1:
+            tt_ = torch.tensor([el_f], device=dev)
+            torch.distributed.all_reduce(tt_, op=torch.distributed.ReduceOp.MAX)
+            el_f = tt_.item()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        extract_audio_features_device(audio, sr, device=dev)
+        e1.record()
+        torch.cuda.synchronize()
+        feat = {"value": round(B * T * world * args.feature_steps / el_f, 1), "unit": "frames/s",
+                "ms_per_step": round(el_f / args.feature_steps * 1e3, 3), "steps": args.feature_steps,
+                "feature_ms_per_step": round(e0.elapsed_time(e1), 3),
+                "workload": "per step: %.1f s of synthetic 88.2 kHz audio per GPU -> GPU MFCC(+d,dd)+autocorr "
+                            "features [%d frames x 256] -> the same train step" % (n_samp / sr, B * T)}
+
     if rank == 0:
         out = {
             "metric": "train frames/sec (audio->blendshape) 228M cfg",
@@ -204,6 +254,8 @@ def main():
             "step_mfma_frac": round(step_tf / BF16_DENSE_PEAK_TFLOPS, 4),
             "final_loss": round(loss_v, 4),
         }
+        if feat is not None:
+            out["feature_inclusive"] = feat
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, T)
         print(json.dumps(out), flush=True)

@@ -117,6 +117,10 @@ int nstl_ln_bwd(const nstl_ln_args* args, void* stream);
 
 /* out[j] = beta*out[j] + sum_p part[p][j]  (f32) */
 int nstl_reduce_rows(const float* part, int n_part, int cols, float* out, float beta, void* stream);
+/* Three such reductions in one launch: matrix m at part + m*mat_stride -> out_m
+ * (LayerNorm backward's dgamma / dbeta / fused bias-grad partials). */
+int nstl_reduce_rows3(const float* part, int64_t mat_stride, int n_mat, int n_part, int cols, float* out0,
+                      float* out1, float* out2, float beta, void* stream);
 /* Column sums of X[rows][cols] (bias gradients): out[j] = beta*out[j] + sum_i X[i][j].
  * partial: [ceil(rows/256)][cols] f32 scratch. */
 int nstl_colsum(int dtype, const void* x, int64_t ld, int rows, int cols, float* partial,

@@ -86,7 +86,7 @@ class AdamArgs(ctypes.Structure):
 # every symbol include/nstl.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "nstl_gemm", "nstl_gemm_workspace_bytes", "nstl_attn_fwd", "nstl_attn_bwd", "nstl_ln_fwd", "nstl_ln_bwd",
-    "nstl_reduce_rows", "nstl_colsum", "nstl_rope", "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step",
+    "nstl_reduce_rows", "nstl_reduce_rows3", "nstl_colsum", "nstl_rope", "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step",
     "nstl_cast", "nstl_copy2d", "nstl_autocorr", "nstl_features", "nstl_features_workspace_bytes",
     "nstl_features_frames", "nstl_last_error_string", "nstl_version",
 ]
@@ -112,6 +112,7 @@ def lib():
         L.nstl_ln_fwd.argtypes = [P(LnArgs), _vp]
         L.nstl_ln_bwd.argtypes = [P(LnArgs), _vp]
         L.nstl_reduce_rows.argtypes = [_vp, _i32, _i32, _vp, _f32, _vp]
+        L.nstl_reduce_rows3.argtypes = [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]
         L.nstl_colsum.argtypes = [_i32, _vp, _i64, _i32, _i32, _vp, _vp, _f32, _vp]
         L.nstl_rope.argtypes = [_i32, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _vp]
         L.nstl_loss_fwd_bwd.argtypes = [P(LossArgs), _vp]
@@ -212,6 +213,13 @@ def ln_fwd(a, stream=None):
 
 def ln_bwd(a, stream=None):
     check(lib().nstl_ln_bwd(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_ln_bwd")
+
+
+def reduce_rows3(part, n_part, cols, outs, beta, stream=None):
+    """part: [n_mat][rows >= n_part][cols] f32; outs: n_mat f32 vectors."""
+    ptrs = [o.data_ptr() for o in outs] + [None] * (3 - len(outs))
+    check(lib().nstl_reduce_rows3(part.data_ptr(), part.stride(0), len(outs), n_part, cols, ptrs[0], ptrs[1], ptrs[2],
+                                  beta, stream if stream is not None else stream_of()), "nstl_reduce_rows3")
 
 
 def reduce_rows(part, n_part, cols, out, beta, stream=None):

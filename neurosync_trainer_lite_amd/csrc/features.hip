@@ -7,6 +7,7 @@
 // np.correlate and keeps n_lags+1 of them), normalise by lag 0 when non-zero,
 // drop lag 0, replicate near-silent edge frames.  One workgroup per frame; the
 // windowed frame lives in LDS as f64 (the reference is f64 from the window on).
+#include <algorithm>
 #include <cmath>
 #include <mutex>
 #include <vector>
@@ -19,9 +20,19 @@ namespace {
 constexpr int NT = 256;
 constexpr int MAX_FRAME = 4096;
 
+// One workgroup per frame.  Lags 0..n_lags are computed by 24 groups of 8
+// consecutive lags x 10 chunks of the sample index: a thread slides an 8-wide
+// register window along w (two LDS reads per 8 f64 FMAs), chunk partials are
+// summed in LDS.  w is zero-padded past the frame, so sum_{k<L} w[k] w[k+lag]
+// needs no per-lag bound.
+constexpr int AC_LG = 8;      // lags per thread
+constexpr int AC_GROUPS = 24; // lag groups: up to 192 lags (0..n_lags <= 191)
+constexpr int AC_CHUNKS = 10; // sample-index chunks
+
 __global__ __launch_bounds__(NT) void autocorr_kernel(const float* y, int64_t n, int L, int hop, int n_lags,
-                                                       double* out) {
-  __shared__ double w[MAX_FRAME];
+                                                       const double* __restrict__ hann, double* out) {
+  __shared__ double w[MAX_FRAME + AC_LG * AC_GROUPS];
+  __shared__ double part[AC_CHUNKS][AC_LG * AC_GROUPS];
   __shared__ double red[NT / 64];
   const int f = blockIdx.x, tid = threadIdx.x;
   const int64_t start = (int64_t)f * hop - L / 2;
@@ -34,6 +45,7 @@ __global__ __launch_bounds__(NT) void autocorr_kernel(const float* y, int64_t n,
     w[k] = v;
     s += v;
   }
+  for (int k = L + tid; k < L + AC_LG * AC_GROUPS; k += NT) w[k] = 0.0;
   s = wave_sum_d(s);
   if ((tid & 63) == 0) red[tid >> 6] = s;
   __syncthreads();
@@ -43,20 +55,66 @@ __global__ __launch_bounds__(NT) void autocorr_kernel(const float* y, int64_t n,
   const float mean_f = (float)mean;
   for (int k = tid; k < L; k += NT) {
     const float c = (float)w[k] - mean_f;
-    const double hann = L > 1 ? 0.5 - 0.5 * cos(2.0 * M_PI * k / (L - 1)) : 1.0;
-    w[k] = (double)c * hann;
+    w[k] = (double)c * hann[k];
+  }
+  __syncthreads();
+  if (tid < AC_GROUPS * AC_CHUNKS) {
+    const int g = tid % AC_GROUPS, c = tid / AC_GROUPS;
+    const int l0 = g * AC_LG;
+    const int chunk = (L + AC_CHUNKS - 1) / AC_CHUNKS;
+    const int k0 = c * chunk, k1 = min(L, k0 + chunk);
+    double acc[AC_LG], win[AC_LG];
+#pragma unroll
+    for (int r = 0; r < AC_LG; ++r) {
+      acc[r] = 0.0;
+      win[r] = w[k0 + l0 + r];
+    }
+    for (int k = k0; k < k1; ++k) {
+      const double a = w[k];
+#pragma unroll
+      for (int r = 0; r < AC_LG; ++r) acc[r] = fma(a, win[r], acc[r]);
+#pragma unroll
+      for (int r = 0; r < AC_LG - 1; ++r) win[r] = win[r + 1];
+      win[AC_LG - 1] = w[k + l0 + AC_LG];
+    }
+#pragma unroll
+    for (int r = 0; r < AC_LG; ++r) part[c][l0 + r] = acc[r];
   }
   __syncthreads();
   __shared__ double ac0;
   for (int lag = tid; lag <= n_lags; lag += NT) {
     double acc = 0.0;
-    for (int k = 0; k < L - lag; ++k) acc += w[k] * w[k + lag];
+#pragma unroll
+    for (int c = 0; c < AC_CHUNKS; ++c) acc += part[c][lag];
     if (lag == 0) ac0 = acc;
     if (lag > 0) out[(int64_t)f * n_lags + (lag - 1)] = acc;
   }
   __syncthreads();
   if (ac0 != 0.0)
     for (int lag = tid; lag < n_lags; lag += NT) out[(int64_t)f * n_lags + lag] /= ac0;
+}
+
+// np.hanning(L) (symmetric), computed on the host in f64 once per (device, L)
+int get_hann(int L, const double** out) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<int, int>, double*>> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nstl::fail((int)hipErrorNoDevice, "autocorr: no device");
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& e : cache)
+    if (e.first.first == dev && e.first.second == L) {
+      *out = e.second;
+      return 0;
+    }
+  std::vector<double> h(L);
+  for (int k = 0; k < L; ++k) h[k] = L > 1 ? 0.5 - 0.5 * std::cos(2.0 * M_PI * k / (L - 1)) : 1.0;
+  double* d = nullptr;
+  if (hipMalloc((void**)&d, L * sizeof(double)) != hipSuccess) return nstl::fail((int)hipErrorOutOfMemory, "autocorr: alloc");
+  if (hipMemcpy(d, h.data(), L * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+    return nstl::fail((int)hipErrorUnknown, "autocorr: upload");
+  cache.push_back({{dev, L}, d});
+  *out = d;
+  return 0;
 }
 
 __global__ void autocorr_edges(double* out, int n_frames, int n_lags) {
@@ -85,13 +143,16 @@ extern "C" int nstl_autocorr(const float* y, int64_t n_samples, int frame_length
                              double* out, int n_frames, void* stream) {
   NSTL_CHECK_ARG(y && out && n_samples > frame_length / 2 && frame_length > 1 && frame_length <= MAX_FRAME,
                  "nstl_autocorr: bad sizes");
-  NSTL_CHECK_ARG(hop_length > 0 && n_lags > 0 && n_lags < frame_length && n_lags < 512, "nstl_autocorr: bad lags");
+  NSTL_CHECK_ARG(hop_length > 0 && n_lags > 0 && n_lags < frame_length && n_lags < AC_LG * AC_GROUPS,
+                 "nstl_autocorr: bad lags");
   const int64_t padded = n_samples + 2 * (frame_length / 2);
   const int expect = (int)((padded - frame_length) / hop_length + 1);
   NSTL_CHECK_ARG(n_frames == expect, "nstl_autocorr: n_frames %d != %d", n_frames, expect);
   hipStream_t st = (hipStream_t)stream;
+  const double* hann = nullptr;
+  if (int rc = get_hann(frame_length, &hann)) return rc;
   hipLaunchKernelGGL(autocorr_kernel, dim3(n_frames), dim3(NT), 0, st, y, n_samples, frame_length, hop_length,
-                     n_lags, out);
+                     n_lags, hann, out);
   NSTL_LAUNCH_CHECK("nstl_autocorr");
   hipLaunchKernelGGL(autocorr_edges, dim3(1), dim3(256), 0, st, out, n_frames, n_lags);
   NSTL_LAUNCH_CHECK("nstl_autocorr edges");
@@ -125,8 +186,8 @@ struct FeatTables {
   int dev = -1, sr = 0, n_fft = 0, nb = 0, kp = 0;
   float* basis = nullptr;   // [2nb][kp]: rows 0..nb-1 cos, nb..2nb-1 sin (window in frames)
   float* window = nullptr;  // [n_fft] periodic Hann
-  float* mel = nullptr;     // [N_MELS][nb]
-  int* band = nullptr;      // [N_MELS][2] first/last+1 non-zero bin
+  float* melK = nullptr;    // [N_MELS][nbp] zero-padded GEMM operand (K-major)
+  int nbp = 0;
   float* dct = nullptr;     // [N_MFCC][N_MELS]
   float* sg = nullptr;      // [2 orders][SG_W fit positions][SG_W taps]
 };
@@ -211,8 +272,9 @@ int get_tables(int sr, const FeatTables** out) {
   t->nb = t->n_fft / 2 + 1;
   t->kp = (t->n_fft + 3) / 4 * 4;
   const int n_fft = t->n_fft, nb = t->nb, kp = t->kp;
-  std::vector<float> basis((size_t)2 * nb * kp, 0.f), win(n_fft), mel((size_t)N_MELS * nb, 0.f), dct(N_MFCC * N_MELS);
-  std::vector<int> band(2 * N_MELS);
+  t->nbp = (nb + 63) / 64 * 64;
+  std::vector<float> basis((size_t)2 * nb * kp, 0.f), win(n_fft), dct(N_MFCC * N_MELS);
+  std::vector<float> melK((size_t)N_MELS * t->nbp, 0.f);
   for (int k = 0; k < nb; ++k)
     for (int n = 0; n < n_fft; ++n) {
       // exact integer phase reduction keeps the f64 argument small
@@ -227,20 +289,13 @@ int get_tables(int sr, const FeatTables** out) {
   for (int i = 0; i < N_MELS + 2; ++i) mel_f[i] = mel_to_hz(m_lo + (m_hi - m_lo) * i / (N_MELS + 1));
   for (int i = 0; i < N_MELS; ++i) {
     const double enorm = 2.0 / (mel_f[i + 2] - mel_f[i]);
-    int lo = nb, hi = 0;
     for (int b = 0; b < nb; ++b) {
       const double fb = b * ((double)sr / n_fft);
       const double lower = -(mel_f[i] - fb) / (mel_f[i + 1] - mel_f[i]);
       const double upper = (mel_f[i + 2] - fb) / (mel_f[i + 2] - mel_f[i + 1]);
       const double w = std::max(0.0, std::min(lower, upper)) * enorm;
-      mel[(size_t)i * nb + b] = (float)w;
-      if (w > 0) {
-        lo = std::min(lo, b);
-        hi = b + 1;
-      }
+      melK[(size_t)i * t->nbp + b] = (float)w;
     }
-    band[2 * i] = lo < hi ? lo : 0;
-    band[2 * i + 1] = hi;
   }
   for (int k = 0; k < N_MFCC; ++k)
     for (int m = 0; m < N_MELS; ++m)
@@ -251,8 +306,7 @@ int get_tables(int sr, const FeatTables** out) {
   savgol_table(2, sg + SG_W * SG_W);
   int rc = upload((void**)&t->basis, basis.data(), basis.size() * 4);
   if (!rc) rc = upload((void**)&t->window, win.data(), win.size() * 4);
-  if (!rc) rc = upload((void**)&t->mel, mel.data(), mel.size() * 4);
-  if (!rc) rc = upload((void**)&t->band, band.data(), band.size() * 4);
+  if (!rc) rc = upload((void**)&t->melK, melK.data(), melK.size() * 4);
   if (!rc) rc = upload((void**)&t->dct, dct.data(), dct.size() * 4);
   if (!rc) rc = upload((void**)&t->sg, sg, sizeof(sg));
   if (rc) return rc;
@@ -273,53 +327,38 @@ __global__ __launch_bounds__(256) void stft_frames_kernel(const float* __restric
   }
 }
 
-__device__ __forceinline__ int ordered_key(float v) {
-  const int i = __float_as_int(v);
-  return i >= 0 ? i : i ^ 0x7fffffff;
-}
-__device__ __forceinline__ float from_key(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff); }
-
-// one wave per frame: power spectrum -> mel bands -> dB
-__global__ __launch_bounds__(256) void mel_db_kernel(const float* __restrict__ X, int F, int nb,
-                                                     const float* __restrict__ mel, const int* __restrict__ band,
-                                                     float* __restrict__ db, int* __restrict__ max_key) {
-  extern __shared__ float pw[];  // [4][nb]
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int f = blockIdx.x * 4 + wave;
-  float* p = pw + wave * nb;
-  float mx = -INFINITY;
-  if (f < F) {
-    const float* xr = X + (int64_t)f * 2 * nb;
-    for (int b = lane; b < nb; b += 64) {
-      const float c = xr[b], s = xr[nb + b];
-      p[b] = c * c + s * s;
+// |X|^2 for bins 0..nb-1 into rows of nbp (zero tail): the mel GEMM's A operand
+__global__ __launch_bounds__(256) void power_kernel(const float* __restrict__ X, int F, int nb, int nbp,
+                                                   float* __restrict__ P) {
+  const int64_t total = (int64_t)F * nbp;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int f = (int)(e / nbp), b = (int)(e % nbp);
+    float v = 0.f;
+    if (b < nb) {
+      const float c = X[(int64_t)f * 2 * nb + b], s = X[(int64_t)f * 2 * nb + nb + b];
+      v = c * c + s * s;
     }
+    P[e] = v;
   }
-  __syncthreads();
-  if (f < F) {
-    for (int m = lane; m < N_MELS; m += 64) {
-      const int lo = band[2 * m], hi = band[2 * m + 1];
-      const float* w = mel + (int64_t)m * nb;
-      float acc = 0.f;
-      for (int b = lo; b < hi; ++b) acc = fmaf(w[b], p[b], acc);
-      const float v = 10.f * log10f(fmaxf(1e-10f, acc));
-      db[(int64_t)f * N_MELS + m] = v;
-      mx = fmaxf(mx, v);
-    }
-  }
-  mx = wave_max(mx);
-  if (lane == 0 && f < F) atomicMax(max_key, ordered_key(mx));
 }
 
-// mfcc[k][f] = sum_m dct[k][m] * max(db[f][m], max_db - 80)
-__global__ __launch_bounds__(256) void dct_kernel(const float* __restrict__ db, int F, const float* __restrict__ dct,
+// clip-wide max of the mel power (non-negative floats order as their bits)
+__global__ __launch_bounds__(256) void melmax_kernel(const float* __restrict__ mel, int64_t n, int* __restrict__ key) {
+  float m = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) m = fmaxf(m, mel[e]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(key, __float_as_int(m));
+}
+
+// mfcc[k][f] = sum_m dct[k][m] * max(db[f][m], max_db - 80), db = 10 log10(max(1e-10, mel))
+__global__ __launch_bounds__(256) void dct_kernel(const float* __restrict__ mel, int F, const float* __restrict__ dct,
                                                   const int* __restrict__ max_key, float* __restrict__ mfcc) {
   __shared__ float tile[64][N_MELS + 1];
   const int f0 = blockIdx.x * 64;
-  const float floor_db = from_key(*max_key) - 80.f;
+  const float floor_db = 10.f * log10f(fmaxf(1e-10f, __int_as_float(*max_key))) - 80.f;
   for (int i = threadIdx.x; i < 64 * N_MELS; i += 256) {
     const int r = i / N_MELS, m = i % N_MELS;
-    tile[r][m] = f0 + r < F ? fmaxf(db[(int64_t)(f0 + r) * N_MELS + m], floor_db) : 0.f;
+    tile[r][m] = f0 + r < F ? fmaxf(10.f * log10f(fmaxf(1e-10f, mel[(int64_t)(f0 + r) * N_MELS + m])), floor_db) : 0.f;
   }
   __syncthreads();
   const int r = threadIdx.x & 63;
@@ -420,7 +459,7 @@ FeatLayout feat_layout(int64_t n_samples, int sr) {
   return L;
 }
 
-__global__ void init_key(int* k) { *k = INT_MIN; }
+__global__ void init_key(int* k) { *k = 0; }  // mel power >= 0: bits of 0.f
 }  // namespace
 
 extern "C" int64_t nstl_features_workspace_bytes(int64_t n_samples, int sr) {
@@ -461,9 +500,21 @@ extern "C" int nstl_features(const float* y, int64_t n_samples, int sr, float* o
   g.A = frames; g.lda = L.kp; g.B = T->basis; g.ldb = L.kp; g.C = X; g.ldc = 2 * L.nb;
   g.M = L.F; g.N = 2 * L.nb; g.K = L.kp; g.alpha = 1.f; g.beta = 0.f; g.epilogue = NSTL_EPI_NONE; g.split_k = 1;
   if (int rc = nstl_gemm(&g, stream)) return rc;
+  // mel power = |X|^2 (frames buffer reused) @ mel^T, f32 MFMA GEMM
+  float* P = frames;
+  const int64_t np = (int64_t)L.F * T->nbp;
+  hipLaunchKernelGGL(power_kernel, dim3((unsigned)std::min<int64_t>((np + 255) / 256, 65536)), dim3(256), 0, st, X,
+                     L.F, L.nb, T->nbp, P);
+  NSTL_LAUNCH_CHECK("nstl_features power");
+  nstl_gemm_args gm = {};
+  gm.dtype = NSTL_F32; gm.c_dtype = NSTL_F32; gm.a_kmajor = 1; gm.b_kmajor = 1;
+  gm.A = P; gm.lda = T->nbp; gm.B = T->melK; gm.ldb = T->nbp; gm.C = db; gm.ldc = N_MELS;
+  gm.M = L.F; gm.N = N_MELS; gm.K = T->nbp; gm.alpha = 1.f; gm.beta = 0.f; gm.epilogue = NSTL_EPI_NONE; gm.split_k = 1;
+  if (int rc = nstl_gemm(&gm, stream)) return rc;
   hipLaunchKernelGGL(init_key, dim3(1), dim3(1), 0, st, key);
-  hipLaunchKernelGGL(mel_db_kernel, dim3((L.F + 3) / 4), dim3(256), 4 * L.nb * sizeof(float), st, X, L.F, L.nb,
-                     T->mel, T->band, db, key);
+  const int64_t nm = (int64_t)L.F * N_MELS;
+  hipLaunchKernelGGL(melmax_kernel, dim3((unsigned)std::min<int64_t>((nm + 255) / 256, 1024)), dim3(256), 0, st, db,
+                     nm, key);
   NSTL_LAUNCH_CHECK("nstl_features mel");
   hipLaunchKernelGGL(dct_kernel, dim3((L.F + 63) / 64), dim3(256), 0, st, db, L.F, T->dct, key, mf);
   NSTL_LAUNCH_CHECK("nstl_features dct");

@@ -285,6 +285,40 @@ extern "C" int nstl_colsum(int dtype, const void* x, int64_t ld, int rows, int c
   return 0;
 }
 
+// Up to three [n_part][cols] partial-sum matrices (stride mat_stride floats)
+// reduced over rows into three outputs in one launch: 64 columns x 16 row
+// groups per block, blockIdx.y = matrix.
+__global__ __launch_bounds__(1024) void reduce_rows3_kernel(const float* part, int64_t mat_stride, int n_part,
+                                                            int cols, float* o0, float* o1, float* o2, float beta) {
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cl;
+  float* out = blockIdx.y == 0 ? o0 : blockIdx.y == 1 ? o1 : o2;
+  const float* pm = part + blockIdx.y * mat_stride;
+  float s = 0.f;
+  if (j < cols)
+    for (int k = rg; k < n_part; k += 16) s += pm[(int64_t)k * cols + j];
+  __shared__ float red[16][64];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && j < cols && out != nullptr) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][cl];
+    out[j] = beta != 0.f ? beta * out[j] + t : t;
+  }
+}
+
+extern "C" int nstl_reduce_rows3(const float* part, int64_t mat_stride, int n_mat, int n_part, int cols, float* out0,
+                                 float* out1, float* out2, float beta, void* stream) {
+  NSTL_CHECK_ARG(part && out0 && n_mat >= 1 && n_mat <= 3 && n_part > 0 && cols > 0, "nstl_reduce_rows3: bad args");
+  NSTL_CHECK_ARG(n_mat < 2 || out1, "nstl_reduce_rows3: out1 missing");
+  NSTL_CHECK_ARG(n_mat < 3 || out2, "nstl_reduce_rows3: out2 missing");
+  hipLaunchKernelGGL(reduce_rows3_kernel, dim3((cols + 63) / 64, n_mat), dim3(1024), 0, (hipStream_t)stream, part,
+                     mat_stride, n_part, cols, out0, out1, out2, beta);
+  NSTL_LAUNCH_CHECK("nstl_reduce_rows3");
+  return 0;
+}
+
 extern "C" int nstl_reduce_rows(const float* part, int n_part, int cols, float* out, float beta, void* stream) {
   NSTL_CHECK_ARG(part && out && n_part > 0 && cols > 0, "nstl_reduce_rows: bad args");
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + 63) / 64), dim3(NT), 0, (hipStream_t)stream, part, n_part,

@@ -292,11 +292,9 @@ class Seq2SeqEngine:
             target, tiles = 256, t256
         else:
             target, tiles = 512, ((n + 127) // 128) * ((k + 127) // 128)
-        s = 1
-        while s * 2 * tiles <= target and s < 16:
-            s *= 2
-        while s > 1 and (m // s < 1024 or m % (64 * s)):
-            s //= 2
+        s = max(1, min(16, target // tiles))
+        while s > 1 and m // s < 1024:
+            s -= 1
         return s
 
     # ------------------------------------------------------------ primitives
@@ -355,10 +353,10 @@ class Seq2SeqEngine:
         if bias_of is not None:
             a.dbranch_part = bb.ln_part[2].data_ptr()
         K.ln_bwd(a, stream=self.st)
-        K.reduce_rows(bb.ln_part[0], bb.n_part, self.D, self.gb(prefix + ".weight"), bf, stream=self.st)
-        K.reduce_rows(bb.ln_part[1], bb.n_part, self.D, self.gb(prefix + ".bias"), bf, stream=self.st)
+        outs = [self.gb(prefix + ".weight"), self.gb(prefix + ".bias")]
         if bias_of is not None:
-            K.reduce_rows(bb.ln_part[2], bb.n_part, self.D, self.gb(bias_of), bf, stream=self.st)
+            outs.append(self.gb(bias_of))
+        K.reduce_rows3(bb.ln_part, bb.n_part, self.D, outs, bf, stream=self.st)
 
     def _attn(self, q, k, v, o, lse, seed, T, B):
         a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
