@@ -135,7 +135,8 @@ def main():
     real_gemm = K.gemm
 
     def timed_gemm(A, B_, C, M, N, Kd, **kw):
-        st = torch.cuda.current_stream()
+        # the stream the GEMM is launched on (weight-gradient GEMMs run on a side stream)
+        st = torch.cuda.ExternalStream(kw["stream"]) if kw.get("stream") else torch.cuda.current_stream()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         real_gemm(A, B_, C, M, N, Kd, **kw)

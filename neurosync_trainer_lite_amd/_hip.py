@@ -12,7 +12,9 @@ import os
 
 import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnstl_hip.so")
+# NSTL_LIB_PATH: A/B timing of another build of the same sources (tools/ only)
+LIB_PATH = os.environ.get("NSTL_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                            "libnstl_hip.so")
 
 F32, BF16 = 0, 1
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU_DROP, EPI_BIAS_ROPE, EPI_DRELU_DROP = 0, 1, 2, 3, 4

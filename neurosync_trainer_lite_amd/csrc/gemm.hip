@@ -513,9 +513,11 @@ NSTL_DEV void retire_next(int t, int nk) {
 // The epilogue kind is a template parameter (EM_*), so each instantiation
 // carries only its own elementwise code: the generic, branchy form measured
 // ~800 VALU + 600 SALU instructions per wave per tile (≈5 µs per 256^2 tile,
-// VALU-issue bound).  vmcnt counts loads and stores together, so any input
-// load (RoPE cos/sin, the dReLU operand, old C) is issued one iteration ahead,
-// before the current store, and the bias (fixed per lane) once per tile.
+// VALU-issue bound).  vmcnt counts loads and stores together, so the input
+// loads of a 64-row pass (RoPE cos/sin, the dReLU operand, old C) are all
+// issued before the pass's first store: one memory latency per pass (loading
+// one iteration ahead paid ~1 µs per iteration).  The bias (fixed per lane)
+// is loaded once per tile.
 enum { EM_GENERIC = 0, EM_BF16 = 1, EM_RELU_DROP = 2, EM_ROPE = 3, EM_DRELU = 4, EM_F32 = 5, EM_WS = 6 };
 
 constexpr int RING_EPI_RB = 64 * 4 + 16;          // padded f32 scratch row
@@ -539,6 +541,9 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
   constexpr int LPR = 64 / CW;   // lanes per 64-column row (8 / 16)
   constexpr int RPI = 64 / LPR;  // rows per wave instruction (8 / 4)
   constexpr int NIT = 64 / RPI;  // iterations per 64-row pass
+  // per-iteration input registers, all issued before a pass starts
+  constexpr int ND = EM == EM_DRELU ? NIT : 1;                          // dReLU operand (bf16 x 8)
+  constexpr int NF = EM == EM_F32 ? NIT : (EM == EM_ROPE ? 2 * NIT : 1);  // old C / cos|sin (f32 x 4)
   char* const C = EM == EM_WS ? (char*)(p.ws + (int64_t)blockIdx.y * p.M * p.N) : p.C;
   const int64_t ldc = EM == EM_WS ? p.N : p.ldc;
   const int c = (lane % LPR) * CW, j = col0 + c;
@@ -554,50 +559,67 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
   }
   const bool rope_col = EM == EM_ROPE && j < p.rope_cols;
   const int rhalf = p.rope_dim >> 1;
+  // cos/sin of 8 columns = 4 consecutive table entries (16 B) when rope_dim % 8 == 0
+  const bool rope_vec = (p.rope_dim & 7) == 0;
+  const int r0 = lane / LPR;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
-    stage_half(acc, half, p.alpha, lane, scr);
-    const int r0 = lane / LPR;
     const int ib = row0 + half * 64 + r0;
-    // inputs of iteration it, loaded one iteration ahead
-    float in_a[CW], in_b[CW];
-    auto prefetch = [&](int i, float* xa, float* xb) {
-      if (i >= p.M || !colok) return;
-      if (EM == EM_ROPE && rope_col) {
-        const int t = i % p.rope_T;
+    // Issue every input load of this pass first: one memory latency per pass
+    // instead of one per iteration (and no load queued behind the stores).
+    bf16x8 ind[ND];
+    f32x4 inf[NF];
 #pragma unroll
-        for (int e = 0; e < CW; e += 2) {
-          const int pr = ((j + e) % p.rope_dim) >> 1;
-          xa[e] = p.rope_cos[t * rhalf + pr];
-          xa[e + 1] = p.rope_sin[t * rhalf + pr];
-        }
-      } else if (EM == EM_DRELU) {
-        const bf16* ap = (const bf16*)p.aux + (int64_t)i * p.ld_aux + j;
-        if (vec && (p.ld_aux % CW) == 0) {
-          const bf16x8 a8 = *(const bf16x8*)ap;
-#pragma unroll
-          for (int e = 0; e < CW; ++e) xa[e] = (float)a8[e % 8];
-        } else {
-#pragma unroll
-          for (int e = 0; e < CW; ++e) xa[e] = j + e < p.N ? (float)ap[e] : 0.f;
-        }
-      } else if (EM == EM_F32 && use_beta) {
-        const float* cp = (const float*)C + (int64_t)i * ldc + j;
-        if (vec) {
-          const f32x4 o = *(const f32x4*)cp;
-#pragma unroll
-          for (int e = 0; e < CW; ++e) xb[e] = o[e % 4];
-        } else {
-#pragma unroll
-          for (int e = 0; e < CW; ++e) xb[e] = j + e < p.N ? cp[e] : 0.f;
-        }
-      }
-    };
-#pragma unroll
-    for (int e = 0; e < CW; ++e) in_a[e] = in_b[e] = 0.f;
-    prefetch(ib, in_a, in_b);
-#pragma unroll 2
     for (int it = 0; it < NIT; ++it) {
+      const int i = ib + it * RPI;
+      const bool ok = i < p.M && colok;
+      if (EM == EM_ROPE) {
+        f32x4 cs = {1.f, 1.f, 1.f, 1.f}, sn = {0.f, 0.f, 0.f, 0.f};
+        if (ok && rope_col) {
+          const int t = i % p.rope_T;
+          if (rope_vec) {
+            const int pr = (j % p.rope_dim) >> 1;
+            cs = *(const f32x4*)(p.rope_cos + t * rhalf + pr);
+            sn = *(const f32x4*)(p.rope_sin + t * rhalf + pr);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int pr = ((j + 2 * e) % p.rope_dim) >> 1;
+              cs[e] = p.rope_cos[t * rhalf + pr];
+              sn[e] = p.rope_sin[t * rhalf + pr];
+            }
+          }
+        }
+        inf[2 * it] = cs;
+        inf[2 * it + 1] = sn;
+      } else if (EM == EM_DRELU) {
+        bf16x8 a8 = {};
+        if (ok) {
+          const bf16* ap = (const bf16*)p.aux + (int64_t)i * p.ld_aux + j;
+          if (vec && (p.ld_aux % CW) == 0) {
+            a8 = *(const bf16x8*)ap;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a8[e] = j + e < p.N ? ap[e] : (bf16)0.f;
+          }
+        }
+        ind[it % ND] = a8;
+      } else if (EM == EM_F32) {
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
+        if (ok && use_beta) {
+          const float* cp = (const float*)C + (int64_t)i * ldc + j;
+          if (vec) {
+            o = *(const f32x4*)cp;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = j + e < p.N ? cp[e] : 0.f;
+          }
+        }
+        inf[it % NF] = o;
+      }
+    }
+    stage_half(acc, half, p.alpha, lane, scr);
+    auto body = [&](int it) {
       const int i = ib + it * RPI;
       const char* src = scr + (it * RPI + r0) * RING_EPI_RB + c * 4;
       float v[CW];
@@ -611,10 +633,6 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
           for (int e = 0; e < 4; ++e) v[(4 + e) % CW] = v1[e];
         }
       }
-      float na[CW], nb[CW];
-#pragma unroll
-      for (int e = 0; e < CW; ++e) na[e] = nb[e] = 0.f;
-      if (it + 1 < NIT) prefetch(i + RPI, na, nb);
       if (i < p.M && colok) {
 #pragma unroll
         for (int e = 0; e < CW; ++e) v[e] += bias[e];
@@ -633,20 +651,23 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
           }
         } else if (EM == EM_ROPE) {
           if (rope_col) {
+            const f32x4 cs = inf[(2 * it) % NF], sn = inf[(2 * it + 1) % NF];
 #pragma unroll
             for (int e = 0; e < CW; e += 2) {
-              const float x0 = v[e], x1 = v[e + 1], cs = in_a[e], sn = in_a[e + 1];
-              v[e] = x0 * cs - x1 * sn;
-              v[e + 1] = x0 * sn + x1 * cs;
+              const float x0 = v[e], x1 = v[e + 1];
+              v[e] = x0 * cs[(e / 2) % 4] - x1 * sn[(e / 2) % 4];
+              v[e + 1] = x0 * sn[(e / 2) % 4] + x1 * cs[(e / 2) % 4];
             }
           }
         } else if (EM == EM_DRELU) {
+          const bf16x8 a8 = ind[it % ND];
 #pragma unroll
-          for (int e = 0; e < CW; ++e) v[e] = in_a[e] > 0.f ? v[e] * p.inv_keep : 0.f;
+          for (int e = 0; e < CW; ++e) v[e] = (float)a8[e % 8] > 0.f ? v[e] * p.inv_keep : 0.f;
         } else if (EM == EM_F32) {
           if (use_beta) {
+            const f32x4 o = inf[it % NF];
 #pragma unroll
-            for (int e = 0; e < CW; ++e) v[e] += p.beta * in_b[e];
+            for (int e = 0; e < CW; ++e) v[e] += p.beta * o[e % 4];
           }
         }
         char* dst = C + ((int64_t)i * ldc + j) * ESZ;
@@ -665,11 +686,15 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
             }
         }
       }
+    };
+    // input registers are indexed by iteration: unroll fully; the others keep
+    // the loop short (a full unroll of the dropout hash costs I-cache)
+    if constexpr (ND > 1 || NF > 1) {
 #pragma unroll
-      for (int e = 0; e < CW; ++e) {
-        in_a[e] = na[e];
-        in_b[e] = nb[e];
-      }
+      for (int it = 0; it < NIT; ++it) body(it);
+    } else {
+#pragma unroll 2
+      for (int it = 0; it < NIT; ++it) body(it);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
@@ -954,7 +979,8 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
 
   // the 256x256 LDS-DMA kernel: bf16, K a multiple of its 64-deep K tile, and at
   // least 32 of its tiles (measured on the 228M step's shapes, tools/bench_gemm.py;
-  // smaller/odd problems take the 128 kernel)
+  // smaller/odd problems take the 128 kernel.  A 1024^2 dW split 16 ways on the
+  // 256 kernel ties the 128 kernel split 8 ways: 60 vs 61 us, tools/bench_gemm_epi.py)
   const int64_t big_tiles = (int64_t)((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
   const bool big = a->dtype == NSTL_BF16 && a->K % 64 == 0 && a->M >= BIG && a->N >= BIG && big_tiles >= 32 &&
                    !getenv_small_gemm();
