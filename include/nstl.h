@@ -108,7 +108,8 @@ typedef struct nstl_ln_args {
   const float* dout;       /* f32 [rows][D] */
   float* ds;               /* f32 [rows][D] (may alias dout) */
   void* dbranch;           /* dtype: ds * masks / (1-p)^n_masks, may be NULL */
-  float* dgamma_part; float* dbeta_part; int n_part;   /* [n_part][D] */
+  float* dgamma_part; float* dbeta_part; int n_part;   /* [n_part][D]; n_part <= rows/8
+                                                          (rows/4 when D % 256 != 0) */
   float* dbranch_part;     /* optional [n_part][D]: column sums of dbranch (the bias
                               gradient of the Linear that produced y) */
 } nstl_ln_args;

@@ -4,7 +4,9 @@
 //             (+ optional global-PE rotation of `out`, model.py:246)
 //   backward: ds = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat));
 //             dbranch = ds * masks / (1-p)^n ; per-block dgamma/dbeta partials.
-// One wave per row; each lane owns VPL = D/64 contiguous columns (vector I/O).
+// One wave per row; each lane owns VPL = D/64 columns: contiguous (D = 128), or
+// when D % 256 == 0 four-column groups 256 apart (every wave instruction then
+// covers one contiguous span).
 #include <algorithm>
 
 #include "../../include/nstl.h"
@@ -208,11 +210,234 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(LnParams p) {
   }
 }
 
+// Backward for D % 256 == 0 (the step's D = 1024): 8 waves per block, lane l
+// owns columns k*256 + 4l .. +3 (k < D/256), so every load/store instruction of
+// a wave covers one contiguous 512 B (bf16) / 1 KB (f32) span, and the next
+// row's inputs are loaded before the current row is reduced (two rows in flight
+// per wave: ~100 KB per CU, what HBM latency needs).
+constexpr int NTB = 512;
+
+template <typename T>
+NSTL_DEV void load4(const T* p, float (&v)[4]) {
+  if constexpr (sizeof(T) == 2) {
+    const uint2 u = *(const uint2*)p;
+    const T* e = (const T*)&u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = to_f32(e[j]);
+  } else {
+    const float4 u = *(const float4*)p;
+    v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+  }
+}
+template <typename T>
+NSTL_DEV void store4(T* p, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    uint2 u;
+    T* e = (T*)&u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = from_f32<T>(v[j]);
+    *(uint2*)p = u;
+  } else {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+template <typename T, int VPL>
+__global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
+  constexpr int NK = VPL / 4;  // 4-column groups per lane
+  constexpr int NWB = NTB / 64;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float gam[VPL], dg[VPL], db[VPL], dyb[VPL];
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      gam[4 * k + e] = p.gamma[k * 256 + 4 * lane + e];
+      dg[4 * k + e] = db[4 * k + e] = dyb[4 * k + e] = 0.f;
+    }
+  const int stride = gridDim.x * NWB;
+  int row = blockIdx.x * NWB + w;
+  float xh[VPL], gy[VPL], mean = 0.f, rstd = 0.f;
+  auto load = [&](int r, float (&x)[VPL], float (&g)[VPL], float& mu, float& rs) {
+    const int64_t base = (int64_t)r * p.D + 4 * lane;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      float t4[4], g4[4];
+      load4<T>((const T*)p.s_in + base + k * 256, t4);
+      load4<float>(p.dout + base + k * 256, g4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[4 * k + e] = t4[e];
+        g[4 * k + e] = g4[e];
+      }
+    }
+    mu = p.mean[r];
+    rs = p.rstd[r];
+  };
+  if (row < p.rows) load(row, xh, gy, mean, rstd);
+  for (; row < p.rows; row += stride) {
+    const int nxt = row + stride;
+    float xn[VPL], gn[VPL], mn = 0.f, rn = 0.f;
+    if (nxt < p.rows) load(nxt, xn, gn, mn, rn);
+    const int64_t base = (int64_t)row * p.D + 4 * lane;
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      xh[j] = (xh[j] - mean) * rstd;
+      dg[j] += gy[j] * xh[j];
+      db[j] += gy[j];
+      const float gg = gy[j] * gam[j];
+      a1 += gg;
+      a2 += gg * xh[j];
+    }
+    const float m1 = wave_sum(a1) / p.D, m2 = wave_sum(a2) / p.D;
+    float d[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) d[j] = rstd * (gy[j] * gam[j] - m1 - xh[j] * m2);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) store4<float>(p.ds + base + k * 256, d + 4 * k);
+    if (p.dbranch) {
+      if (p.thresh && p.n_masks > 0) {
+#pragma unroll
+        for (int k = 0; k < NK; ++k)
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            float s0, s1;
+            branch_scale2(p, (uint64_t)base + k * 256 + e, s0, s1);
+            d[4 * k + e] *= s0;
+            d[4 * k + e + 1] *= s1;
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) d[j] = to_f32(from_f32<T>(d[j]));  // sum what is stored
+#pragma unroll
+      for (int k = 0; k < NK; ++k) store4<T>((T*)p.dbranch + base + k * 256, d + 4 * k);
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) dyb[j] += d[j];
+    }
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      xh[j] = xn[j];
+      gy[j] = gn[j];
+    }
+    mean = mn;
+    rstd = rn;
+  }
+  // per-block partials: reduce the waves through LDS, column order
+  __shared__ float red[3][NWB][1024];
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = k * 256 + 4 * lane + e;
+      red[0][w][c] = dg[4 * k + e];
+      red[1][w][c] = db[4 * k + e];
+      red[2][w][c] = dyb[4 * k + e];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < p.D; c += NTB) {
+    float a = 0.f, b = 0.f, y = 0.f;
+#pragma unroll
+    for (int k = 0; k < NWB; ++k) {
+      a += red[0][k][c];
+      b += red[1][k][c];
+      y += red[2][k][c];
+    }
+    p.dgp[(int64_t)blockIdx.x * p.D + c] = a;
+    p.dbp[(int64_t)blockIdx.x * p.D + c] = b;
+    if (p.dyp) p.dyp[(int64_t)blockIdx.x * p.D + c] = y;
+  }
+}
+
+// Forward with the interleaved column map of ln_bwd_kernel_il (D % 256 == 0):
+// lane l owns columns k*256 + 4l .. +3, one row per wave.
+template <typename T, int VPL>
+__global__ __launch_bounds__(NT) void ln_fwd_kernel_il(LnParams p) {
+  constexpr int NK = VPL / 4;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (row >= p.rows) return;
+  const int64_t base = (int64_t)row * p.D + 4 * lane;
+  float s[VPL], xv[VPL];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    float y4[4], x4[4] = {0.f, 0.f, 0.f, 0.f};
+    load4<T>((const T*)p.y + base + k * 256, y4);
+    if (p.x) load4<T>((const T*)p.x + base + k * 256, x4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s[4 * k + e] = y4[e];
+      xv[4 * k + e] = x4[e];
+    }
+  }
+  if (p.thresh && p.n_masks > 0) {
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        float m0, m1;
+        branch_scale2(p, (uint64_t)base + k * 256 + e, m0, m1);
+        s[4 * k + e] *= m0;
+        s[4 * k + e + 1] *= m1;
+      }
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    s[j] += xv[j];
+    sum += s[j];
+  }
+  const float mean = wave_sum(sum) / p.D;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const float d = s[j] - mean;
+    sq += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / p.D + p.eps);
+  float o[VPL];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    if (p.s_out) store4<T>((T*)p.s_out + base + k * 256, s + 4 * k);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = k * 256 + 4 * lane + e;
+      // round to the storage type first so `rot_out` rotates exactly what `out` holds
+      o[4 * k + e] = to_f32(from_f32<T>((s[4 * k + e] - mean) * rstd * p.gamma[c] + p.beta[c]));
+    }
+    store4<T>((T*)p.out + base + k * 256, o + 4 * k);
+  }
+  if (lane == 0) {
+    p.mean[row] = mean;
+    p.rstd[row] = rstd;
+  }
+  if (p.rot_out) {
+    const int t = row % p.rope_T, half = p.D >> 1;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      float r[4];
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const int pr = (k * 256 + 4 * lane + e) >> 1;
+        const float c = p.rope_cos[t * half + pr], sn = p.rope_sin[t * half + pr];
+        r[e] = o[4 * k + e] * c - o[4 * k + e + 1] * sn;
+        r[e + 1] = o[4 * k + e] * sn + o[4 * k + e + 1] * c;
+      }
+      store4<T>((T*)p.rot_out + base + k * 256, r);
+    }
+  }
+}
+
 template <typename T, bool BWD>
 int dispatch(const LnParams& p, int grid, hipStream_t st) {
 #define NSTL_LN_CASE(V)                                                                     \
   case V:                                                                                   \
-    if (BWD) hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(grid), dim3(NT), 0, st, p);    \
+    if (BWD && V % 4 == 0)                                                                  \
+      hipLaunchKernelGGL((ln_bwd_kernel_il<T, (V % 4 == 0 ? V : 4)>), dim3(grid), dim3(NTB), 0, st, p); \
+    else if (BWD) hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(grid), dim3(NT), 0, st, p); \
+    else if (V % 4 == 0)                                                                    \
+      hipLaunchKernelGGL((ln_fwd_kernel_il<T, (V % 4 == 0 ? V : 4)>), dim3(grid), dim3(NT), 0, st, p); \
     else hipLaunchKernelGGL((ln_fwd_kernel<T, V>), dim3(grid), dim3(NT), 0, st, p);        \
     break;
   switch (p.D / 64) {
@@ -267,8 +492,10 @@ extern "C" int nstl_ln_bwd(const nstl_ln_args* a, void* stream) {
   if (rc) return rc;
   NSTL_CHECK_ARG(a->s_in && a->dout && a->ds && a->mean && a->rstd, "nstl_ln_bwd: null tensor");
   NSTL_CHECK_ARG(a->dgamma_part && a->dbeta_part && a->n_part > 0, "nstl_ln_bwd: partials");
-  const int grid = std::min(a->n_part, (a->rows + NT / 64 - 1) / (NT / 64));
-  NSTL_CHECK_ARG(grid == a->n_part, "nstl_ln_bwd: n_part (%d) must be <= rows/4", a->n_part);
+  // n_part blocks; each needs at least one row per wave (4 waves; 8 when D % 256 == 0)
+  const int nw = (a->D % 256 == 0) ? NTB / 64 : NT / 64;
+  const int grid = std::min(a->n_part, (a->rows + nw - 1) / nw);
+  NSTL_CHECK_ARG(grid == a->n_part, "nstl_ln_bwd: n_part (%d) must be <= rows/%d", a->n_part, nw);
   return a->dtype == NSTL_BF16 ? dispatch<bf16, true>(p, grid, (hipStream_t)stream)
                                : dispatch<float, true>(p, grid, (hipStream_t)stream);
 }

@@ -110,7 +110,7 @@ class _Buffers:
             self.demb = e(M, D)
             self.dpred = torch.zeros(M, 64, dtype=dt, device=dev)
             self.dsum = e(B * eng.H * T, dtype=f32)  # attention backward rowsum(dO * O)
-            self.n_part = max(1, min(256, M // 4))
+            self.n_part = max(1, min(256, M // 8))  # LN backward: >= 1 row per wave (8 waves)
             self.ln_part = e(3, self.n_part, D, dtype=f32)
             self.col_part = e((M + 255) // 256, max(Fd, 3 * D, 64), dtype=f32)
             self.ws = e(eng.splitk_ws_elems(M), dtype=f32)

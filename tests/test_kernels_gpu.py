@@ -314,6 +314,34 @@ def test_layernorm_fwd_bwd(dt, D):
     check(f64(bp).sum(0), bb.grad, 1e-5, "ln dbeta")
 
 
+@pytest.mark.parametrize("D", [128, 256, 512, 1024])
+@pytest.mark.parametrize("with_x", [True, False])
+def test_layernorm_fwd_global_pe(D, with_x):
+    """rot_out = GlobalPositionalEncoding(out) (model.py:29-48, :246) fused into
+    the final encoder LayerNorm; x = None is the plain LN of y."""
+    from neurosync_trainer_lite_amd.engine import rotation_tables
+    dt, T, rows = torch.float32, 50, 100
+    x, y = rnd(rows, D, seed=60), rnd(rows, D, seed=61)
+    g, b = 1 + 0.1 * rnd(D, seed=62), 0.1 * rnd(D, seed=63)
+    out = torch.empty(rows, D, device=DEV)
+    rot = torch.empty(rows, D, device=DEV)
+    stats = torch.empty(2, rows, device=DEV)
+    cs, sn = rotation_tables(T, D, DEV)
+    a = ln_args(dt, rows, D, x if with_x else None, y, g, b, None, out, stats)
+    a.rot_out, a.rope_cos, a.rope_sin, a.rope_T = rot.data_ptr(), cs.data_ptr(), sn.data_ptr(), T
+    K.ln_fwd(a)
+    torch.cuda.synchronize()
+    inp = f64(x) + f64(y) if with_x else f64(y)
+    ref = torch.nn.functional.layer_norm(inp, (D,), f64(g), f64(b), 1e-5)
+    check(out, ref, 2e-6, "ln out")
+    t = torch.arange(rows) % T
+    c, s_ = f64(cs)[t], f64(sn)[t]
+    e, o = ref[:, 0::2], ref[:, 1::2]
+    rr = torch.stack([e * c - o * s_, e * s_ + o * c], dim=-1).reshape(rows, D)
+    check(rot, rr, 2e-6, "ln rot_out")
+    check(stats[0], inp.mean(1), 1e-6, "ln mean")
+
+
 @pytest.mark.parametrize("n_masks", [1, 2])
 def test_layernorm_dropout_masks(n_masks):
     dt, rows, D, p = torch.float32, 64, 256, 0.3
@@ -339,6 +367,39 @@ def test_layernorm_dropout_masks(n_masks):
     K.ln_bwd(a)
     torch.cuda.synchronize()
     check(dbr, f64(ds) * m / (1 - p) ** n_masks, 1e-6, "dbranch masks")
+
+
+@pytest.mark.parametrize("rows,npart", [(37, 4), (1000, 125)])
+def test_layernorm_bwd_ragged_partials(rows, npart):
+    """Row counts that do not fill the last block's waves; the fused bias-gradient
+    partials (dbranch_part) against torch on the same masked dbranch."""
+    dt, D, p = torch.bfloat16, 1024, 0.3
+    x, y = rnd(rows, D, dtype=dt, seed=50), rnd(rows, D, dtype=dt, seed=51)
+    g, b = 1 + 0.1 * rnd(D, seed=52), 0.1 * rnd(D, seed=53)
+    s = torch.empty(rows, D, dtype=dt, device=DEV)
+    out = torch.empty(rows, D, dtype=dt, device=DEV)
+    stats = torch.empty(2, rows, device=DEV)
+    K.ln_fwd(ln_args(dt, rows, D, x, y, g, b, s, out, stats, 2, p, (5, 6)))
+    dout = rnd(rows, D, seed=54)
+    ds = torch.empty(rows, D, device=DEV)
+    dbr = torch.empty(rows, D, dtype=dt, device=DEV)
+    part = torch.empty(3, npart, D, device=DEV)
+    a = ln_args(dt, rows, D, x, y, g, b, None, out, stats, 2, p, (5, 6))
+    a.s_in, a.dout, a.ds, a.dbranch = s.data_ptr(), dout.data_ptr(), ds.data_ptr(), dbr.data_ptr()
+    a.dgamma_part, a.dbeta_part, a.n_part = part[0].data_ptr(), part[1].data_ptr(), npart
+    a.dbranch_part = part[2].data_ptr()
+    K.ln_bwd(a)
+    torch.cuda.synchronize()
+    ss = f64(s).requires_grad_(True)
+    gg, bb = f64(g).requires_grad_(True), f64(b).requires_grad_(True)
+    torch.nn.functional.layer_norm(ss, (D,), gg, bb, 1e-5).backward(f64(dout))
+    check(ds, ss.grad, 1e-2, "ln ds")
+    # the same masks as the forward: dbranch / ds is 0 or 1/(1-p)^2
+    ratio = f64(dbr)[f64(ds).abs() > 1e-3] / f64(ds)[f64(ds).abs() > 1e-3]
+    assert ((ratio.abs() < 1e-6) | ((ratio - 1 / 0.49).abs() < 0.02)).all()
+    check(f64(part[0]).sum(0), gg.grad, 2e-3, "ln dgamma")
+    check(f64(part[1]).sum(0), bb.grad, 1e-5, "ln dbeta")
+    check(f64(part[2]).sum(0), f64(dbr).sum(0), 1e-5, "ln dbranch colsum")
 
 
 # ---------------------------------------------------------------------------

