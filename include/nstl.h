@@ -85,6 +85,10 @@ typedef struct nstl_attn_args {
   const float* rope_cos; const float* rope_sin;  /* [T][dh/2]; non-null: dq,dk rotated back */
   int rope_q, rope_k;
   float* dsum;                /* backward scratch [B*H*T] f32: rowsum(dO * O) */
+  uint64_t* mask_bits;        /* optional [B*H*T*T/64]: the dropout keep bits.  Forward
+                                 writes them, backward reads them instead of re-hashing
+                                 (MFMA path: head_dim 64; ignored elsewhere).  NULL:
+                                 both directions hash (seed, element). */
 } nstl_attn_args;
 int nstl_attn_fwd(const nstl_attn_args* args, void* stream);
 int nstl_attn_bwd(const nstl_attn_args* args, void* stream);

@@ -49,7 +49,7 @@ class AttnArgs(ctypes.Structure):
         ("dout", _vp), ("dout_ld", _i64), ("dq", _vp), ("dq_ld", _i64), ("dk", _vp), ("dk_ld", _i64),
         ("dv", _vp), ("dv_ld", _i64),
         ("rope_cos", _vp), ("rope_sin", _vp), ("rope_q", _i32), ("rope_k", _i32),
-        ("dsum", _vp),
+        ("dsum", _vp), ("mask_bits", _vp),
     ]
 
 

@@ -35,6 +35,7 @@ struct AttnParams {
   char* o; int64_t o_ld;
   float* lse;
   float* dsum;
+  uint64_t* mask;  // dropout keep bits (fast path), see mask_word()
   const char* dout; int64_t dout_ld;
   char* dq; int64_t dq_ld;
   char* dk; int64_t dk_ld;
@@ -69,6 +70,24 @@ NSTL_DEV void store_elem(char* base, int64_t e, float v) {
 
 // dropout element index: key-major so that (q, q+1) form a hash pair
 NSTL_DEV uint64_t drop_idx(int bh, int T, int q, int k) { return ((uint64_t)bh * T + k) * T + q; }
+
+// Stored keep bits (MFMA path): one 64-bit word per (query tile qt, key tile kt,
+// query % 4) of a head, bit 16 * ((q % 16) / 4) + key % 16 -- exactly the
+// ballot of the keep decisions of one accumulator register r over a wave in
+// the forward / dQ layout (lane 16g + c: query 4g + r, key c).  A head's words
+// are [qt][kt][4] (T*T/64 of them).
+NSTL_DEV int64_t mask_word(int bh, int nt, int qt, int kt, int r) {
+  return (((int64_t)bh * nt + qt) * nt + kt) * 4 + r;
+}
+NSTL_DEV uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = __shfl((uint32_t)v, src), hi = __shfl((uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+NSTL_DEV uint64_t readlane64(uint64_t v, int src) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, src);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
 
 // four consecutive values of one lane as an 8-byte (bf16) / 16-byte (f32) LDS write
 NSTL_DEV void put4(char* dst, float a, float b, float c, float d, bf16) {
@@ -160,6 +179,7 @@ __global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
     // dropout + P^T (unnormalised) into this wave's image [T keys][16 rows]
     char* Pw = Pimg + w * max(T_, 64) * RBP;  // also holds the 16 x 64 O tile
     const int qrow = qb0 + q0 + 4 * g;  // this lane's first query (even)
+    uint32_t mlo = 0, mhi = 0;          // lane kt*4 + r: keep bits of (kt, r)
 #pragma unroll
     for (int kt = 0; kt < 16; ++kt) {
       if (kt < nkt) {
@@ -174,10 +194,21 @@ __global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
           v1 = k1 ? v1 * p.inv_keep : 0.f;
           v2 = k2 ? v2 * p.inv_keep : 0.f;
           v3 = k3 ? v3 * p.inv_keep : 0.f;
+          if (p.mask) {  // the 4 ballots (wave-uniform) into lanes kt*4 .. +3
+            const uint64_t b[4] = {__ballot(k0), __ballot(k1), __ballot(k2), __ballot(k3)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (lane == kt * 4 + r) {
+                mlo = (uint32_t)b[r];
+                mhi = (uint32_t)(b[r] >> 32);
+              }
+          }
         }
         put4(Pw + key * RBP + 4 * g * ESZ, v0, v1, v2, v3, T());
       }
     }
+    if (p.thresh && p.mask && lane < nkt * 4)
+      p.mask[mask_word(bh, nkt, (qb0 + q0) >> 4, 0, 0) + lane] = ((uint64_t)mhi << 32) | mlo;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     f32x4 o[4];
 #pragma unroll
@@ -326,6 +357,10 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
 
   const float c2 = p.scale * LOG2E;
   char* S2 = scratch + w * 2 * 32 * RBS;
+  // stored keep bits of this wave's 16 queries: lane kt*4 + r holds word (kt, r)
+  const bool use_mask = p.thresh && p.mask;
+  uint64_t mword = 0;
+  if (use_mask && lane < nkt * 4) mword = p.mask[mask_word(bh, nkt, q0 >> 4, 0, 0) + lane];
   f32x4 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -346,7 +381,10 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
       // accumulator: row = query (4g + r), col = key
       const int key = kt * 16 + (lane & 15);
       bool keep[4] = {true, true, true, true};
-      if (p.thresh) {
+      if (use_mask) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) keep[r] = (readlane64(mword, kt * 4 + r) >> lane) & 1;
+      } else if (p.thresh) {
         const uint64_t idx = drop_idx(bh, T_, q0 + 4 * g, key);
         nstl_keep2(p.seed, idx, p.thresh, keep[0], keep[1]);
         nstl_keep2(p.seed, idx + 2, p.thresh, keep[2], keep[3]);
@@ -433,6 +471,10 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
 
   const float c2 = p.scale * LOG2E;
   char* S1 = scratch + w * 2 * 32 * RBS;  // [32 rows][16] images
+  // stored keep bits for this wave's 16 keys: lane 4*qt + r holds word (qt, k0/16, r)
+  const bool use_mask = p.thresh && p.mask;
+  uint64_t mword = 0;
+  if (use_mask && (lane >> 2) < nkt) mword = p.mask[mask_word(bh, nkt, lane >> 2, k0 >> 4, lane & 3)];
   char* S2 = S1 + 32 * RBS;
   f32x4 dk[4], dv[4];
 #pragma unroll
@@ -454,6 +496,9 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
       // accumulator: row = key (4g + r), col = query
       const int q = qt * 16 + (lane & 15);
       const float lq = lse_s[q], dqv = dq_s[q];
+      // query q's bits for keys k0 + 4g .. +3: 4 consecutive bits of word (qt, q % 4)
+      uint32_t nib = 0;
+      if (use_mask) nib = (uint32_t)(shfl64(mword, 4 * qt + (lane & 3)) >> (16 * ((lane & 15) >> 2) + 4 * g));
       float pd[4], ds[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -461,7 +506,7 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
         const float pv = exp2f(st[r] * c2 - lq);
         float pdr = pv, dpd = dpt[r];
         if (p.thresh) {
-          const bool keep = nstl_keep(p.seed, drop_idx(bh, T_, q, key), p.thresh);
+          const bool keep = use_mask ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, key), p.thresh);
           pdr = keep ? pv * p.inv_keep : 0.f;
           dpd = keep ? dpd * p.inv_keep : 0.f;
         }
@@ -760,6 +805,7 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   p.o = (char*)a->o; p.o_ld = a->o_ld;
   p.lse = a->lse;
   p.dsum = a->dsum;
+  p.mask = a->mask_bits;
   p.dout = (const char*)a->dout; p.dout_ld = a->dout_ld;
   p.dq = (char*)a->dq; p.dq_ld = a->dq_ld;
   p.dk = (char*)a->dk; p.dk_ld = a->dk_ld;

@@ -110,6 +110,11 @@ class _Buffers:
             self.demb = e(M, D)
             self.dpred = torch.zeros(M, 64, dtype=dt, device=dev)
             self.dsum = e(B * eng.H * T, dtype=f32)  # attention backward rowsum(dO * O)
+            # attention dropout keep bits, written by the forward, read by the backward
+            nw = max(1, B * eng.H * T * T // 64)
+            self.e_mask = [e(nw, dtype=torch.int64) for _ in range(L)]
+            self.d_mask = [e(nw, dtype=torch.int64) for _ in range(L)]
+            self.d_maskc = [e(nw, dtype=torch.int64) for _ in range(L)]
             self.n_part = max(1, min(256, M // 8))  # LN backward: >= 1 row per wave (8 waves)
             self.ln_part = e(3, self.n_part, D, dtype=f32)
             self.col_part = e((M + 255) // 256, max(Fd, 3 * D, 64), dtype=f32)
@@ -416,13 +421,14 @@ class Seq2SeqEngine:
             outs.append(self.gb(bias_of))
         K.reduce_rows3(bb.ln_part, bb.n_part, self.D, outs, bf, stream=self.st)
 
-    def _attn(self, q, k, v, o, lse, seed, T, B):
+    def _attn(self, q, k, v, o, lse, seed, T, B, mask=None):
         a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
                         v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed,
                         dh=self.dh)
+        a.mask_bits = K.ptr(mask)
         K.attn_fwd(a, stream=self.st)
 
-    def _attn_bwd(self, q, k, v, o, lse, do, dq, dk, dv, seed, T, B):
+    def _attn_bwd(self, q, k, v, o, lse, do, dq, dk, dv, seed, T, B, mask=None):
         a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
                         v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed,
                         dh=self.dh)
@@ -432,6 +438,7 @@ class Seq2SeqEngine:
         cs, sn = self.rope(T, self.dh)
         a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
         a.dsum = self.cur.dsum.data_ptr()
+        a.mask_bits = K.ptr(mask)
         self._guard(dq, dk, dv)
         K.attn_bwd(a, stream=self.st)
 
@@ -443,7 +450,8 @@ class Seq2SeqEngine:
         qkv, o, lse = bb.layer(bb.e_qkv, l), bb.layer(bb.e_o, l), bb.layer(bb.e_lse, l)
         self._gemm_fwd(x, pre + "self_attn.q_linear.weight", qkv, K.EPI_BIAS_ROPE, rows=3,
                        rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=2 * D)
-        self._attn(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, sd("attn"), T, B)
+        self._attn(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, sd("attn"), T, B,
+                   mask=bb.e_mask[l] if bb.save else None)
         self._gemm_fwd(o, pre + "self_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         st = bb.layer(bb.e_stats, l)
         x1 = bb.layer(bb.e_x1, l)
@@ -464,7 +472,8 @@ class Seq2SeqEngine:
         qkv = L_(bb.d_qkv)
         self._gemm_fwd(x, pre + "self_attn.q_linear.weight", qkv, K.EPI_BIAS_ROPE, rows=3,
                        rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=2 * D)
-        self._attn(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], L_(bb.d_o), L_(bb.d_lse), sd("attn"), T, B)
+        self._attn(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], L_(bb.d_o), L_(bb.d_lse), sd("attn"), T, B,
+                   mask=bb.d_mask[l] if bb.save else None)
         self._gemm_fwd(L_(bb.d_o), pre + "self_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         x1 = L_(bb.d_x1)
         self._ln(x, bb.y, x1, st[0:2], pre + "norm1", 2, (sd("resid"), sd("drop1")), L_(bb.d_s1))
@@ -473,7 +482,8 @@ class Seq2SeqEngine:
                        rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D)
         self._gemm_fwd(mem, pre + "multihead_attn.k_linear.weight", kvc, K.EPI_BIAS_ROPE, rows=2,
                        rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D)
-        self._attn(qc, kvc[:, :D], kvc[:, D:], L_(bb.d_oc), L_(bb.d_lsec), sd("xattn"), T, B)
+        self._attn(qc, kvc[:, :D], kvc[:, D:], L_(bb.d_oc), L_(bb.d_lsec), sd("xattn"), T, B,
+                   mask=bb.d_maskc[l] if bb.save else None)
         self._gemm_fwd(L_(bb.d_oc), pre + "multihead_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         x2 = L_(bb.d_x2)
         self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 2, (sd("xresid"), sd("drop2x")), L_(bb.d_s2))
@@ -600,7 +610,7 @@ class Seq2SeqEngine:
         with torch.cuda.stream(self._side):
             red.ready(upto)
 
-    def _attn_block_bwd(self, bb, pre, x_in, qkv, o, lse, st, s1, norm, seeds, T, bf):
+    def _attn_block_bwd(self, bb, pre, x_in, qkv, o, lse, st, s1, norm, seeds, T, bf, mask):
         """Backward through x1 = LN(x_in + drop(drop(out_linear(attn(x_in))))) (self-attention)."""
         D, ws = self.D, bb.ws
         self._ln_bwd(s1, st, pre + norm, bb.dres, bb.dres, bb.dy, 2, seeds[0:2], bf,
@@ -608,7 +618,7 @@ class Seq2SeqEngine:
         self._dw(bb.dy, o, pre + "self_attn.out_linear.weight", 1, bf, ws, bias=False)
         self._dx(bb.dy, pre + "self_attn.out_linear.weight", 1, bb.dattn, 0.0)
         self._attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, bb.dattn,
-                       bb.dqkv[:, :D], bb.dqkv[:, D:2 * D], bb.dqkv[:, 2 * D:], seeds[2], T, bb.B)
+                       bb.dqkv[:, :D], bb.dqkv[:, D:2 * D], bb.dqkv[:, 2 * D:], seeds[2], T, bb.B, mask=mask)
         self._dw(bb.dqkv, x_in, pre + "self_attn.q_linear.weight", 3, bf, ws)
         self._dx(bb.dqkv, pre + "self_attn.q_linear.weight", 3, bb.dres, 1.0)
 
@@ -629,7 +639,7 @@ class Seq2SeqEngine:
         x_in = bb.x0 if l == 0 else bb.e_x2[l - 1]
         self._ffn_bwd(bb, pre, bb.e_x1[l], bb.e_h[l], bb.e_s2[l], st[2:4], "norm2", sd("drop2"), bf)
         self._attn_block_bwd(bb, pre, x_in, bb.e_qkv[l], bb.e_o[l], bb.e_lse[l], st[0:2], bb.e_s1[l], "norm1",
-                             (sd("resid"), sd("drop1"), sd("attn")), T, bf)
+                             (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.e_mask[l])
 
     def _dec_layer_bwd(self, bb, l, T, bf, first):
         D, ws = self.D, bb.ws
@@ -646,13 +656,13 @@ class Seq2SeqEngine:
         self._dx(bb.dy, m + "out_linear.weight", 1, bb.dattn, 0.0)
         kvc = bb.d_kvc[l]
         self._attn_bwd(bb.d_qc[l], kvc[:, :D], kvc[:, D:], bb.d_oc[l], bb.d_lsec[l], bb.dattn,
-                       bb.dq, bb.dkv[:, :D], bb.dkv[:, D:], sd("xattn"), T, bb.B)
+                       bb.dq, bb.dkv[:, :D], bb.dkv[:, D:], sd("xattn"), T, bb.B, mask=bb.d_maskc[l])
         self._dw(bb.dq, bb.d_x1[l], m + "q_linear.weight", 1, bf, ws)
         self._dx(bb.dq, m + "q_linear.weight", 1, bb.dres, 1.0)
         self._dw(bb.dkv, bb.mem, m + "k_linear.weight", 2, bf, ws)
         self._dx(bb.dkv, m + "k_linear.weight", 2, bb.dmem, 0.0 if first else 1.0)
         self._attn_block_bwd(bb, pre, x_in, bb.d_qkv[l], bb.d_o[l], bb.d_lse[l], st[0:2], bb.d_s1[l], "norm1",
-                             (sd("resid"), sd("drop1"), sd("attn")), T, bf)
+                             (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.d_mask[l])
 
 
 class Seq2SeqFunction(torch.autograd.Function):

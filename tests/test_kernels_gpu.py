@@ -251,6 +251,44 @@ def test_attention_dropout_consistency(dt, T):
     check(dv, vv.grad.transpose(1, 2).reshape(M, D), tolb, "dv (dropout)")
 
 
+@pytest.mark.parametrize("dt,T", [(torch.bfloat16, 64), (torch.bfloat16, 128), (torch.bfloat16, 256),
+                                  (torch.float32, 128)])
+def test_attention_stored_mask_bits(dt, T):
+    """The forward's stored keep bits (nstl_attn_args.mask_bits) drive the backward
+    to the same bits as re-hashing (seed, element): identical outputs, keep rate 1-p."""
+    B, H, dh, p = 2, 3, 64, 0.3
+    M, D = B * T, H * dh
+    qkv = rnd(M, 3 * D, dtype=dt, scale=0.5, seed=70)
+    do = rnd(M, D, dtype=dt, seed=71)
+    cs, sn = rotation_tables(T, dh, DEV)
+    code = K.dtype_code(dt)
+    outs = []
+    for stored in (False, True):
+        o = torch.empty(M, D, dtype=dt, device=DEV)
+        lse = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
+        dqkv = torch.zeros(M, 3 * D, dtype=dt, device=DEV)
+        dsum = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
+        mask = torch.full((B * H * T * T // 64,), -1, dtype=torch.int64, device=DEV)
+        a = K.attn_args(code, B, T, H, qkv.data_ptr(), 3 * D, qkv[:, D:].data_ptr(), 3 * D,
+                        qkv[:, 2 * D:].data_ptr(), 3 * D, o.data_ptr(), D, lse.data_ptr(), p, 4242, dh=dh)
+        if stored:
+            a.mask_bits = mask.data_ptr()
+        K.attn_fwd(a)
+        a.dout, a.dout_ld = do.data_ptr(), D
+        a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dqkv.data_ptr(), 3 * D, dqkv[:, D:].data_ptr(), 3 * D,
+                                                        dqkv[:, 2 * D:].data_ptr(), 3 * D)
+        a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
+        a.dsum = dsum.data_ptr()
+        K.attn_bwd(a)
+        torch.cuda.synchronize()
+        outs.append((o.clone(), dqkv.clone(), mask.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    bits = outs[1][2].cpu().numpy().view(np.uint8)
+    frac = np.unpackbits(bits).mean()
+    assert abs(frac - (1 - p)) < 0.01, frac
+
+
 def test_attention_rejects_bad_shapes():
     t = torch.zeros(64, 3 * 64, device=DEV)
     lse = torch.zeros(64, device=DEV)

@@ -38,7 +38,7 @@ dsum = torch.empty(B * H * T, device=dev)
 cs, sn = rotation_tables(T, DH, dev)
 extra = {}
 mask = None
-if hasattr(K.AttnArgs, "mask_bits") and os.environ.get("NSTL_ATTN_MASK", "1") == "1":
+if os.environ.get("NSTL_ATTN_MASK", "1") == "1":   # stored keep bits (0: re-hash in backward)
     mask = torch.empty(B * H * T * T // 8, dtype=torch.uint8, device=dev)
 for p in (0.3, 0.0):
     def args():
