@@ -154,7 +154,23 @@ def main():
     # Timing events around every launch cost ~1.7 ms per step (228M), so they are
     # recorded in the last `--gemm-sample-steps` timed steps only.
     sample = [False]
+    real_grouped = K.gemm_grouped
+
+    def timed_grouped(problems, stream=None):
+        if not sample[0]:
+            real_grouped(problems, stream=stream)
+            return
+        st = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        real_grouped(problems, stream=stream)
+        e1.record(st)
+        fl = sum(2.0 * M * N * Kd for _, _, _, M, N, Kd, _ in problems)
+        by = sum((M * Kd + N * Kd) * A.element_size() + M * N * C.element_size() for A, _, C, M, N, Kd, _ in problems)
+        gemm_events.append((e0, e1, fl, by))
+
     K.gemm = timed_gemm
+    K.gemm_grouped = timed_grouped
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -167,6 +183,7 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     K.gemm = real_gemm
+    K.gemm_grouped = real_grouped
     if world > 1:
         tt = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
@@ -253,7 +270,7 @@ def main():
             "config": {"workload": "228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam)",
                        "model": "NeuroSync Seq2Seq 228M", "global_batch": B * world, "seq_len": T,
                        "frames_per_step": B * T * world, "parallelism": "dp%d" % world},
-            "roofline": {"bound": "mfma", "kernel": "nstl GEMM family (gemm256r_kernel + gemm_kernel), every launch "
+            "roofline": {"bound": "mfma", "kernel": "nstl GEMM family (gemm256r_kernel, its grouped form, gemm_kernel), every launch "
                                                     "of the last %d timed steps" % n_sampled,
                          "achieved": round(achieved_tf, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": traffic,

@@ -62,6 +62,15 @@ typedef struct nstl_gemm_args {
   void* workspace; int64_t workspace_bytes;
 } nstl_gemm_args;
 int nstl_gemm(const nstl_gemm_args* args, void* stream);
+
+/* Up to NSTL_GEMM_GROUP_MAX independent problems in ONE launch (grouped GEMM):
+   each a bf16 problem for the 256x256 kernel (M, N >= 256, K % 64 == 0), no
+   epilogue, no split-K, all with the same a_kmajor / b_kmajor / c_dtype and
+   beta use (0 / nonzero); alpha, beta, pointers and shapes per problem.  The
+   weight gradients of one decoder layer (utils/model.py:193-216 Linears,
+   backward) are ~256 tiles: one full round with no split-K partials. */
+#define NSTL_GEMM_GROUP_MAX 8
+int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream);
 int64_t nstl_gemm_workspace_bytes(int M, int N, int split_k);
 
 /* Non-causal multi-head attention with per-head RoPE already applied to q,k

@@ -87,7 +87,7 @@ class AdamArgs(ctypes.Structure):
 
 # every symbol include/nstl.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "nstl_gemm", "nstl_gemm_workspace_bytes", "nstl_attn_fwd", "nstl_attn_bwd", "nstl_ln_fwd", "nstl_ln_bwd",
+    "nstl_gemm", "nstl_gemm_grouped", "nstl_gemm_workspace_bytes", "nstl_attn_fwd", "nstl_attn_bwd", "nstl_ln_fwd", "nstl_ln_bwd",
     "nstl_reduce_rows", "nstl_reduce_rows3", "nstl_colsum", "nstl_rope", "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step",
     "nstl_cast", "nstl_copy2d", "nstl_autocorr", "nstl_features", "nstl_features_workspace_bytes",
     "nstl_features_frames", "nstl_last_error_string", "nstl_version",
@@ -107,6 +107,7 @@ def lib():
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         P = ctypes.POINTER
         L.nstl_gemm.argtypes = [P(GemmArgs), _vp]
+        L.nstl_gemm_grouped.argtypes = [P(GemmArgs), _i32, _vp]
         L.nstl_gemm_workspace_bytes.argtypes = [_i32, _i32, _i32]
         L.nstl_gemm_workspace_bytes.restype = _i64
         L.nstl_attn_fwd.argtypes = [P(AttnArgs), _vp]
@@ -160,10 +161,28 @@ def dtype_code(dt):
 # ---------------------------------------------------------------------------
 # thin call wrappers
 # ---------------------------------------------------------------------------
-def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None,
-         alpha=1.0, beta=0.0, epilogue=EPI_NONE, bias=None, aux=None, ld_aux=0, p_drop=0.0, seed=0,
-         rope=None, rope_cols=0, split_k=1, workspace=None, stream=None):
+def gemm(A, B, C, M, N, K, *, stream=None, **kw):
     """C[i,j] = alpha sum_r A(i,r) B(j,r) (+beta C) + epilogue.  See include/nstl.h."""
+    a = gemm_args(A, B, C, M, N, K, **kw)
+    check(lib().nstl_gemm(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_gemm")
+
+
+GEMM_GROUP_MAX = 8
+
+
+def gemm_grouped(problems, stream=None):
+    """Independent GEMMs in one launch (nstl_gemm_grouped): `problems` is a list of
+    (A, B, C, M, N, K, kwargs) with the gemm() keyword arguments."""
+    arr = (GemmArgs * len(problems))()
+    for i, (A, B, C, M, N, K, kw) in enumerate(problems):
+        arr[i] = gemm_args(A, B, C, M, N, K, **kw)
+    check(lib().nstl_gemm_grouped(arr, len(problems), stream if stream is not None else stream_of()),
+          "nstl_gemm_grouped")
+
+
+def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None,
+              alpha=1.0, beta=0.0, epilogue=EPI_NONE, bias=None, aux=None, ld_aux=0, p_drop=0.0, seed=0,
+              rope=None, rope_cols=0, split_k=1, workspace=None):
     a = GemmArgs()
     a.dtype = dtype_code(A.dtype)
     a.c_dtype = dtype_code(C.dtype)
@@ -188,7 +207,7 @@ def gemm(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, 
     if workspace is not None:
         a.workspace = workspace.data_ptr()
         a.workspace_bytes = workspace.numel() * workspace.element_size()
-    check(lib().nstl_gemm(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_gemm")
+    return a
 
 
 def attn_args(dtype, B, T, H, q, q_ld, k, k_ld, v, v_ld, o, o_ld, lse, p_drop, seed, dh=64):

@@ -542,8 +542,12 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
   constexpr int RPI = 64 / LPR;  // rows per wave instruction (8 / 4)
   constexpr int NIT = 64 / RPI;  // iterations per 64-row pass
   // per-iteration input registers, all issued before a pass starts
-  constexpr int ND = EM == EM_DRELU ? NIT : 1;                          // dReLU operand (bf16 x 8)
-  constexpr int NF = EM == EM_F32 ? NIT : (EM == EM_ROPE ? 2 * NIT : 1);  // old C / cos|sin (f32 x 4)
+  // old C (f32 out) in two sub-passes of NI iterations (64 VGPRs for a whole pass
+  // would push the kernel past 256); the other inputs one sub-pass per pass
+  constexpr int SUBS = EM == EM_F32 ? 2 : 1;
+  constexpr int NI = NIT / SUBS;
+  constexpr int ND = EM == EM_DRELU ? NI : 1;                         // dReLU operand (bf16 x 8)
+  constexpr int NF = EM == EM_F32 ? NI : (EM == EM_ROPE ? 2 * NI : 1);  // old C / cos|sin (f32 x 4)
   char* const C = EM == EM_WS ? (char*)(p.ws + (int64_t)blockIdx.y * p.M * p.N) : p.C;
   const int64_t ldc = EM == EM_WS ? p.N : p.ldc;
   const int c = (lane % LPR) * CW, j = col0 + c;
@@ -564,13 +568,16 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
   const int r0 = lane / LPR;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
-    const int ib = row0 + half * 64 + r0;
-    // Issue every input load of this pass first: one memory latency per pass
-    // instead of one per iteration (and no load queued behind the stores).
+   const int ib = row0 + half * 64 + r0;
+#pragma unroll
+   for (int sub = 0; sub < SUBS; ++sub) {
+    // Issue every input load of this (sub-)pass first: one memory latency per
+    // pass instead of one per iteration (and no load queued behind the stores).
     bf16x8 ind[ND];
     f32x4 inf[NF];
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
+    for (int iu = 0; iu < NI; ++iu) {
+      const int it = sub * NI + iu;
       const int i = ib + it * RPI;
       const bool ok = i < p.M && colok;
       if (EM == EM_ROPE) {
@@ -590,8 +597,8 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
             }
           }
         }
-        inf[2 * it] = cs;
-        inf[2 * it + 1] = sn;
+        inf[2 * iu] = cs;
+        inf[2 * iu + 1] = sn;
       } else if (EM == EM_DRELU) {
         bf16x8 a8 = {};
         if (ok) {
@@ -603,7 +610,7 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
             for (int e = 0; e < 8; ++e) a8[e] = j + e < p.N ? ap[e] : (bf16)0.f;
           }
         }
-        ind[it % ND] = a8;
+        ind[iu % ND] = a8;
       } else if (EM == EM_F32) {
         f32x4 o = {0.f, 0.f, 0.f, 0.f};
         if (ok && use_beta) {
@@ -615,11 +622,12 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
             for (int e = 0; e < 4; ++e) o[e] = j + e < p.N ? cp[e] : 0.f;
           }
         }
-        inf[it % NF] = o;
+        inf[iu % NF] = o;
       }
     }
-    stage_half(acc, half, p.alpha, lane, scr);
-    auto body = [&](int it) {
+    if (sub == 0) stage_half(acc, half, p.alpha, lane, scr);
+    auto body = [&](int iu) {
+      const int it = sub * NI + iu;
       const int i = ib + it * RPI;
       const char* src = scr + (it * RPI + r0) * RING_EPI_RB + c * 4;
       float v[CW];
@@ -651,7 +659,7 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
           }
         } else if (EM == EM_ROPE) {
           if (rope_col) {
-            const f32x4 cs = inf[(2 * it) % NF], sn = inf[(2 * it + 1) % NF];
+            const f32x4 cs = inf[(2 * iu) % NF], sn = inf[(2 * iu + 1) % NF];
 #pragma unroll
             for (int e = 0; e < CW; e += 2) {
               const float x0 = v[e], x1 = v[e + 1];
@@ -660,12 +668,12 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
             }
           }
         } else if (EM == EM_DRELU) {
-          const bf16x8 a8 = ind[it % ND];
+          const bf16x8 a8 = ind[iu % ND];
 #pragma unroll
           for (int e = 0; e < CW; ++e) v[e] = (float)a8[e % 8] > 0.f ? v[e] * p.inv_keep : 0.f;
         } else if (EM == EM_F32) {
           if (use_beta) {
-            const f32x4 o = inf[it % NF];
+            const f32x4 o = inf[iu % NF];
 #pragma unroll
             for (int e = 0; e < CW; ++e) v[e] += p.beta * o[e % 4];
           }
@@ -691,11 +699,12 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
     // the loop short (a full unroll of the dropout hash costs I-cache)
     if constexpr (ND > 1 || NF > 1) {
 #pragma unroll
-      for (int it = 0; it < NIT; ++it) body(it);
+      for (int iu = 0; iu < NI; ++iu) body(iu);
     } else {
 #pragma unroll 2
-      for (int it = 0; it < NIT; ++it) body(it);
+      for (int iu = 0; iu < NI; ++iu) body(iu);
     }
+   }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 }
@@ -716,18 +725,19 @@ NSTL_DEV void ring_epi_generic(const GemmParams& p, const f32x4 (&acc)[8][4], in
   }
 }
 
+constexpr int R_SMEM = R_STAGES * R_SLOT;
+static_assert(8 * RING_EPI_WAVE <= R_SMEM, "epilogue scratch must fit in the ring");
+
+// One 256 x 256 output tile of p: `id` is the tile's linear index in p's grid
+// (already XCD-remapped by the caller), `kz` its split-K chunk.
 template <bool AK, bool BKM, int EM>
-__global__ __launch_bounds__(BIG_NT, 1) void gemm256r_kernel(GemmParams p) {
-  constexpr int SMEM = R_STAGES * R_SLOT;
-  static_assert(8 * RING_EPI_WAVE <= SMEM, "epilogue scratch must fit in the ring");
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int nt_m = (p.M + BIG - 1) / BIG, nt_n = (p.N + BIG - 1) / BIG;
-  // XCD-contiguous id ranges, then grouped order (GROUP_M row tiles per group,
-  // column-fastest inside): an XCD's 32 co-resident blocks cover ~4 x 8 tiles
-  const int id = xcd_remap(blockIdx.x, nt_m * nt_n);
+  const int nt_n = (p.N + BIG - 1) / BIG, nt_m = (p.M + BIG - 1) / BIG;
+  // grouped order (GROUP_M row tiles per group, column-fastest inside) over
+  // XCD-contiguous id ranges: an XCD's 32 co-resident blocks cover ~4 x 8 tiles
   constexpr int GROUP_M = 4;
   const int per_group = GROUP_M * nt_n;
   const int first_m = (id / per_group) * GROUP_M;
@@ -735,7 +745,7 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm256r_kernel(GemmParams p) {
   const int in_g = id % per_group;
   const int tm = first_m + in_g % gm, tn = in_g / gm;
   const int m0 = tm * BIG, n0 = tn * BIG;
-  const int kz0 = blockIdx.y * p.k_chunk;
+  const int kz0 = kz * p.k_chunk;
   const int kz1 = min(p.K, kz0 + p.k_chunk);
   const int nk = (kz1 - kz0) / R_BK;
   const uint32_t smem_u32 = lds_u32(smem);
@@ -807,6 +817,32 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm256r_kernel(GemmParams p) {
   const int row0 = m0 + wm * 128, col0 = n0 + wn * 64;
   if (EM == EM_GENERIC) ring_epi_generic(p, acc, row0, col0, lane, scr);
   else ring_epi<EM>(p, acc, row0, col0, lane, scr);
+}
+
+template <bool AK, bool BKM, int EM>
+__global__ __launch_bounds__(BIG_NT, 1) void gemm256r_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[R_SMEM];
+  const int nt = ((p.M + BIG - 1) / BIG) * ((p.N + BIG - 1) / BIG);
+  ring_tile<AK, BKM, EM>(p, xcd_remap(blockIdx.x, nt), blockIdx.y, smem);
+}
+
+// Grouped launch: independent problems of one kind back to back in one grid
+// (block b -> problem g with tile_end[g-1] <= b' < tile_end[g], b' XCD-remapped
+// over all tiles).  One launch of a decoder layer's ~256 weight-gradient tiles
+// fills the chip for one round with no split-K partials to reduce.
+struct GroupParams {
+  GemmParams g[NSTL_GEMM_GROUP_MAX];
+  int tile_end[NSTL_GEMM_GROUP_MAX];
+  int n;
+};
+
+template <bool AK, bool BKM, int EM>
+__global__ __launch_bounds__(BIG_NT, 1) void gemm256r_group_kernel(GroupParams gp) {
+  __shared__ __attribute__((aligned(16))) char smem[R_SMEM];
+  const int gid = xcd_remap(blockIdx.x, gp.tile_end[gp.n - 1]);
+  int g = 0;
+  while (g + 1 < gp.n && gid >= gp.tile_end[g]) ++g;
+  ring_tile<AK, BKM, EM>(gp.g[g], gid - (g > 0 ? gp.tile_end[g - 1] : 0), 0, smem);
 }
 
 // which lean epilogue fits this call (EM_GENERIC when none does)
@@ -933,7 +969,10 @@ extern "C" int64_t nstl_gemm_workspace_bytes(int M, int N, int split_k) {
   return split_k > 1 ? (int64_t)split_k * M * N * 4 : 0;
 }
 
-extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
+namespace {
+
+// validate one problem and fill its kernel parameters (no split-K decisions)
+int make_params(const nstl_gemm_args* a, GemmParams& p) {
   NSTL_CHECK_ARG(a != nullptr, "nstl_gemm: null args");
   NSTL_CHECK_ARG(a->dtype == NSTL_F32 || a->dtype == NSTL_BF16, "nstl_gemm: bad dtype %d", a->dtype);
   NSTL_CHECK_ARG(a->c_dtype == NSTL_F32 || a->c_dtype == NSTL_BF16, "nstl_gemm: bad c_dtype");
@@ -959,7 +998,6 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   if (a->epilogue == NSTL_EPI_DRELU_DROP) NSTL_CHECK_ARG(a->aux != nullptr, "nstl_gemm: aux missing");
   NSTL_CHECK_ARG(a->p_drop >= 0.f && a->p_drop < 1.f, "nstl_gemm: p_drop out of range");
 
-  GemmParams p;
   p.A = (const char*)a->A; p.lda = a->lda;
   p.B = (const char*)a->B; p.ldb = a->ldb;
   p.C = (char*)a->C; p.ldc = a->ldc;
@@ -976,14 +1014,28 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   p.rope_T = a->rope_T; p.rope_dim = a->rope_dim; p.rope_cols = a->rope_cols;
   p.ws = nullptr;
   p.debug_skip_epilogue = getenv_debug_skip_epi();
+  p.k_chunk = a->K;
+  return 0;
+}
+
+bool big_ok(const nstl_gemm_args* a) {
+  const int64_t big_tiles = (int64_t)((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
+  return a->dtype == NSTL_BF16 && a->K % 64 == 0 && a->M >= BIG && a->N >= BIG && big_tiles >= 32 &&
+         !getenv_small_gemm();
+}
+
+}  // namespace
+
+extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
+  GemmParams p;
+  if (int rc = make_params(a, p)) return rc;
+  const int esz = a->dtype == NSTL_F32 ? 4 : 2;
 
   // the 256x256 LDS-DMA kernel: bf16, K a multiple of its 64-deep K tile, and at
   // least 32 of its tiles (measured on the 228M step's shapes, tools/bench_gemm.py;
   // smaller/odd problems take the 128 kernel.  A 1024^2 dW split 16 ways on the
   // 256 kernel ties the 128 kernel split 8 ways: 60 vs 61 us, tools/bench_gemm_epi.py)
-  const int64_t big_tiles = (int64_t)((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
-  const bool big = a->dtype == NSTL_BF16 && a->K % 64 == 0 && a->M >= BIG && a->N >= BIG && big_tiles >= 32 &&
-                   !getenv_small_gemm();
+  const bool big = big_ok(a);
   const int BKe = big ? 64 : 128 / esz;
   int splits = a->split_k > 1 ? a->split_k : 1;
   if (splits > 1) {
@@ -1010,5 +1062,41 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
                        p.c_f32, a->beta, a->epilogue == NSTL_EPI_BIAS ? a->bias : nullptr);
     NSTL_LAUNCH_CHECK("nstl_gemm splitk_reduce");
   }
+  return 0;
+}
+
+extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream) {
+  NSTL_CHECK_ARG(args != nullptr && n >= 1 && n <= NSTL_GEMM_GROUP_MAX, "nstl_gemm_grouped: 1..%d problems (got %d)",
+                 NSTL_GEMM_GROUP_MAX, n);
+  GroupParams gp;
+  gp.n = n;
+  int tiles = 0;
+  for (int g = 0; g < n; ++g) {
+    const nstl_gemm_args* a = args + g;
+    if (int rc = make_params(a, gp.g[g])) return rc;
+    NSTL_CHECK_ARG(a->dtype == NSTL_BF16 && a->K % 64 == 0 && a->M >= BIG && a->N >= BIG,
+                   "nstl_gemm_grouped: problem %d is not a 256-kernel problem (bf16, M, N >= 256, K %% 64 == 0)", g);
+    NSTL_CHECK_ARG(a->epilogue == NSTL_EPI_NONE && a->split_k <= 1,
+                   "nstl_gemm_grouped: problem %d: no epilogue, no split-K", g);
+    NSTL_CHECK_ARG(a->a_kmajor == args[0].a_kmajor && a->b_kmajor == args[0].b_kmajor &&
+                       a->c_dtype == args[0].c_dtype && (a->beta != 0.f) == (args[0].beta != 0.f),
+                   "nstl_gemm_grouped: problem %d differs in layout, output type or beta use", g);
+    tiles += ((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
+    gp.tile_end[g] = tiles;
+  }
+  const int em = ring_epi_mode(args, gp.g[0]);
+  NSTL_CHECK_ARG(em == EM_F32 || em == EM_BF16, "nstl_gemm_grouped: f32 output, or bf16 without beta");
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(tiles), block(BIG_NT);
+#define NSTL_GROUP_LAUNCH(AKv, BKv)                                                                        \
+  if (em == EM_F32) hipLaunchKernelGGL((gemm256r_group_kernel<AKv, BKv, EM_F32>), grid, block, 0, st, gp); \
+  else hipLaunchKernelGGL((gemm256r_group_kernel<AKv, BKv, EM_BF16>), grid, block, 0, st, gp);
+  const bool ak = args[0].a_kmajor, bk = args[0].b_kmajor;
+  if (ak && bk) { NSTL_GROUP_LAUNCH(true, true) }
+  else if (ak && !bk) { NSTL_GROUP_LAUNCH(true, false) }
+  else if (!ak && !bk) { NSTL_GROUP_LAUNCH(false, false) }
+  else { NSTL_GROUP_LAUNCH(false, true) }
+#undef NSTL_GROUP_LAUNCH
+  NSTL_LAUNCH_CHECK("nstl_gemm_grouped");
   return 0;
 }

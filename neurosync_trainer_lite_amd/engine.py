@@ -102,6 +102,7 @@ class _Buffers:
             self.dres = e(M, D, dtype=f32)
             self.dmem = e(M, D, dtype=f32)
             self.dy = e(M, D)
+            self.dy_f, self.dy_x = e(M, D), e(M, D)  # decoder: dy of FFN2 / cross out_linear (grouped dW)
             self.dattn = e(M, D)
             self.dqkv = e(M, 3 * D)
             self.dq = e(M, D)
@@ -155,6 +156,10 @@ class Seq2SeqEngine:
         self.dw_stream_on = os.environ.get("NSTL_DW_STREAM", "0") == "1"
         self._side = None          # torch.cuda.Stream for dW (+ bias colsum)
         self._side_reads = []      # (lo, hi, event): bytes a queued dW still reads
+        # NSTL_DW_GROUP=0: one GEMM per weight gradient (split-K) instead of one
+        # grouped launch per decoder layer (its 7 weight gradients are 256 tiles)
+        self.dw_group_on = os.environ.get("NSTL_DW_GROUP", "1") != "0"
+        self._defer = None         # weight-gradient jobs of the current decoder layer
 
     # ------------------------------------------------------------------ setup
     def _check_shapes(self):
@@ -325,10 +330,17 @@ class Seq2SeqEngine:
 
     def _dw(self, dy, x, wname, rows, bf, ws, bias=True):
         """grad(W) (+)= dy^T x ; grad(b) (+)= colsum(dy) (unless the bias gradient
-        was already produced by the LayerNorm backward that wrote dy)."""
+        was already produced by the LayerNorm backward that wrote dy).  Inside a
+        decoder layer the GEMM is queued for that layer's grouped launch."""
         G = self.gw(wname, rows)
         n, k = G.shape
         m = dy.shape[0]
+        if self._defer is not None:
+            self._defer.append((dy, x, G, bf))
+            if bias:
+                bname = wname.replace(".weight", ".bias")
+                K.colsum(dy, dy.stride(0), m, n, self.cur.col_part, self.gb(bname, rows), bf, stream=self.st)
+            return
         s = self.splits(n, k, m)
         st = self._side_begin()
         K.gemm(dy, x, G, n, k, m, a_kmajor=False, b_kmajor=False, beta=bf, split_k=s, workspace=ws, stream=st)
@@ -336,6 +348,23 @@ class Seq2SeqEngine:
             bname = wname.replace(".weight", ".bias")
             K.colsum(dy, dy.stride(0), m, n, self.cur.col_part, self.gb(bname, rows), bf, stream=st)
         self._side_end(dy)
+
+    def _dw_flush(self, ws):
+        """Launch the queued weight gradients: one grouped GEMM (no split-K) when
+        every problem suits the 256 kernel, else one split-K GEMM each."""
+        jobs, self._defer = self._defer, None
+        ok = all(self.dt == torch.bfloat16 and G.shape[0] >= 256 and G.shape[1] >= 256 and dy.shape[0] >= 256
+                 and dy.shape[0] % 64 == 0 for dy, x, G, bf in jobs) and len(jobs) <= K.GEMM_GROUP_MAX
+        if ok:
+            K.gemm_grouped([(dy, x, G, G.shape[0], G.shape[1], dy.shape[0],
+                             dict(a_kmajor=False, b_kmajor=False, beta=bf)) for dy, x, G, bf in jobs],
+                           stream=self.st)
+            return
+        for dy, x, G, bf in jobs:
+            n, k = G.shape
+            m = dy.shape[0]
+            K.gemm(dy, x, G, n, k, m, a_kmajor=False, b_kmajor=False, beta=bf, split_k=self.splits(n, k, m),
+                   workspace=ws, stream=self.st)
 
     # ---------------------------------------------------- side (dW) stream
     # A dW GEMM only reads dy (a backward scratch buffer) and a saved activation
@@ -622,13 +651,14 @@ class Seq2SeqEngine:
         self._dw(bb.dqkv, x_in, pre + "self_attn.q_linear.weight", 3, bf, ws)
         self._dx(bb.dqkv, pre + "self_attn.q_linear.weight", 3, bb.dres, 1.0)
 
-    def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf):
+    def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf, dy=None):
         """Backward through x_out = LN(x_in + drop(FFN(x_in)))."""
         ws = self.cur.ws
-        self._ln_bwd(s_out, st, pre + norm, bb.dres, bb.dres, bb.dy, 1, (seed_drop, 0), bf,
+        dy = bb.dy if dy is None else dy
+        self._ln_bwd(s_out, st, pre + norm, bb.dres, bb.dres, dy, 1, (seed_drop, 0), bf,
                      bias_of=pre + "ffn.linear2.bias")
-        self._dw(bb.dy, h, pre + "ffn.linear2.weight", 1, bf, ws, bias=False)
-        self._dx(bb.dy, pre + "ffn.linear2.weight", 1, bb.dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p)
+        self._dw(dy, h, pre + "ffn.linear2.weight", 1, bf, ws, bias=False)
+        self._dx(dy, pre + "ffn.linear2.weight", 1, bb.dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p)
         self._dw(bb.dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws)
         self._dx(bb.dh, pre + "ffn.linear1.weight", 1, bb.dres, 1.0)
 
@@ -647,13 +677,18 @@ class Seq2SeqEngine:
         sd = lambda s: _seed(self.base_seed, False, l, s)
         st = bb.d_stats[l]
         x_in = bb.xdec0 if l == 0 else bb.d_x3[l - 1]
-        self._ffn_bwd(bb, pre, bb.d_x2[l], bb.d_h[l], bb.d_s3[l], st[4:6], "norm3", sd("drop3"), bf)
+        grouped = self.dw_group_on and self._side is None
+        if grouped:
+            self._defer = []
+        self._ffn_bwd(bb, pre, bb.d_x2[l], bb.d_h[l], bb.d_s3[l], st[4:6], "norm3", sd("drop3"), bf,
+                      dy=bb.dy_f if grouped else None)
         # cross attention block: x2 = LN(x1 + drop(drop(out(attn(q(x1), kv(mem))))))
         m = pre + "multihead_attn."
-        self._ln_bwd(bb.d_s2[l], st[2:4], pre + "norm2", bb.dres, bb.dres, bb.dy, 2, (sd("xresid"), sd("drop2x")), bf,
+        dyx = bb.dy_x if grouped else bb.dy
+        self._ln_bwd(bb.d_s2[l], st[2:4], pre + "norm2", bb.dres, bb.dres, dyx, 2, (sd("xresid"), sd("drop2x")), bf,
                      bias_of=m + "out_linear.bias")
-        self._dw(bb.dy, bb.d_oc[l], m + "out_linear.weight", 1, bf, ws, bias=False)
-        self._dx(bb.dy, m + "out_linear.weight", 1, bb.dattn, 0.0)
+        self._dw(dyx, bb.d_oc[l], m + "out_linear.weight", 1, bf, ws, bias=False)
+        self._dx(dyx, m + "out_linear.weight", 1, bb.dattn, 0.0)
         kvc = bb.d_kvc[l]
         self._attn_bwd(bb.d_qc[l], kvc[:, :D], kvc[:, D:], bb.d_oc[l], bb.d_lsec[l], bb.dattn,
                        bb.dq, bb.dkv[:, :D], bb.dkv[:, D:], sd("xattn"), T, bb.B, mask=bb.d_maskc[l])
@@ -663,6 +698,8 @@ class Seq2SeqEngine:
         self._dx(bb.dkv, m + "k_linear.weight", 2, bb.dmem, 0.0 if first else 1.0)
         self._attn_block_bwd(bb, pre, x_in, bb.d_qkv[l], bb.d_o[l], bb.d_lse[l], st[0:2], bb.d_s1[l], "norm1",
                              (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.d_mask[l])
+        if grouped:
+            self._dw_flush(ws)
 
 
 class Seq2SeqFunction(torch.autograd.Function):

@@ -141,6 +141,36 @@ def test_gemm_rejects_bad_args():
         K.gemm(A, A, C, 16, 16, 12, lda=10)
 
 
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_grouped_weight_gradients(beta):
+    """nstl_gemm_grouped: independent dW = dY^T X problems of different shapes in one
+    launch equal the same problems done one by one (and torch)."""
+    m = 1024
+    shapes = [(512, 256), (256, 768), (768, 512), (256, 256)]
+    probs, refs, outs = [], [], []
+    for i, (n, k) in enumerate(shapes):
+        dY, X = rnd(m, n, dtype=torch.bfloat16, seed=80 + i), rnd(m, k, dtype=torch.bfloat16, seed=90 + i)
+        G = rnd(n, k, seed=100 + i)
+        ref = f64(dY).t() @ f64(X) + beta * f64(G)
+        probs.append((dY, X, G, n, k, m, dict(a_kmajor=False, b_kmajor=False, beta=beta)))
+        refs.append(ref)
+        outs.append(G)
+    K.gemm_grouped(probs)
+    torch.cuda.synchronize()
+    for (n, k), G, ref in zip(shapes, outs, refs):
+        check(G, ref, 1e-5, "grouped dW %dx%d" % (n, k))
+
+
+def test_gemm_grouped_rejects_mixed_layouts():
+    A = torch.zeros(256, 256, dtype=torch.bfloat16, device=DEV)
+    C = torch.zeros(256, 256, device=DEV)
+    with pytest.raises(RuntimeError, match="differs"):
+        K.gemm_grouped([(A, A, C, 256, 256, 256, dict(a_kmajor=False, b_kmajor=False)),
+                        (A, A, C, 256, 256, 256, dict(a_kmajor=True, b_kmajor=False))])
+    with pytest.raises(RuntimeError, match="256-kernel"):
+        K.gemm_grouped([(A, A, C, 256, 128, 256, dict(a_kmajor=False, b_kmajor=False))])
+
+
 # ---------------------------------------------------------------------------
 def attn_ref(q, k, v, scale, mask=None, p=0.0):
     s = (q @ k.transpose(-1, -2)) * scale

@@ -65,5 +65,12 @@ for name, n, k, split in (("dW  out  split8", D, D, 8), ("dW  out  split16", D, 
     G = torch.zeros(n, k, dtype=torch.float32, device=dev)
     s = t(lambda: K.gemm(dY, X, G, n, k, M, a_kmajor=False, b_kmajor=False, split_k=split, workspace=ws))
     rows.append((name, 2 * M * n * k, s))
+# one 256-tile weight-gradient GEMM without split-K (K = all 16384 tokens): the rate
+# a per-layer grouped dW launch would run at; beta 0 and 1 (gradient accumulation)
+dY, X = r(M, 4096), r(M, 4096)
+G = torch.zeros(4096, 4096, dtype=torch.float32, device=dev)
+for beta in (0.0, 1.0):
+    s = t(lambda: K.gemm(dY, X, G, 4096, 4096, M, a_kmajor=False, b_kmajor=False, beta=beta))
+    rows.append(("dW  4096^2 nosplit b%d" % beta, 2 * M * 4096 * 4096, s))
 for nm, fl, s in rows:
     print("%-22s %8.1f TF/s %9.1f us" % (nm, fl / s / 1e12, s * 1e6))
