@@ -60,8 +60,13 @@ typedef struct nstl_gemm_args {
   int rope_T, rope_dim, rope_cols;
   int split_k;                         /* >1: f32 partials in workspace, then reduce */
   void* workspace; int64_t workspace_bytes;
+  float* colsum_part;                  /* optional [nstl_gemm_colsum_rows()][N] f32: per-128-row
+                                          column sums of C as stored (DRELU_DROP on the 256
+                                          kernel: the FFN1 bias gradient before nstl_reduce_rows) */
 } nstl_gemm_args;
 int nstl_gemm(const nstl_gemm_args* args, void* stream);
+/* Rows of colsum_part for these arguments, or 0 when the call cannot produce it. */
+int nstl_gemm_colsum_rows(const nstl_gemm_args* args);
 
 /* Up to NSTL_GEMM_GROUP_MAX independent problems in ONE launch (grouped GEMM):
    each a bf16 problem for the 256x256 kernel (M, N >= 256, K % 64 == 0), no
@@ -98,9 +103,16 @@ typedef struct nstl_attn_args {
                                  writes them, backward reads them instead of re-hashing
                                  (MFMA path: head_dim 64; ignored elsewhere).  NULL:
                                  both directions hash (seed, element). */
+  float* dbias_part;          /* optional backward output [nstl_attn_bias_rows()][3*H*dh] f32:
+                                 per-(batch, 128-row block) column sums of dq | dk | dv as
+                                 stored = the q/k/v projection bias gradients before the
+                                 final row reduction (nstl_reduce_rows). MFMA path only. */
 } nstl_attn_args;
 int nstl_attn_fwd(const nstl_attn_args* args, void* stream);
 int nstl_attn_bwd(const nstl_attn_args* args, void* stream);
+/* Rows of dbias_part for these arguments, or 0 when the call takes the generic
+   kernels (which do not produce it). */
+int nstl_attn_bias_rows(const nstl_attn_args* args);
 
 /* Post-LN residual block tail: s = x + dropout(dropout(y)); out = LN(s).
  * Replaces `src = src + self.dropoutN(src2); src = self.normN(src)` at
@@ -131,6 +143,9 @@ int nstl_ln_bwd(const nstl_ln_args* args, void* stream);
 
 /* out[j] = beta*out[j] + sum_p part[p][j]  (f32) */
 int nstl_reduce_rows(const float* part, int n_part, int cols, float* out, float beta, void* stream);
+/* the same over a column window of a wider matrix: rows ld floats apart */
+int nstl_reduce_rows_strided(const float* part, int64_t ld, int n_part, int cols, float* out, float beta,
+                             void* stream);
 /* Three such reductions in one launch: matrix m at part + m*mat_stride -> out_m
  * (LayerNorm backward's dgamma / dbeta / fused bias-grad partials). */
 int nstl_reduce_rows3(const float* part, int64_t mat_stride, int n_mat, int n_part, int cols, float* out0,

@@ -36,7 +36,7 @@ class GemmArgs(ctypes.Structure):
         ("bias", _vp), ("aux", _vp), ("ld_aux", _i64),
         ("p_drop", _f32), ("seed", _u64),
         ("rope_cos", _vp), ("rope_sin", _vp), ("rope_T", _i32), ("rope_dim", _i32), ("rope_cols", _i32),
-        ("split_k", _i32), ("workspace", _vp), ("workspace_bytes", _i64),
+        ("split_k", _i32), ("workspace", _vp), ("workspace_bytes", _i64), ("colsum_part", _vp),
     ]
 
 
@@ -49,7 +49,7 @@ class AttnArgs(ctypes.Structure):
         ("dout", _vp), ("dout_ld", _i64), ("dq", _vp), ("dq_ld", _i64), ("dk", _vp), ("dk_ld", _i64),
         ("dv", _vp), ("dv_ld", _i64),
         ("rope_cos", _vp), ("rope_sin", _vp), ("rope_q", _i32), ("rope_k", _i32),
-        ("dsum", _vp), ("mask_bits", _vp),
+        ("dsum", _vp), ("mask_bits", _vp), ("dbias_part", _vp),
     ]
 
 
@@ -87,10 +87,12 @@ class AdamArgs(ctypes.Structure):
 
 # every symbol include/nstl.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "nstl_gemm", "nstl_gemm_grouped", "nstl_gemm_workspace_bytes", "nstl_attn_fwd", "nstl_attn_bwd", "nstl_ln_fwd", "nstl_ln_bwd",
-    "nstl_reduce_rows", "nstl_reduce_rows3", "nstl_colsum", "nstl_rope", "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step",
-    "nstl_cast", "nstl_copy2d", "nstl_autocorr", "nstl_features", "nstl_features_workspace_bytes",
-    "nstl_features_frames", "nstl_last_error_string", "nstl_version",
+    "nstl_gemm", "nstl_gemm_grouped", "nstl_gemm_colsum_rows", "nstl_gemm_workspace_bytes",
+    "nstl_attn_fwd", "nstl_attn_bwd", "nstl_attn_bias_rows", "nstl_ln_fwd", "nstl_ln_bwd",
+    "nstl_reduce_rows", "nstl_reduce_rows_strided", "nstl_reduce_rows3", "nstl_colsum", "nstl_rope",
+    "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
+    "nstl_features", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
+    "nstl_version",
 ]
 
 _lib = None
@@ -108,13 +110,18 @@ def lib():
         P = ctypes.POINTER
         L.nstl_gemm.argtypes = [P(GemmArgs), _vp]
         L.nstl_gemm_grouped.argtypes = [P(GemmArgs), _i32, _vp]
+        L.nstl_gemm_colsum_rows.argtypes = [P(GemmArgs)]
+        L.nstl_gemm_colsum_rows.restype = _i32
         L.nstl_gemm_workspace_bytes.argtypes = [_i32, _i32, _i32]
         L.nstl_gemm_workspace_bytes.restype = _i64
         L.nstl_attn_fwd.argtypes = [P(AttnArgs), _vp]
         L.nstl_attn_bwd.argtypes = [P(AttnArgs), _vp]
+        L.nstl_attn_bias_rows.argtypes = [P(AttnArgs)]
+        L.nstl_attn_bias_rows.restype = _i32
         L.nstl_ln_fwd.argtypes = [P(LnArgs), _vp]
         L.nstl_ln_bwd.argtypes = [P(LnArgs), _vp]
         L.nstl_reduce_rows.argtypes = [_vp, _i32, _i32, _vp, _f32, _vp]
+        L.nstl_reduce_rows_strided.argtypes = [_vp, _i64, _i32, _i32, _vp, _f32, _vp]
         L.nstl_reduce_rows3.argtypes = [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]
         L.nstl_colsum.argtypes = [_i32, _vp, _i64, _i32, _i32, _vp, _vp, _f32, _vp]
         L.nstl_rope.argtypes = [_i32, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _vp]
@@ -167,6 +174,11 @@ def gemm(A, B, C, M, N, K, *, stream=None, **kw):
     check(lib().nstl_gemm(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_gemm")
 
 
+def gemm_colsum_rows(A, B, C, M, N, K, **kw):
+    """Partial rows nstl_gemm would write to colsum_part for these arguments (0: unsupported)."""
+    return lib().nstl_gemm_colsum_rows(ctypes.byref(gemm_args(A, B, C, M, N, K, **kw)))
+
+
 GEMM_GROUP_MAX = 8
 
 
@@ -182,7 +194,7 @@ def gemm_grouped(problems, stream=None):
 
 def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None,
               alpha=1.0, beta=0.0, epilogue=EPI_NONE, bias=None, aux=None, ld_aux=0, p_drop=0.0, seed=0,
-              rope=None, rope_cols=0, split_k=1, workspace=None):
+              rope=None, rope_cols=0, split_k=1, workspace=None, colsum_part=None):
     a = GemmArgs()
     a.dtype = dtype_code(A.dtype)
     a.c_dtype = dtype_code(C.dtype)
@@ -207,6 +219,7 @@ def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=N
     if workspace is not None:
         a.workspace = workspace.data_ptr()
         a.workspace_bytes = workspace.numel() * workspace.element_size()
+    a.colsum_part = ptr(colsum_part)
     return a
 
 
@@ -218,6 +231,10 @@ def attn_args(dtype, B, T, H, q, q_ld, k, k_ld, v, v_ld, o, o_ld, lse, p_drop, s
     a.o, a.o_ld, a.lse = o, o_ld, lse
     a.p_drop, a.seed = p_drop, seed & 0xFFFFFFFFFFFFFFFF
     return a
+
+
+def attn_bias_rows(a):
+    return lib().nstl_attn_bias_rows(ctypes.byref(a))
 
 
 def attn_fwd(a, stream=None):
@@ -246,6 +263,13 @@ def reduce_rows3(part, n_part, cols, outs, beta, stream=None):
 def reduce_rows(part, n_part, cols, out, beta, stream=None):
     check(lib().nstl_reduce_rows(part.data_ptr(), n_part, cols, out.data_ptr(), beta,
                                  stream if stream is not None else stream_of()), "nstl_reduce_rows")
+
+
+def reduce_rows_strided(part, ld, n_part, cols, out, beta, stream=None):
+    """out (+)= column sums of part[:n_part, :cols] (f32, rows ld floats apart; part
+    may be a column-offset view)."""
+    check(lib().nstl_reduce_rows_strided(part.data_ptr(), ld, n_part, cols, out.data_ptr(), beta,
+                                         stream if stream is not None else stream_of()), "nstl_reduce_rows_strided")
 
 
 def colsum(x, ld, rows, cols, partial, out, beta, stream=None):

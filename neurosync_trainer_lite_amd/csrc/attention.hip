@@ -36,6 +36,7 @@ struct AttnParams {
   float* lse;
   float* dsum;
   uint64_t* mask;  // dropout keep bits (fast path), see mask_word()
+  float* dbias;    // optional [B * nblk][3 * H * DH] column sums of dq | dk | dv (fast path)
   const char* dout; int64_t dout_ld;
   char* dq; int64_t dq_ld;
   char* dk; int64_t dk_ld;
@@ -277,6 +278,35 @@ NSTL_DEV void store_tile16x64(const float (&v)[4][4], char* scr, char* gbase, in
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// Bias gradients fused into the backward stores: column sums of a wave's stored
+// 16 x 64 tile (rounded to T, as colsum() of the stored tensor would see it) go
+// to red[w][64]; the LAST wave to finish (an LDS arrival counter, no barrier,
+// so early waves leave at once) adds the block's waves in fixed order and
+// writes one partial row: deterministic, no float atomics.
+template <typename T>
+NSTL_DEV void wave_colsum16x64(const float (&v)[4][4], float* red, int w, int lane) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    float c = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c += to_f32(from_f32<T>(v[dt][r]));
+    c += __shfl_xor(c, 16);
+    c += __shfl_xor(c, 32);
+    if (lane < 16) red[w * 64 + dt * 16 + lane] = c;
+  }
+}
+NSTL_DEV bool last_to_arrive(unsigned* cnt, int nw, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's red[] writes are done
+  unsigned old = 0;
+  if (lane == 0) old = atomicAdd(cnt, 1u);
+  return __shfl(old, 0) == (unsigned)(nw - 1);
+}
+NSTL_DEV void wave_sum_out(const float* red, int nw, float* out, int lane) {
+  float c = 0.f;
+  for (int k = 0; k < nw; ++k) c += red[k * 64 + lane];
+  out[lane] = c;
+}
+
 // ---------------------------------------------------------------------------
 // Backward, as two kernels (8 waves, 128 rows: all of T=128, so each (b, h)
 // operand is staged once) with ~48 KB LDS, 3 resident per CU:
@@ -351,9 +381,19 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
       lq[r] = p.lse[(int64_t)bh * T_ + q0 + 4 * g + r] * LOG2E;
     }
   }
+  float* red = (float*)(scratch + (BWD_NT / 64) * 2 * 32 * RBS);  // [8 waves][64] bias partials
+  unsigned* arrived = (unsigned*)(red + 2 * (BWD_NT / 64) * 64);
+  if (tid == 0) *arrived = 0u;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (!act) return;
+  float* bias_row = p.dbias ? p.dbias + (int64_t)(b * gridDim.x + blockIdx.x) * 3 * p.H * DH : nullptr;
+  if (!act) {
+    if (bias_row) {
+      red[w * 64 + lane] = 0.f;
+      if (last_to_arrive(arrived, BWD_NT / 64, lane)) wave_sum_out(red, BWD_NT / 64, bias_row + h * DH, lane);
+    }
+    return;
+  }
 
   const float c2 = p.scale * LOG2E;
   char* S2 = scratch + w * 2 * 32 * RBS;
@@ -424,6 +464,10 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
     }
   }
   store_tile16x64<T>(vq, S2, p.dq + ((tok0 + q0) * p.dq_ld + h * DH) * ESZ, p.dq_ld, lane);
+  if (bias_row) {
+    wave_colsum16x64<T>(vq, red, w, lane);
+    if (last_to_arrive(arrived, BWD_NT / 64, lane)) wave_sum_out(red, BWD_NT / 64, bias_row + h * DH, lane);
+  }
 }
 
 template <typename T>
@@ -465,9 +509,24 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
       gload_frag<T>(fv[u], vrow, 32 * u + 8 * g);
     }
   }
+  float* red = (float*)(scratch + (BWD_NT / 64) * 2 * 32 * RBS);  // [2][8 waves][64] bias partials
+  unsigned* arrived = (unsigned*)(red + 2 * (BWD_NT / 64) * 64);
+  if (tid == 0) *arrived = 0u;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (!act) return;
+  constexpr int NWB = BWD_NT / 64;
+  float* bias_row = p.dbias ? p.dbias + (int64_t)(b * gridDim.x + blockIdx.x) * 3 * p.H * DH : nullptr;
+  if (!act) {
+    if (bias_row) {
+      red[w * 64 + lane] = 0.f;
+      red[NWB * 64 + w * 64 + lane] = 0.f;
+      if (last_to_arrive(arrived, NWB, lane)) {
+        wave_sum_out(red, NWB, bias_row + p.H * DH + h * DH, lane);
+        wave_sum_out(red + NWB * 64, NWB, bias_row + 2 * p.H * DH + h * DH, lane);
+      }
+    }
+    return;
+  }
 
   const float c2 = p.scale * LOG2E;
   char* S1 = scratch + w * 2 * 32 * RBS;  // [32 rows][16] images
@@ -547,13 +606,22 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
   }
   store_tile16x64<T>(vk, S1, p.dk + ((tok0 + k0) * p.dk_ld + h * DH) * ESZ, p.dk_ld, lane);
   store_tile16x64<T>(vv, S1, p.dv + ((tok0 + k0) * p.dv_ld + h * DH) * ESZ, p.dv_ld, lane);
+  if (bias_row) {
+    wave_colsum16x64<T>(vk, red, w, lane);
+    wave_colsum16x64<T>(vv, red + NWB * 64, w, lane);
+    if (last_to_arrive(arrived, NWB, lane)) {
+      wave_sum_out(red, NWB, bias_row + p.H * DH + h * DH, lane);
+      wave_sum_out(red + NWB * 64, NWB, bias_row + 2 * p.H * DH + h * DH, lane);
+    }
+  }
 }
 
 size_t fwd_lds_bytes(int T, int esz) {
   return (size_t)(2 * T + FWD_QB) * DH * esz + (FWD_NT / 64) * (size_t)std::max(T, 64) * 16 * esz;
 }
-size_t bwd_lds_bytes(int T, int esz) {  // either backward kernel
-  return (size_t)2 * T * DH * esz + 2 * T * 4 + (BWD_NT / 64) * 2 * 32 * 16 * (size_t)esz;
+size_t bwd_lds_bytes(int T, int esz) {  // either backward kernel (+ 2 x [8][64] f32 bias partials + counter)
+  return (size_t)2 * T * DH * esz + 2 * T * 4 + (BWD_NT / 64) * 2 * 32 * 16 * (size_t)esz +
+         2 * (BWD_NT / 64) * 64 * 4 + 16;
 }
 
 // ---------------------------------------------------------------------------
@@ -798,6 +866,7 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
                    "nstl_attn_bwd: dq/dk/dv must be 16-byte aligned");
     NSTL_CHECK_ARG(!(a->rope_q || a->rope_k) || (a->rope_cos && a->rope_sin), "nstl_attn_bwd: rope tables");
     NSTL_CHECK_ARG(!use_fast(a) || a->dsum, "nstl_attn_bwd: dsum scratch [B*H*T] f32 missing");
+    NSTL_CHECK_ARG(!a->dbias_part || use_fast(a), "nstl_attn_bwd: dbias_part needs the MFMA path (head_dim 64)");
   }
   p.q = (const char*)a->q; p.q_ld = a->q_ld;
   p.k = (const char*)a->k; p.k_ld = a->k_ld;
@@ -806,6 +875,7 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   p.lse = a->lse;
   p.dsum = a->dsum;
   p.mask = a->mask_bits;
+  p.dbias = a->dbias_part;
   p.dout = (const char*)a->dout; p.dout_ld = a->dout_ld;
   p.dq = (char*)a->dq; p.dq_ld = a->dq_ld;
   p.dk = (char*)a->dk; p.dk_ld = a->dk_ld;
@@ -873,4 +943,9 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
   }
   if ((rc = launch(attn_bwd_dq_kernel<float>, grid, lds, st, p, "nstl_attn_bwd dq", BWD_NT))) return rc;
   return launch(attn_bwd_dkv_kernel<float>, grid, lds, st, p, "nstl_attn_bwd dkv", BWD_NT);
+}
+
+extern "C" int nstl_attn_bias_rows(const nstl_attn_args* a) {
+  if (a == nullptr || !use_fast(a)) return 0;
+  return a->B * ((a->T + BWD_ROWS - 1) / BWD_ROWS);
 }

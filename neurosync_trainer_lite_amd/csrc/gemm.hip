@@ -39,6 +39,7 @@ struct GemmParams {
   const float* rope_cos; const float* rope_sin; int rope_T, rope_dim, rope_cols;
   float* ws;
   int debug_skip_epilogue; int k_chunk;  // split-K: partial slabs [z][M][N]
+  float* colsum_part;  // [ceil(M/128)][N]: column sums of C as stored (dReLU ring epilogue)
 };
 
 // Epilogue over a wave's MT x 4 grid of 16x16 accumulators whose origin is
@@ -566,6 +567,11 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
   // cos/sin of 8 columns = 4 consecutive table entries (16 B) when rope_dim % 8 == 0
   const bool rope_vec = (p.rope_dim & 7) == 0;
   const int r0 = lane / LPR;
+  // dReLU epilogue: column sums of the stored dh (the FFN1 bias gradient)
+  const bool csum_on = EM == EM_DRELU && p.colsum_part != nullptr;
+  float csum[CW];
+#pragma unroll
+  for (int e = 0; e < CW; ++e) csum[e] = 0.f;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
    const int ib = row0 + half * 64 + r0;
@@ -671,6 +677,10 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
           const bf16x8 a8 = ind[iu % ND];
 #pragma unroll
           for (int e = 0; e < CW; ++e) v[e] = (float)a8[e % 8] > 0.f ? v[e] * p.inv_keep : 0.f;
+          if (csum_on) {
+#pragma unroll
+            for (int e = 0; e < CW; ++e) csum[e] += (float)(bf16)v[e];  // sum what is stored
+          }
         } else if (EM == EM_F32) {
           if (use_beta) {
             const f32x4 o = inf[iu % NF];
@@ -706,6 +716,20 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
     }
    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (csum_on) {
+    // lanes l, l + LPR, ... share columns: fold them, then LPR lanes write the
+    // wave's 64 column sums as one partial row (this wave's 128 rows)
+#pragma unroll
+    for (int e = 0; e < CW; ++e)
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) csum[e] += __shfl_xor(csum[e], o);
+    if (lane < LPR && colok) {
+      float* dst = p.colsum_part + (int64_t)(row0 >> 7) * p.N + j;
+#pragma unroll
+      for (int e = 0; e < CW; ++e)
+        if (j + e < p.N) dst[e] = csum[e];
+    }
   }
 }
 
@@ -1015,6 +1039,7 @@ int make_params(const nstl_gemm_args* a, GemmParams& p) {
   p.ws = nullptr;
   p.debug_skip_epilogue = getenv_debug_skip_epi();
   p.k_chunk = a->K;
+  p.colsum_part = a->colsum_part;
   return 0;
 }
 
@@ -1036,6 +1061,9 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   // smaller/odd problems take the 128 kernel.  A 1024^2 dW split 16 ways on the
   // 256 kernel ties the 128 kernel split 8 ways: 60 vs 61 us, tools/bench_gemm_epi.py)
   const bool big = big_ok(a);
+  NSTL_CHECK_ARG(!a->colsum_part || (big && a->epilogue == NSTL_EPI_DRELU_DROP && a->split_k <= 1 &&
+                                      ring_epi_mode(a, p) == EM_DRELU && getenv_ring()),
+                 "nstl_gemm: colsum_part needs the 256 kernel's dReLU epilogue (nstl_gemm_colsum_rows)");
   const int BKe = big ? 64 : 128 / esz;
   int splits = a->split_k > 1 ? a->split_k : 1;
   if (splits > 1) {
@@ -1076,7 +1104,7 @@ extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream
     if (int rc = make_params(a, gp.g[g])) return rc;
     NSTL_CHECK_ARG(a->dtype == NSTL_BF16 && a->K % 64 == 0 && a->M >= BIG && a->N >= BIG,
                    "nstl_gemm_grouped: problem %d is not a 256-kernel problem (bf16, M, N >= 256, K %% 64 == 0)", g);
-    NSTL_CHECK_ARG(a->epilogue == NSTL_EPI_NONE && a->split_k <= 1,
+    NSTL_CHECK_ARG(a->epilogue == NSTL_EPI_NONE && a->split_k <= 1 && !a->colsum_part,
                    "nstl_gemm_grouped: problem %d: no epilogue, no split-K", g);
     NSTL_CHECK_ARG(a->a_kmajor == args[0].a_kmajor && a->b_kmajor == args[0].b_kmajor &&
                        a->c_dtype == args[0].c_dtype && (a->beta != 0.f) == (args[0].beta != 0.f),
@@ -1099,4 +1127,12 @@ extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream
 #undef NSTL_GROUP_LAUNCH
   NSTL_LAUNCH_CHECK("nstl_gemm_grouped");
   return 0;
+}
+
+extern "C" int nstl_gemm_colsum_rows(const nstl_gemm_args* a) {
+  GemmParams p;
+  if (a == nullptr || make_params(a, p) != 0) return 0;
+  if (!big_ok(a) || a->epilogue != NSTL_EPI_DRELU_DROP || a->split_k > 1 || !getenv_ring()) return 0;
+  if (ring_epi_mode(a, p) != EM_DRELU) return 0;
+  return (a->M + 127) / 128;
 }

@@ -161,16 +161,16 @@ __global__ void colsum_kernel(const T* x, int64_t ld, int rows, int cols, float*
 
 // out[j] = beta*out[j] + sum_k part[k][j]: block = 64 columns x 4 row groups
 __global__ __launch_bounds__(NT) void reduce_rows_kernel(const float* part, int n_part, int cols, float* out,
-                                                         float beta) {
+                                                         float beta, int64_t ld) {
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + cl;
   float s = 0.f;
   if (j < cols) {
     int k = rg;
     for (; k + 12 < n_part; k += 16)
-      s += (part[(int64_t)k * cols + j] + part[(int64_t)(k + 4) * cols + j]) +
-           (part[(int64_t)(k + 8) * cols + j] + part[(int64_t)(k + 12) * cols + j]);
-    for (; k < n_part; k += 4) s += part[(int64_t)k * cols + j];
+      s += (part[(int64_t)k * ld + j] + part[(int64_t)(k + 4) * ld + j]) +
+           (part[(int64_t)(k + 8) * ld + j] + part[(int64_t)(k + 12) * ld + j]);
+    for (; k < n_part; k += 4) s += part[(int64_t)k * ld + j];
   }
   __shared__ float red[4][64];
   red[rg][cl] = s;
@@ -280,7 +280,8 @@ extern "C" int nstl_colsum(int dtype, const void* x, int64_t ld, int rows, int c
       hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(NT), 0, st, (const float*)x, ld, rows, cols, partial);
   }
   NSTL_LAUNCH_CHECK("nstl_colsum");
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + 63) / 64), dim3(NT), 0, st, partial, nchunk, cols, out, beta);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + 63) / 64), dim3(NT), 0, st, partial, nchunk, cols, out, beta,
+                     (int64_t)cols);
   NSTL_LAUNCH_CHECK("nstl_colsum reduce");
   return 0;
 }
@@ -320,9 +321,14 @@ extern "C" int nstl_reduce_rows3(const float* part, int64_t mat_stride, int n_ma
 }
 
 extern "C" int nstl_reduce_rows(const float* part, int n_part, int cols, float* out, float beta, void* stream) {
-  NSTL_CHECK_ARG(part && out && n_part > 0 && cols > 0, "nstl_reduce_rows: bad args");
+  return nstl_reduce_rows_strided(part, cols, n_part, cols, out, beta, stream);
+}
+
+extern "C" int nstl_reduce_rows_strided(const float* part, int64_t ld, int n_part, int cols, float* out, float beta,
+                                        void* stream) {
+  NSTL_CHECK_ARG(part && out && n_part > 0 && cols > 0 && ld >= cols, "nstl_reduce_rows: bad args");
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((cols + 63) / 64), dim3(NT), 0, (hipStream_t)stream, part, n_part,
-                     cols, out, beta);
+                     cols, out, beta, ld);
   NSTL_LAUNCH_CHECK("nstl_reduce_rows");
   return 0;
 }

@@ -111,6 +111,10 @@ class _Buffers:
             self.demb = e(M, D)
             self.dpred = torch.zeros(M, 64, dtype=dt, device=dev)
             self.dsum = e(B * eng.H * T, dtype=f32)  # attention backward rowsum(dO * O)
+            # attention backward: per-(batch, 128 rows) column sums of dq | dk | dv (bias grads)
+            self.abias = e(B * ((T + 127) // 128), 3 * D, dtype=f32)
+            # FFN2 dX (dReLU epilogue): per-128-row column sums of dh (FFN1 bias grad)
+            self.hpart = e((M + 127) // 128, Fd, dtype=f32)
             # attention dropout keep bits, written by the forward, read by the backward
             nw = max(1, B * eng.H * T * T // 64)
             self.e_mask = [e(nw, dtype=torch.int64) for _ in range(L)]
@@ -160,6 +164,9 @@ class Seq2SeqEngine:
         # grouped launch per decoder layer (its 7 weight gradients are 256 tiles)
         self.dw_group_on = os.environ.get("NSTL_DW_GROUP", "1") != "0"
         self._defer = None         # weight-gradient jobs of the current decoder layer
+        # NSTL_FUSED_BIAS=0: q/k/v and FFN1 bias gradients by colsum() instead of
+        # the attention-backward / dReLU-epilogue column sums
+        self.fused_bias_on = os.environ.get("NSTL_FUSED_BIAS", "1") != "0"
 
     # ------------------------------------------------------------------ setup
     def _check_shapes(self):
@@ -406,13 +413,22 @@ class Seq2SeqEngine:
             self._main.wait_stream(self._side)
             self._side_reads = []
 
-    def _dx(self, dy, wname, rows, out, beta, epi=K.EPI_NONE, aux=None, p_drop=0.0):
-        """out (+)= dy W  (W: [N][K] read as [r][j])."""
+    def _dx(self, dy, wname, rows, out, beta, epi=K.EPI_NONE, aux=None, p_drop=0.0, colsum=None):
+        """out (+)= dy W  (W: [N][K] read as [r][j]).  colsum = (partials, grad(b), beta):
+        the bias gradient of the Linear whose input gradient `out` is, from the
+        epilogue's column sums; returns False when the kernel cannot produce them."""
         W = self.w(wname, rows)
         n, k = W.shape
         self._guard(out)
-        K.gemm(dy, W, out, dy.shape[0], k, n, a_kmajor=True, b_kmajor=False, beta=beta, epilogue=epi, aux=aux,
-               ld_aux=aux.stride(0) if aux is not None else 0, p_drop=p_drop, stream=self.st)
+        kw = dict(a_kmajor=True, b_kmajor=False, beta=beta, epilogue=epi, aux=aux,
+                  ld_aux=aux.stride(0) if aux is not None else 0, p_drop=p_drop)
+        m = dy.shape[0]
+        nrows = K.gemm_colsum_rows(dy, W, out, m, k, n, **kw) if colsum is not None and self.fused_bias_on else 0
+        fused = 0 < nrows <= (colsum[0].shape[0] if colsum is not None else 0)
+        K.gemm(dy, W, out, m, k, n, colsum_part=colsum[0] if fused else None, stream=self.st, **kw)
+        if fused:
+            K.reduce_rows(colsum[0], nrows, k, colsum[1], colsum[2], stream=self.st)
+        return fused
 
     def _ln(self, x, y, out, stats, prefix, n_masks, seeds, s_out, rot=None, T=None):
         a = K.LnArgs()
@@ -457,7 +473,11 @@ class Seq2SeqEngine:
         a.mask_bits = K.ptr(mask)
         K.attn_fwd(a, stream=self.st)
 
-    def _attn_bwd(self, q, k, v, o, lse, do, dq, dk, dv, seed, T, B, mask=None):
+    def _attn_bwd(self, q, k, v, o, lse, do, dq, dk, dv, seed, T, B, mask=None, bias=(), bf=0.0):
+        """Attention backward.  `bias`: (column offset in q|k|v, columns, grad(bias)
+        view) -- the projection bias gradients, reduced from the kernel's fused
+        column sums.  Returns False when the call took the generic kernels (no
+        sums: the caller's colsum provides them)."""
         a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
                         v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed,
                         dh=self.dh)
@@ -468,8 +488,16 @@ class Seq2SeqEngine:
         a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
         a.dsum = self.cur.dsum.data_ptr()
         a.mask_bits = K.ptr(mask)
+        part = self.cur.abias
+        rows = K.attn_bias_rows(a) if bias and self.fused_bias_on else 0
+        fused = 0 < rows <= part.shape[0]
+        if fused:
+            a.dbias_part = part.data_ptr()
         self._guard(dq, dk, dv)
         K.attn_bwd(a, stream=self.st)
+        for off, n, out in (bias if fused else ()):
+            K.reduce_rows_strided(part[:, off:], part.stride(0), rows, n, out, bf, stream=self.st)
+        return fused
 
     # --------------------------------------------------------------- forward
     def _enc_layer(self, bb, l, x, T):
@@ -646,9 +674,10 @@ class Seq2SeqEngine:
                      bias_of=pre + "self_attn.out_linear.bias")
         self._dw(bb.dy, o, pre + "self_attn.out_linear.weight", 1, bf, ws, bias=False)
         self._dx(bb.dy, pre + "self_attn.out_linear.weight", 1, bb.dattn, 0.0)
-        self._attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, bb.dattn,
-                       bb.dqkv[:, :D], bb.dqkv[:, D:2 * D], bb.dqkv[:, 2 * D:], seeds[2], T, bb.B, mask=mask)
-        self._dw(bb.dqkv, x_in, pre + "self_attn.q_linear.weight", 3, bf, ws)
+        fused = self._attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, bb.dattn,
+                               bb.dqkv[:, :D], bb.dqkv[:, D:2 * D], bb.dqkv[:, 2 * D:], seeds[2], T, bb.B, mask=mask,
+                               bias=[(0, 3 * D, self.gb(pre + "self_attn.q_linear.bias", 3))], bf=bf)
+        self._dw(bb.dqkv, x_in, pre + "self_attn.q_linear.weight", 3, bf, ws, bias=not fused)
         self._dx(bb.dqkv, pre + "self_attn.q_linear.weight", 3, bb.dres, 1.0)
 
     def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf, dy=None):
@@ -658,8 +687,9 @@ class Seq2SeqEngine:
         self._ln_bwd(s_out, st, pre + norm, bb.dres, bb.dres, dy, 1, (seed_drop, 0), bf,
                      bias_of=pre + "ffn.linear2.bias")
         self._dw(dy, h, pre + "ffn.linear2.weight", 1, bf, ws, bias=False)
-        self._dx(dy, pre + "ffn.linear2.weight", 1, bb.dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p)
-        self._dw(bb.dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws)
+        fused = self._dx(dy, pre + "ffn.linear2.weight", 1, bb.dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p,
+                         colsum=(bb.hpart, self.gb(pre + "ffn.linear1.bias"), bf))
+        self._dw(bb.dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws, bias=not fused)
         self._dx(bb.dh, pre + "ffn.linear1.weight", 1, bb.dres, 1.0)
 
     def _enc_layer_bwd(self, bb, l, T, bf):
@@ -690,11 +720,13 @@ class Seq2SeqEngine:
         self._dw(dyx, bb.d_oc[l], m + "out_linear.weight", 1, bf, ws, bias=False)
         self._dx(dyx, m + "out_linear.weight", 1, bb.dattn, 0.0)
         kvc = bb.d_kvc[l]
-        self._attn_bwd(bb.d_qc[l], kvc[:, :D], kvc[:, D:], bb.d_oc[l], bb.d_lsec[l], bb.dattn,
-                       bb.dq, bb.dkv[:, :D], bb.dkv[:, D:], sd("xattn"), T, bb.B, mask=bb.d_maskc[l])
-        self._dw(bb.dq, bb.d_x1[l], m + "q_linear.weight", 1, bf, ws)
+        fused = self._attn_bwd(bb.d_qc[l], kvc[:, :D], kvc[:, D:], bb.d_oc[l], bb.d_lsec[l], bb.dattn,
+                               bb.dq, bb.dkv[:, :D], bb.dkv[:, D:], sd("xattn"), T, bb.B, mask=bb.d_maskc[l],
+                               bias=[(0, D, self.gb(m + "q_linear.bias")), (D, 2 * D, self.gb(m + "k_linear.bias", 2))],
+                               bf=bf)
+        self._dw(bb.dq, bb.d_x1[l], m + "q_linear.weight", 1, bf, ws, bias=not fused)
         self._dx(bb.dq, m + "q_linear.weight", 1, bb.dres, 1.0)
-        self._dw(bb.dkv, bb.mem, m + "k_linear.weight", 2, bf, ws)
+        self._dw(bb.dkv, bb.mem, m + "k_linear.weight", 2, bf, ws, bias=not fused)
         self._dx(bb.dkv, m + "k_linear.weight", 2, bb.dmem, 0.0 if first else 1.0)
         self._attn_block_bwd(bb, pre, x_in, bb.d_qkv[l], bb.d_o[l], bb.d_lse[l], st[0:2], bb.d_s1[l], "norm1",
                              (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.d_mask[l])

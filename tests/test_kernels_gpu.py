@@ -141,6 +141,31 @@ def test_gemm_rejects_bad_args():
         K.gemm(A, A, C, 16, 16, 12, lda=10)
 
 
+@pytest.mark.parametrize("M,N", [(16384 // 8, 4096), (1000, 2048)])
+def test_gemm_drelu_colsum_partials(M, N):
+    """colsum_part: the dReLU epilogue's per-128-row column sums of the stored dh
+    (FFN1 bias gradient) against torch on the stored output; ragged M."""
+    Kd = 512
+    dY, W = rnd(M, Kd, dtype=torch.bfloat16, seed=120), rnd(Kd, N, dtype=torch.bfloat16, seed=121)
+    h = torch.relu(rnd(M, N, dtype=torch.bfloat16, seed=122))
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    kw = dict(a_kmajor=True, b_kmajor=False, epilogue=K.EPI_DRELU_DROP, aux=h, ld_aux=N, p_drop=0.25)
+    rows = K.gemm_colsum_rows(dY, W, out, M, N, Kd, **kw)
+    assert rows == (M + 127) // 128
+    part = torch.full((rows, N), float("nan"), device=DEV)
+    K.gemm(dY, W, out, M, N, Kd, colsum_part=part, **kw)
+    bgrad = torch.zeros(N, device=DEV)
+    K.reduce_rows(part, rows, N, bgrad, 0.0)
+    torch.cuda.synchronize()
+    check(bgrad, f64(out).sum(0), 1e-5, "dReLU colsum")
+    ref = (f64(dY) @ f64(W)) * (f64(h) > 0) / 0.75
+    check(out, ref, 1e-2, "dReLU out")
+    # other epilogues / the 128 kernel cannot produce the sums
+    assert K.gemm_colsum_rows(dY, W, out, M, N, Kd, a_kmajor=True, b_kmajor=False) == 0
+    with pytest.raises(RuntimeError, match="colsum_part"):
+        K.gemm(dY, W, out, M, N, Kd, a_kmajor=True, b_kmajor=False, colsum_part=part)
+
+
 @pytest.mark.parametrize("beta", [0.0, 1.0])
 def test_gemm_grouped_weight_gradients(beta):
     """nstl_gemm_grouped: independent dW = dY^T X problems of different shapes in one
@@ -317,6 +342,46 @@ def test_attention_stored_mask_bits(dt, T):
     bits = outs[1][2].cpu().numpy().view(np.uint8)
     frac = np.unpackbits(bits).mean()
     assert abs(frac - (1 - p)) < 0.01, frac
+
+
+@pytest.mark.parametrize("dt,T", [(torch.bfloat16, 128), (torch.bfloat16, 64), (torch.bfloat16, 256),
+                                  (torch.float32, 96)])
+def test_attention_bias_partials(dt, T):
+    """dbias_part: the backward's fused column sums of dq | dk | dv (as stored) give
+    the q/k/v projection bias gradients after a row reduction."""
+    B, H, dh = 3, 2, 64
+    M, D = B * T, H * dh
+    qkv = rnd(M, 3 * D, dtype=dt, scale=0.5, seed=110)
+    o = torch.empty(M, D, dtype=dt, device=DEV)
+    lse = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
+    a = K.attn_args(K.dtype_code(dt), B, T, H, qkv.data_ptr(), 3 * D, qkv[:, D:].data_ptr(), 3 * D,
+                    qkv[:, 2 * D:].data_ptr(), 3 * D, o.data_ptr(), D, lse.data_ptr(), 0.2, 99, dh=dh)
+    K.attn_fwd(a)
+    do = rnd(M, D, dtype=dt, seed=111)
+    dqkv = torch.zeros(M, 3 * D, dtype=dt, device=DEV)
+    cs, sn = rotation_tables(T, dh, DEV)
+    a.dout, a.dout_ld = do.data_ptr(), D
+    a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dqkv.data_ptr(), 3 * D, dqkv[:, D:].data_ptr(), 3 * D,
+                                                    dqkv[:, 2 * D:].data_ptr(), 3 * D)
+    a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
+    dsum = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
+    a.dsum = dsum.data_ptr()
+    rows = K.attn_bias_rows(a)
+    assert rows == B * ((T + 127) // 128)
+    part = torch.full((rows, 3 * D), float("nan"), device=DEV)
+    a.dbias_part = part.data_ptr()
+    K.attn_bwd(a)
+    out = torch.full((3 * D,), 5.0, device=DEV)
+    K.reduce_rows_strided(part, 3 * D, rows, 3 * D, out, 1.0)
+    qpart = torch.zeros(D, device=DEV)
+    K.reduce_rows_strided(part[:, D:], 3 * D, rows, D, qpart, 0.0)   # the k window alone
+    torch.cuda.synchronize()
+    ref = f64(dqkv).sum(0)
+    check(out - 5.0, ref, 1e-5, "fused q|k|v bias grads")
+    check(qpart, ref[D:2 * D], 1e-5, "k window")
+    # the generic kernels do not produce the sums
+    a.dh = 32
+    assert K.attn_bias_rows(a) == 0
 
 
 def test_attention_rejects_bad_shapes():
