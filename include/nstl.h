@@ -137,6 +137,9 @@ typedef struct nstl_ln_args {
                                                           (rows/4 when D % 256 != 0) */
   float* dbranch_part;     /* optional [n_part][D]: column sums of dbranch (the bias
                               gradient of the Linear that produced y) */
+  const void* dout2;       /* optional dtype [rows][D], added to dout: the input gradient
+                              of a Linear fed by this LN's output, kept in dtype as the
+                              reference's autocast casts it (utils/model.py Linears) */
 } nstl_ln_args;
 int nstl_ln_fwd(const nstl_ln_args* args, void* stream);
 int nstl_ln_bwd(const nstl_ln_args* args, void* stream);

@@ -62,6 +62,7 @@ struct LnParams {
   char* s_out; char* out; float* mean; float* rstd;
   char* rot_out; const float* rope_cos; const float* rope_sin; int rope_T;
   const char* s_in; const float* dout; float* ds; char* dbranch;
+  const char* dout2;  // optional dtype addend of dout
   float* dgp; float* dbp; float* dyp;
 };
 
@@ -154,6 +155,12 @@ __global__ __launch_bounds__(NT) void ln_bwd_kernel(LnParams p) {
     float xh[VPL], gy[VPL];
     load_row<T, VPL>((const T*)p.s_in + base, xh);
     load_row<float, VPL>(p.dout + base, gy);
+    if (p.dout2) {
+      float g2[VPL];
+      load_row<T, VPL>((const T*)p.dout2 + base, g2);
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) gy[j] += g2[j];
+    }
     float a1 = 0.f, a2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
@@ -263,13 +270,14 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
     const int64_t base = (int64_t)r * p.D + 4 * lane;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      float t4[4], g4[4];
+      float t4[4], g4[4], a4[4] = {0.f, 0.f, 0.f, 0.f};
       load4<T>((const T*)p.s_in + base + k * 256, t4);
       load4<float>(p.dout + base + k * 256, g4);
+      if (p.dout2) load4<T>((const T*)p.dout2 + base + k * 256, a4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         x[4 * k + e] = t4[e];
-        g[4 * k + e] = g4[e];
+        g[4 * k + e] = g4[e] + a4[e];
       }
     }
     mu = p.mean[r];
@@ -470,6 +478,7 @@ int fill(LnParams& p, const nstl_ln_args* a) {
   p.rot_out = (char*)a->rot_out; p.rope_cos = a->rope_cos; p.rope_sin = a->rope_sin; p.rope_T = a->rope_T;
   p.s_in = (const char*)a->s_in; p.dout = a->dout; p.ds = a->ds; p.dbranch = (char*)a->dbranch;
   p.dgp = a->dgamma_part; p.dbp = a->dbeta_part; p.dyp = a->dbranch_part;
+  p.dout2 = (const char*)a->dout2;
   return 0;
 }
 

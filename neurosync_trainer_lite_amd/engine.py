@@ -103,6 +103,7 @@ class _Buffers:
             self.dmem = e(M, D, dtype=f32)
             self.dy = e(M, D)
             self.dy_f, self.dy_x = e(M, D), e(M, D)  # decoder: dy of FFN2 / cross out_linear (grouped dW)
+            self.dadd = e(M, D)  # a Linear's input gradient (dtype), added by the next LN backward
             self.dattn = e(M, D)
             self.dqkv = e(M, 3 * D)
             self.dq = e(M, D)
@@ -167,6 +168,11 @@ class Seq2SeqEngine:
         # NSTL_FUSED_BIAS=0: q/k/v and FFN1 bias gradients by colsum() instead of
         # the attention-backward / dReLU-epilogue column sums
         self.fused_bias_on = os.environ.get("NSTL_FUSED_BIAS", "1") != "0"
+        # NSTL_RES_HANDOFF=0: input gradients of the Linears fed by a LayerNorm are
+        # accumulated into the f32 residual gradient by the GEMM (read-modify-write)
+        # instead of being written in the compute dtype and added by the next LN backward
+        self.res_handoff_on = os.environ.get("NSTL_RES_HANDOFF", "1") != "0"
+        self._dadd_pending = False
 
     # ------------------------------------------------------------------ setup
     def _check_shapes(self):
@@ -430,6 +436,19 @@ class Seq2SeqEngine:
             K.reduce_rows(colsum[0], nrows, k, colsum[1], colsum[2], stream=self.st)
         return fused
 
+    def _dx_res(self, dy, wname, rows, last=False):
+        """Input gradient of a Linear whose input is a LayerNorm output: accumulate
+        it into the f32 residual gradient.  Handoff mode writes it in the compute
+        dtype (as the reference's autocast rounds it) for the next LN backward to
+        add; `last` (the consumer is not an LN backward) keeps the f32 accumulate."""
+        bb = self.cur
+        if self.res_handoff_on and not last:
+            assert not self._dadd_pending
+            self._dx(dy, wname, rows, bb.dadd, 0.0)
+            self._dadd_pending = True
+        else:
+            self._dx(dy, wname, rows, bb.dres, 1.0)
+
     def _ln(self, x, y, out, stats, prefix, n_masks, seeds, s_out, rot=None, T=None):
         a = K.LnArgs()
         a.dtype = K.dtype_code(self.dt)
@@ -457,6 +476,9 @@ class Seq2SeqEngine:
         a.mean, a.rstd = stats[0].data_ptr(), stats[1].data_ptr()
         self._guard(dbranch)
         a.s_in, a.dout, a.ds, a.dbranch = s_in.data_ptr(), dres_in.data_ptr(), dres_out.data_ptr(), K.ptr(dbranch)
+        if self._dadd_pending:
+            a.dout2 = bb.dadd.data_ptr()
+            self._dadd_pending = False
         a.dgamma_part, a.dbeta_part, a.n_part = bb.ln_part[0].data_ptr(), bb.ln_part[1].data_ptr(), bb.n_part
         if bias_of is not None:
             a.dbranch_part = bb.ln_part[2].data_ptr()
@@ -620,6 +642,7 @@ class Seq2SeqEngine:
             self._side = torch.cuda.Stream(self.device)
         self._side_reads = []
         self.p, self.base_seed = sv["p"], sv["seed"]
+        self._dadd_pending = False
         bf = 0.0 if self.grads_fresh else 1.0
         M, D, L = bb.M, self.D, self.L
         ws = bb.ws
@@ -667,7 +690,7 @@ class Seq2SeqEngine:
         with torch.cuda.stream(self._side):
             red.ready(upto)
 
-    def _attn_block_bwd(self, bb, pre, x_in, qkv, o, lse, st, s1, norm, seeds, T, bf, mask):
+    def _attn_block_bwd(self, bb, pre, x_in, qkv, o, lse, st, s1, norm, seeds, T, bf, mask, last=False):
         """Backward through x1 = LN(x_in + drop(drop(out_linear(attn(x_in))))) (self-attention)."""
         D, ws = self.D, bb.ws
         self._ln_bwd(s1, st, pre + norm, bb.dres, bb.dres, bb.dy, 2, seeds[0:2], bf,
@@ -678,7 +701,7 @@ class Seq2SeqEngine:
                                bb.dqkv[:, :D], bb.dqkv[:, D:2 * D], bb.dqkv[:, 2 * D:], seeds[2], T, bb.B, mask=mask,
                                bias=[(0, 3 * D, self.gb(pre + "self_attn.q_linear.bias", 3))], bf=bf)
         self._dw(bb.dqkv, x_in, pre + "self_attn.q_linear.weight", 3, bf, ws, bias=not fused)
-        self._dx(bb.dqkv, pre + "self_attn.q_linear.weight", 3, bb.dres, 1.0)
+        self._dx_res(bb.dqkv, pre + "self_attn.q_linear.weight", 3, last=last)
 
     def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf, dy=None):
         """Backward through x_out = LN(x_in + drop(FFN(x_in)))."""
@@ -690,7 +713,7 @@ class Seq2SeqEngine:
         fused = self._dx(dy, pre + "ffn.linear2.weight", 1, bb.dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p,
                          colsum=(bb.hpart, self.gb(pre + "ffn.linear1.bias"), bf))
         self._dw(bb.dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws, bias=not fused)
-        self._dx(bb.dh, pre + "ffn.linear1.weight", 1, bb.dres, 1.0)
+        self._dx_res(bb.dh, pre + "ffn.linear1.weight", 1)
 
     def _enc_layer_bwd(self, bb, l, T, bf):
         pre = "encoder.transformer_encoder.%d." % l
@@ -699,7 +722,7 @@ class Seq2SeqEngine:
         x_in = bb.x0 if l == 0 else bb.e_x2[l - 1]
         self._ffn_bwd(bb, pre, bb.e_x1[l], bb.e_h[l], bb.e_s2[l], st[2:4], "norm2", sd("drop2"), bf)
         self._attn_block_bwd(bb, pre, x_in, bb.e_qkv[l], bb.e_o[l], bb.e_lse[l], st[0:2], bb.e_s1[l], "norm1",
-                             (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.e_mask[l])
+                             (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.e_mask[l], last=(l == 0))
 
     def _dec_layer_bwd(self, bb, l, T, bf, first):
         D, ws = self.D, bb.ws
@@ -725,11 +748,11 @@ class Seq2SeqEngine:
                                bias=[(0, D, self.gb(m + "q_linear.bias")), (D, 2 * D, self.gb(m + "k_linear.bias", 2))],
                                bf=bf)
         self._dw(bb.dq, bb.d_x1[l], m + "q_linear.weight", 1, bf, ws, bias=not fused)
-        self._dx(bb.dq, m + "q_linear.weight", 1, bb.dres, 1.0)
+        self._dx_res(bb.dq, m + "q_linear.weight", 1)
         self._dw(bb.dkv, bb.mem, m + "k_linear.weight", 2, bf, ws, bias=not fused)
         self._dx(bb.dkv, m + "k_linear.weight", 2, bb.dmem, 0.0 if first else 1.0)
         self._attn_block_bwd(bb, pre, x_in, bb.d_qkv[l], bb.d_o[l], bb.d_lse[l], st[0:2], bb.d_s1[l], "norm1",
-                             (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.d_mask[l])
+                             (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.d_mask[l], last=(l == 0))
         if grouped:
             self._dw_flush(ws)
 

@@ -475,6 +475,35 @@ def test_layernorm_fwd_global_pe(D, with_x):
     check(stats[0], inp.mean(1), 1e-6, "ln mean")
 
 
+@pytest.mark.parametrize("dt,D", [(torch.bfloat16, 1024), (torch.float32, 128), (torch.bfloat16, 256)])
+def test_layernorm_bwd_dout2_addend(dt, D):
+    """dout2 (a Linear's input gradient in the compute dtype) is added to dout:
+    same result as one f32 gradient dout + dout2."""
+    rows = 64
+    x, y = rnd(rows, D, dtype=dt, seed=130), rnd(rows, D, dtype=dt, seed=131)
+    g, b = 1 + 0.1 * rnd(D, seed=132), 0.1 * rnd(D, seed=133)
+    s = torch.empty(rows, D, dtype=dt, device=DEV)
+    out = torch.empty(rows, D, dtype=dt, device=DEV)
+    stats = torch.empty(2, rows, device=DEV)
+    K.ln_fwd(ln_args(dt, rows, D, x, y, g, b, s, out, stats))
+    g1, g2 = rnd(rows, D, seed=134), rnd(rows, D, dtype=dt, seed=135)
+    res = []
+    for split in (True, False):
+        ds = torch.empty(rows, D, device=DEV)
+        part = torch.empty(2, 4, D, device=DEV)
+        a = ln_args(dt, rows, D, x, y, g, b, None, out, stats)
+        dout = g1 if split else g1 + g2.float()
+        a.s_in, a.dout, a.ds, a.dbranch = s.data_ptr(), dout.data_ptr(), ds.data_ptr(), None
+        a.dgamma_part, a.dbeta_part, a.n_part = part[0].data_ptr(), part[1].data_ptr(), 4
+        if split:
+            a.dout2 = g2.data_ptr()
+        K.ln_bwd(a)
+        torch.cuda.synchronize()
+        res.append((ds, part))
+    check(res[0][0], res[1][0], 1e-6, "ds with dout2")
+    check(res[0][1], res[1][1], 1e-6, "dgamma/dbeta with dout2")
+
+
 @pytest.mark.parametrize("n_masks", [1, 2])
 def test_layernorm_dropout_masks(n_masks):
     dt, rows, D, p = torch.float32, 64, 256, 0.3
