@@ -1,0 +1,13 @@
+# bench A/B of two builds of the library in one box session (the engine is the
+# same): new = libnstl_hip.so, old = libnstl_hip_old.so.  tools/ab_lib.sh [reps]
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+REPS=${1:-2}
+OLD=$GRAFT_REPO_ROOT/neurosync_trainer_lite_amd/libnstl_hip_old.so
+for i in $(seq 1 $REPS); do
+  for arm in new old; do
+    if [ $arm = old ]; then export NSTL_LIB_PATH=$OLD; else unset NSTL_LIB_PATH; fi
+    timeout -k 10 300 python bench.py --no-cpu-baseline --feature-steps 0 --steps 30 2>/dev/null \
+      | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$arm', d['value'], d['ms_per_step'], d['roofline']['achieved'])" || exit 1
+  done
+done
