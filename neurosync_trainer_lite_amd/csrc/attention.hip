@@ -6,16 +6,16 @@
 // Shapes are short: T <= 256 frames, dh = 64.  A whole (batch, head) key/value
 // sequence fits in LDS, so there is no online softmax and no cross-workgroup
 // reduction:
-//   forward : workgroup = (b, h, 64 query rows); each wave 16 rows; scores for
-//             all keys live in MFMA accumulators; exact softmax; P^T is staged
-//             through a per-wave LDS image (one 8-byte write per lane and key
-//             tile) and read back with transpose reads as the A operand of P.V.
-//   backward: workgroup = (b, h); phase 1 waves own 16-key tiles and accumulate
-//             dK, dV over all queries; phase 2 waves own 16-query tiles and
-//             accumulate dQ (scores/probabilities recomputed from the saved LSE).
-// Q/K/V/dO tiles arrive by LDS-DMA (global_load_lds_dwordx4, all in flight
-// together; bank swizzle applied on the source address).  Dropout keep-mask is a
-// counter hash of (b, h, key, query): regenerated in backward, never stored.
+//   forward : workgroup = (b, h, 128 queries); each wave 16 queries; scores for
+//             all keys live in MFMA accumulators (S^T layout); exact softmax;
+//             P feeds P.V straight from the score registers (acc_frag).
+//   backward: dQ kernel (workgroup = b, h, 128 queries) and dK/dV kernel
+//             (b, h, 128 keys); scores recomputed from the saved LSE, dS / P^T
+//             again used as register operands.
+// K/V (forward, dQ) and Q/dO (dK/dV) arrive by LDS-DMA (global_load_lds_dwordx4,
+// bank swizzle applied on the source address); a wave's own 16 rows come from
+// global memory straight into MFMA fragments.  Dropout keep-mask: a counter
+// hash of (b, h, query, key), or the bits the forward stored (mask_bits).
 #include <algorithm>
 
 #include "../../include/nstl.h"
@@ -69,14 +69,14 @@ NSTL_DEV void store_elem(char* base, int64_t e, float v) {
   ((T*)base)[e] = from_f32<T>(v);
 }
 
-// dropout element index: key-major so that (q, q+1) form a hash pair
-NSTL_DEV uint64_t drop_idx(int bh, int T, int q, int k) { return ((uint64_t)bh * T + k) * T + q; }
+// dropout element index: query-major, so the key pair (k, k+1) of one query
+// shares a hash (the MFMA kernels hold 4 consecutive keys of a query per lane)
+NSTL_DEV uint64_t drop_idx(int bh, int T, int q, int k) { return ((uint64_t)bh * T + q) * T + k; }
 
 // Stored keep bits (MFMA path): one 64-bit word per (query tile qt, key tile kt,
-// query % 4) of a head, bit 16 * ((q % 16) / 4) + key % 16 -- exactly the
-// ballot of the keep decisions of one accumulator register r over a wave in
-// the forward / dQ layout (lane 16g + c: query 4g + r, key c).  A head's words
-// are [qt][kt][4] (T*T/64 of them).
+// key % 4) of a head, bit 16 * ((key % 16) / 4) + query % 16 -- the ballot of
+// one score register r over a wave in the forward / dQ layout (lane 16g + c:
+// query c, key 4g + r).  A head's words are [qt][kt][4] (T*T/64 of them).
 NSTL_DEV int64_t mask_word(int bh, int nt, int qt, int kt, int r) {
   return (((int64_t)bh * nt + qt) * nt + kt) * 4 + r;
 }
@@ -90,171 +90,55 @@ NSTL_DEV uint64_t readlane64(uint64_t v, int src) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// four consecutive values of one lane as an 8-byte (bf16) / 16-byte (f32) LDS write
-NSTL_DEV void put4(char* dst, float a, float b, float c, float d, bf16) {
-  *(bf16x4*)dst = (bf16x4){(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+// ---------------------------------------------------------------------------
+// Register-operand layout.  Scores are computed TRANSPOSED where the next
+// product reduces over them: mma16(acc, X, Y) gives lane (g, c = lane & 15)
+// the elements (row 4g + r, column c), so with X = keys and Y = queries a lane
+// owns keys 16kt + 4g + r of ITS query c -- exactly what it must supply as the
+// A operand (row c) of a product that sums over keys.  Two score registers
+// (tiles 2j, 2j+1) form one A fragment whose 8 reduction slots are the keys
+// {32j + 4g + 0..3, 32j + 16 + 4g + 0..3}; the B operand is read from its LDS
+// image in that same order (frag_col2), so P / dS never go through LDS.
+template <typename T> NSTL_DEV typename FragT<T>::type acc_frag(const f32x4& a, const f32x4& b);
+template <> NSTL_DEV bf16x8 acc_frag<bf16>(const f32x4& a, const f32x4& b) {
+  return (bf16x8){(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
 }
-NSTL_DEV void put4(char* dst, float a, float b, float c, float d, float) {
-  *(f32x4*)dst = (f32x4){a, b, c, d};
+template <> NSTL_DEV f32x8 acc_frag<float>(const f32x4& a, const f32x4& b) {
+  return (f32x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-// ----------------------------------------------------------------------------
-// Forward: one workgroup of FWD_NT/64 waves per (b, h) and 16*FWD_NT/64 queries
-// (all of T=128), so K and V are staged once per (b, h); each wave owns 16
-// query rows.
-constexpr int FWD_NT = 512, FWD_QB = 16 * FWD_NT / 64;
+// column col16 + (lane & 15) of an image whose rows are the reduction index, rows
+// r0 + 4g + 0..3 then r0 + 16 + 4g + 0..3 (acc_frag's order): two gfx950
+// transpose reads (bf16) / eight element reads (f32)
+template <class Img>
+NSTL_DEV void frag_col2(bf16x8& f, const char* img, int col16, int r0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int byte = (col16 + 4 * p) * 2;
+  const lds_char* base = (const lds_char*)img;
+  s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(base + Img::off(r0 + 4 * g + q, byte)));
+  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(base + Img::off(r0 + 16 + 4 * g + q, byte)));
+  const bf16x4 b0 = __builtin_bit_cast(bf16x4, v0), b1 = __builtin_bit_cast(bf16x4, v1);
+  f = (bf16x8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+}
+template <class Img>
+NSTL_DEV void frag_col2(f32x8& f, const char* img, int col16, int r0, int lane) {
+  const int g = lane >> 4, byte = (col16 + (lane & 15)) * 4;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = *(const float*)(img + Img::off(r0 + 4 * g + (j & 3) + 16 * (j >> 2), byte));
+}
 
 template <typename T>
-__global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
-  typedef typename FragT<T>::type Frag;
-  constexpr int ESZ = (int)sizeof(T);
-  constexpr int RBK = DH * ESZ;   // 128 (bf16) / 256 (f32)
-  constexpr int RBP = 16 * ESZ;   // P^T image rows: 16 queries
-  typedef ImgK<RBK> Img;
-  typedef ImgPlain<RBP> ImgP;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int T_ = p.T, nkt = T_ / 16;
-  char* Kimg = smem;
-  char* Vimg = Kimg + T_ * RBK;
-  char* Qimg = Vimg + T_ * RBK;
-  char* Pimg = Qimg + FWD_QB * RBK;
-
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  const int qb0 = blockIdx.x * FWD_QB;
-  const int nq = min(FWD_QB, T_ - qb0);
-  const int64_t tok0 = (int64_t)b * T_;
-  constexpr int NW = FWD_NT / 64;
-
-  dma_rows<RBK, NW>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
-  dma_rows<RBK, NW>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
-  dma_rows<RBK, NW>(Qimg, p.q + ((tok0 + qb0) * p.q_ld + h * DH) * ESZ, p.q_ld * ESZ, nq, w, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const int q0 = w * 16;  // local row base of this wave
-  if (q0 < nq) {
-    Frag fq[2];
-    frag_row<Img>(fq[0], Qimg, q0 + (lane & 15), 8 * g);
-    frag_row<Img>(fq[1], Qimg, q0 + (lane & 15), 32 + 8 * g);
-    f32x4 s[16];
-#pragma unroll
-    for (int kt = 0; kt < 16; ++kt) {
-      s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      if (kt < nkt) {
-        Frag fk0, fk1;
-        frag_row<Img>(fk0, Kimg, kt * 16 + (lane & 15), 8 * g);
-        frag_row<Img>(fk1, Kimg, kt * 16 + (lane & 15), 32 + 8 * g);
-        mma16(s[kt], fq[0], fk0);
-        mma16(s[kt], fq[1], fk1);
-      }
-    }
-    const float c2 = p.scale * LOG2E;
-    float mx[4], sum[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float m = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 16; ++kt)
-        if (kt < nkt) m = fmaxf(m, s[kt][r]);
-      m = fmaxf(m, __shfl_xor(m, 1));
-      m = fmaxf(m, __shfl_xor(m, 2));
-      m = fmaxf(m, __shfl_xor(m, 4));
-      m = fmaxf(m, __shfl_xor(m, 8));
-      mx[r] = m;
-      float sm = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 16; ++kt)
-        if (kt < nkt) {
-          const float e = exp2f((s[kt][r] - m) * c2);
-          s[kt][r] = e;
-          sm += e;
-        }
-      sm += __shfl_xor(sm, 1);
-      sm += __shfl_xor(sm, 2);
-      sm += __shfl_xor(sm, 4);
-      sm += __shfl_xor(sm, 8);
-      sum[r] = sm;
-    }
-    // dropout + P^T (unnormalised) into this wave's image [T keys][16 rows]
-    char* Pw = Pimg + w * max(T_, 64) * RBP;  // also holds the 16 x 64 O tile
-    const int qrow = qb0 + q0 + 4 * g;  // this lane's first query (even)
-    uint32_t mlo = 0, mhi = 0;          // lane kt*4 + r: keep bits of (kt, r)
-#pragma unroll
-    for (int kt = 0; kt < 16; ++kt) {
-      if (kt < nkt) {
-        const int key = kt * 16 + (lane & 15);
-        float v0 = s[kt][0], v1 = s[kt][1], v2 = s[kt][2], v3 = s[kt][3];
-        if (p.thresh) {
-          bool k0, k1, k2, k3;
-          const uint64_t idx = drop_idx(bh, T_, qrow, key);
-          nstl_keep2(p.seed, idx, p.thresh, k0, k1);
-          nstl_keep2(p.seed, idx + 2, p.thresh, k2, k3);
-          v0 = k0 ? v0 * p.inv_keep : 0.f;
-          v1 = k1 ? v1 * p.inv_keep : 0.f;
-          v2 = k2 ? v2 * p.inv_keep : 0.f;
-          v3 = k3 ? v3 * p.inv_keep : 0.f;
-          if (p.mask) {  // the 4 ballots (wave-uniform) into lanes kt*4 .. +3
-            const uint64_t b[4] = {__ballot(k0), __ballot(k1), __ballot(k2), __ballot(k3)};
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (lane == kt * 4 + r) {
-                mlo = (uint32_t)b[r];
-                mhi = (uint32_t)(b[r] >> 32);
-              }
-          }
-        }
-        put4(Pw + key * RBP + 4 * g * ESZ, v0, v1, v2, v3, T());
-      }
-    }
-    if (p.thresh && p.mask && lane < nkt * 4)
-      p.mask[mask_word(bh, nkt, (qb0 + q0) >> 4, 0, 0) + lane] = ((uint64_t)mhi << 32) | mlo;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    f32x4 o[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < nkt / 2; ++ks) {
-      Frag fp;
-      frag_col<ImgP>(fp, Pw, 0, ks * 32, lane);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        Frag fv;
-        frag_col<Img>(fv, Vimg, dt * 16, ks * 32, lane);
-        mma16(o[dt], fp, fv);
-      }
-    }
-    // O: stage 16 x 64 through the (now free) P^T image, store 16-byte rows
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    char* Ow = Pw;  // [16 rows][64 d] of T = 64 * RBP bytes
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float inv = 1.f / sum[r];
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        *(T*)(Ow + (4 * g + r) * RBK + (dt * 16 + (lane & 15)) * ESZ) = from_f32<T>(o[dt][r] * inv);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    constexpr int CPR = RBK / 16;
-#pragma unroll
-    for (int c = lane; c < 16 * CPR; c += 64) {
-      const int row = c / CPR, ch = c % CPR;
-      const uint4 val = *(const uint4*)(Ow + row * RBK + ch * 16);
-      *(uint4*)(p.o + ((tok0 + qb0 + q0 + row) * p.o_ld + h * DH) * ESZ + ch * 16) = val;
-    }
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        p.lse[(int64_t)bh * T_ + qb0 + q0 + 4 * g + r] = mx[r] * p.scale + logf(sum[r]);
-    }
-  }
+NSTL_DEV void gload_frag(typename FragT<T>::type& f, const T* row, int k0);
+template <>
+NSTL_DEV void gload_frag<bf16>(bf16x8& f, const bf16* row, int k0) {
+  f = *(const bf16x8*)(row + k0);
 }
-
-// rotate a (row t, col d) accumulator element back by -theta (RoPE^T)
-NSTL_DEV float rope_back(float v, int t, int d, const float* cs, const float* sn) {
-  const float partner = __shfl_xor(v, 1);
-  const float c = cs[t * (DH / 2) + (d >> 1)], s = sn[t * (DH / 2) + (d >> 1)];
-  return (d & 1) ? (v * c - partner * s) : (v * c + partner * s);
+template <>
+NSTL_DEV void gload_frag<float>(f32x8& f, const float* row, int k0) {
+  const f32x4 lo = *(const f32x4*)(row + k0), hi = *(const f32x4*)(row + k0 + 4);
+  f = (f32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
 // A wave's 16 x 64 result tile (lane: rows 4g+r, column dt*16 + (lane&15)) to
@@ -278,6 +162,144 @@ NSTL_DEV void store_tile16x64(const float (&v)[4][4], char* scr, char* gbase, in
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// ----------------------------------------------------------------------------
+// Forward: one workgroup of 8 waves per (b, h) and 128 queries (all of T=128),
+// so K and V are staged once per (b, h) by LDS-DMA; each wave owns 16 queries,
+// loaded straight from global memory as MFMA fragments.  S^T = K Q^T in
+// accumulators, exact softmax over the keys (a lane holds 4*T/16 of its
+// query's scores; the rest are in the lanes of the same column, 2 shuffles),
+// dropout, then O = P V with P taken from the score registers (acc_frag).
+constexpr int FWD_NT = 512, FWD_QB = 16 * FWD_NT / 64;
+
+template <typename T>
+__global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
+  typedef typename FragT<T>::type Frag;
+  constexpr int ESZ = (int)sizeof(T);
+  constexpr int RBK = DH * ESZ;   // 128 (bf16) / 256 (f32)
+  typedef ImgK<RBK> Img;
+  constexpr int NW = FWD_NT / 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int T_ = p.T, nkt = T_ / 16;
+  char* Kimg = smem;
+  char* Vimg = Kimg + T_ * RBK;
+  char* Ostage = Vimg + T_ * RBK;  // [NW][16][RBK]
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int qb0 = blockIdx.x * FWD_QB;
+  const int nq = min(FWD_QB, T_ - qb0);
+  const int64_t tok0 = (int64_t)b * T_;
+
+  dma_rows<RBK, NW>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, NW>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
+  const int q0 = qb0 + w * 16;  // this wave's first query
+  const bool act = w * 16 < nq;
+  Frag fq[2];
+  if (act) {
+    const T* qrow = (const T*)p.q + (tok0 + q0 + c) * p.q_ld + h * DH;
+    gload_frag<T>(fq[0], qrow, 8 * g);
+    gload_frag<T>(fq[1], qrow, 32 + 8 * g);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!act) return;
+
+  // s[kt][r] = score(query q0 + c, key 16kt + 4g + r)
+  f32x4 s[16];
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt) {
+    s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (kt < nkt) {
+      Frag fk;
+      frag_row<Img>(fk, Kimg, kt * 16 + c, 8 * g);
+      mma16(s[kt], fk, fq[0]);
+      frag_row<Img>(fk, Kimg, kt * 16 + c, 32 + 8 * g);
+      mma16(s[kt], fk, fq[1]);
+    }
+  }
+  const float c2 = p.scale * LOG2E;
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt)
+    if (kt < nkt) m = fmaxf(fmaxf(fmaxf(m, s[kt][0]), fmaxf(s[kt][1], s[kt][2])), s[kt][3]);
+  m = fmaxf(m, __shfl_xor(m, 16));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt)
+    if (kt < nkt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = exp2f((s[kt][r] - m) * c2);
+        s[kt][r] = e;
+        sum += e;
+      }
+    }
+  sum += __shfl_xor(sum, 16);
+  sum += __shfl_xor(sum, 32);
+  if (p.thresh) {
+    // dropout on P: keys (r, r+1) of this lane's query share one hash
+    const int q = q0 + c;
+    uint32_t mlo = 0, mhi = 0;  // lane kt*4 + r: keep bits of (kt, r)
+#pragma unroll
+    for (int kt = 0; kt < 16; ++kt) {
+      if (kt < nkt) {
+        bool k[4];
+        const uint64_t idx = drop_idx(bh, T_, q, kt * 16 + 4 * g);
+        nstl_keep2(p.seed, idx, p.thresh, k[0], k[1]);
+        nstl_keep2(p.seed, idx + 2, p.thresh, k[2], k[3]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[kt][r] = k[r] ? s[kt][r] * p.inv_keep : 0.f;
+        if (p.mask) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint64_t bal = __ballot(k[r]);
+            if (lane == kt * 4 + r) {
+              mlo = (uint32_t)bal;
+              mhi = (uint32_t)(bal >> 32);
+            }
+          }
+        }
+      }
+    }
+    if (p.mask && lane < nkt * 4) p.mask[mask_word(bh, nkt, q0 >> 4, 0, 0) + lane] = ((uint64_t)mhi << 32) | mlo;
+  }
+  // O = P V over 32-key chunks: o[dt][r] = O(query q0 + 4g + r, d = 16dt + c)
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (2 * j < nkt) {
+      const Frag fp = acc_frag<T>(s[2 * j], s[2 * j + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        Frag fv;
+        frag_col2<Img>(fv, Vimg, dt * 16, 32 * j, lane);
+        mma16(o[dt], fp, fv);
+      }
+    }
+  }
+  // normalise (query 4g + r's sum is in lane 4g + r) and store 16-byte rows
+  float ov[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float inv = 1.f / __shfl(sum, 4 * g + r);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) ov[dt][r] = o[dt][r] * inv;
+  }
+  store_tile16x64<T>(ov, Ostage + w * 16 * RBK, p.o + ((tok0 + q0) * p.o_ld + h * DH) * ESZ, p.o_ld, lane);
+  if (g == 0) p.lse[(int64_t)bh * T_ + q0 + c] = m * p.scale + logf(sum);
+}
+
+// rotate a (row t, col d) accumulator element back by -theta (RoPE^T)
+NSTL_DEV float rope_back(float v, int t, int d, const float* cs, const float* sn) {
+  const float partner = __shfl_xor(v, 1);
+  const float c = cs[t * (DH / 2) + (d >> 1)], s = sn[t * (DH / 2) + (d >> 1)];
+  return (d & 1) ? (v * c - partner * s) : (v * c + partner * s);
+}
+
 // Bias gradients fused into the backward stores: column sums of a wave's stored
 // 16 x 64 tile (rounded to T, as colsum() of the stored tensor would see it) go
 // to red[w][64]; the LAST wave to finish (an LDS arrival counter, no barrier,
@@ -287,12 +309,12 @@ template <typename T>
 NSTL_DEV void wave_colsum16x64(const float (&v)[4][4], float* red, int w, int lane) {
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    float c = 0.f;
+    float cs = 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) c += to_f32(from_f32<T>(v[dt][r]));
-    c += __shfl_xor(c, 16);
-    c += __shfl_xor(c, 32);
-    if (lane < 16) red[w * 64 + dt * 16 + lane] = c;
+    for (int r = 0; r < 4; ++r) cs += to_f32(from_f32<T>(v[dt][r]));
+    cs += __shfl_xor(cs, 16);
+    cs += __shfl_xor(cs, 32);
+    if (lane < 16) red[w * 64 + dt * 16 + lane] = cs;
   }
 }
 NSTL_DEV bool last_to_arrive(unsigned* cnt, int nw, int lane) {
@@ -302,33 +324,22 @@ NSTL_DEV bool last_to_arrive(unsigned* cnt, int nw, int lane) {
   return __shfl(old, 0) == (unsigned)(nw - 1);
 }
 NSTL_DEV void wave_sum_out(const float* red, int nw, float* out, int lane) {
-  float c = 0.f;
-  for (int k = 0; k < nw; ++k) c += red[k * 64 + lane];
-  out[lane] = c;
+  float cs = 0.f;
+  for (int k = 0; k < nw; ++k) cs += red[k * 64 + lane];
+  out[lane] = cs;
 }
 
 // ---------------------------------------------------------------------------
 // Backward, as two kernels (8 waves, 128 rows: all of T=128, so each (b, h)
-// operand is staged once) with ~48 KB LDS, 3 resident per CU:
+// operand is staged once):
 //   attn_bwd_dq : workgroup = (b, h, 128 queries); K, V of (b, h) in LDS; a wave
-//                 owns 16 queries: D = rowsum(dO * O) (also written to p.dsum
-//                 for the second kernel), dS over all keys, dQ = dS K (RoPE^T).
+//                 owns 16 queries (fragments from global): D = rowsum(dO * O)
+//                 (also written to p.dsum for the second kernel), S^T and dP^T
+//                 over all keys, dS^T in registers -> dQ = dS K (RoPE^T).
 //   attn_bwd_dkv: workgroup = (b, h, 128 keys); Q, dO of (b, h) in LDS; a wave
-//                 owns 16 keys: dV = P_drop^T dO, dK = dS^T Q (RoPE^T).
-// A wave's own rows come straight from global memory into MFMA fragments.
+//                 owns 16 keys: S and dP (query rows), P^T / dS^T in registers
+//                 -> dV = P_drop^T dO, dK = dS^T Q (RoPE^T).
 constexpr int BWD_NT = 512, BWD_ROWS = 16 * BWD_NT / 64;  // 8 waves, 128 rows
-
-template <typename T>
-NSTL_DEV void gload_frag(typename FragT<T>::type& f, const T* row, int k0);
-template <>
-NSTL_DEV void gload_frag<bf16>(bf16x8& f, const bf16* row, int k0) {
-  f = *(const bf16x8*)(row + k0);
-}
-template <>
-NSTL_DEV void gload_frag<float>(f32x8& f, const float* row, int k0) {
-  const f32x4 lo = *(const f32x4*)(row + k0), hi = *(const f32x4*)(row + k0 + 4);
-  f = (f32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
 
 template <typename T>
 __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
@@ -336,26 +347,27 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
   constexpr int ESZ = (int)sizeof(T);
   constexpr int RBK = DH * ESZ;
   typedef ImgK<RBK> Img;
-  constexpr int RBS = 16 * ESZ;
-  typedef ImgPlain<RBS> ImgS;
+  constexpr int NW = BWD_NT / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int T_ = p.T, nkt = T_ / 16;
   char* Kimg = smem;
   char* Vimg = Kimg + T_ * RBK;
-  char* scratch = Vimg + T_ * RBK;
+  char* scratch = Vimg + T_ * RBK;                 // [NW][16][RBK] output staging
+  float* red = (float*)(scratch + NW * 16 * RBK);  // [NW][64] bias partials
+  unsigned* arrived = (unsigned*)(red + 2 * NW * 64);
 
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int64_t tok0 = (int64_t)b * T_;
   const int q0 = blockIdx.x * BWD_ROWS + w * 16;
-  dma_rows<RBK, BWD_NT / 64>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
-  dma_rows<RBK, BWD_NT / 64>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, NW>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, NW>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
   const bool act = q0 < T_;
   Frag fq[2], fo[2];
-  float lq[4], dqv[4];
+  float lq = 0.f, dqv = 0.f;  // LSE (log2 units) and D of this lane's query q0 + c
   if (act) {
-    const int qr = q0 + (lane & 15);
+    const int qr = q0 + c;
     const T* qrow = (const T*)p.q + (tok0 + qr) * p.q_ld + h * DH;
     const T* drow = (const T*)p.dout + (tok0 + qr) * p.dout_ld + h * DH;
     const T* orow = (const T*)p.o + (tok0 + qr) * p.o_ld + h * DH;
@@ -366,7 +378,6 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
       gload_frag<T>(fo[u], drow, 32 * u + 8 * g);
       gload_frag<T>(oo[u], orow, 32 * u + 8 * g);
     }
-    // D for row (lane & 15): 16 of its products per lane, then across the 4 groups
     float dpart = 0.f;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -375,14 +386,9 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
     dpart += __shfl_xor(dpart, 16);
     dpart += __shfl_xor(dpart, 32);
     if (g == 0) p.dsum[(int64_t)bh * T_ + qr] = dpart;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      dqv[r] = __shfl(dpart, 4 * g + r);
-      lq[r] = p.lse[(int64_t)bh * T_ + q0 + 4 * g + r] * LOG2E;
-    }
+    dqv = dpart;
+    lq = p.lse[(int64_t)bh * T_ + qr] * LOG2E;
   }
-  float* red = (float*)(scratch + (BWD_NT / 64) * 2 * 32 * RBS);  // [8 waves][64] bias partials
-  unsigned* arrived = (unsigned*)(red + 2 * (BWD_NT / 64) * 64);
   if (tid == 0) *arrived = 0u;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -390,13 +396,12 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
   if (!act) {
     if (bias_row) {
       red[w * 64 + lane] = 0.f;
-      if (last_to_arrive(arrived, BWD_NT / 64, lane)) wave_sum_out(red, BWD_NT / 64, bias_row + h * DH, lane);
+      if (last_to_arrive(arrived, NW, lane)) wave_sum_out(red, NW, bias_row + h * DH, lane);
     }
     return;
   }
 
   const float c2 = p.scale * LOG2E;
-  char* S2 = scratch + w * 2 * 32 * RBS;
   // stored keep bits of this wave's 16 queries: lane kt*4 + r holds word (kt, r)
   const bool use_mask = p.thresh && p.mask;
   uint64_t mword = 0;
@@ -404,52 +409,46 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
   f32x4 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int kc = 0; kc < nkt / 2; ++kc) {
+  for (int j = 0; j < nkt / 2; ++j) {  // 32-key chunks
+    f32x4 dsv[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int kt = kc * 2 + u;
-      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      const int kt = 2 * j + u;
+      f32x4 sc = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
       Frag fb;
-      frag_row<Img>(fb, Kimg, kt * 16 + (lane & 15), 8 * g);
-      mma16(s, fq[0], fb);
-      frag_row<Img>(fb, Kimg, kt * 16 + (lane & 15), 32 + 8 * g);
-      mma16(s, fq[1], fb);
-      frag_row<Img>(fb, Vimg, kt * 16 + (lane & 15), 8 * g);
-      mma16(dp, fo[0], fb);
-      frag_row<Img>(fb, Vimg, kt * 16 + (lane & 15), 32 + 8 * g);
-      mma16(dp, fo[1], fb);
-      // accumulator: row = query (4g + r), col = key
-      const int key = kt * 16 + (lane & 15);
+      frag_row<Img>(fb, Kimg, kt * 16 + c, 8 * g);
+      mma16(sc, fb, fq[0]);
+      frag_row<Img>(fb, Kimg, kt * 16 + c, 32 + 8 * g);
+      mma16(sc, fb, fq[1]);
+      frag_row<Img>(fb, Vimg, kt * 16 + c, 8 * g);
+      mma16(dp, fb, fo[0]);
+      frag_row<Img>(fb, Vimg, kt * 16 + c, 32 + 8 * g);
+      mma16(dp, fb, fo[1]);
+      // sc[r] / dp[r]: S^T / dP^T at (key 16kt + 4g + r, query q0 + c)
       bool keep[4] = {true, true, true, true};
       if (use_mask) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) keep[r] = (readlane64(mword, kt * 4 + r) >> lane) & 1;
       } else if (p.thresh) {
-        const uint64_t idx = drop_idx(bh, T_, q0 + 4 * g, key);
+        const uint64_t idx = drop_idx(bh, T_, q0 + c, kt * 16 + 4 * g);
         nstl_keep2(p.seed, idx, p.thresh, keep[0], keep[1]);
         nstl_keep2(p.seed, idx + 2, p.thresh, keep[2], keep[3]);
       }
-      float ds[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(s[r] * c2 - lq[r]);
+        const float pv = exp2f(sc[r] * c2 - lq);
         float dpd = dp[r];
         if (p.thresh) dpd = keep[r] ? dpd * p.inv_keep : 0.f;
-        ds[r] = pv * (dpd - dqv[r]);
+        dsv[u][r] = pv * (dpd - dqv);
       }
-      // transposed image [key][query]
-      put4(S2 + (u * 16 + (lane & 15)) * RBS + 4 * g * ESZ, ds[0], ds[1], ds[2], ds[3], T());
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    Frag fa;
-    frag_col<ImgS>(fa, S2, 0, 0, lane);  // A(i = query, r = key)
+    const Frag fa = acc_frag<T>(dsv[0], dsv[1]);  // dS, row = query q0 + c
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       Frag fb;
-      frag_col<Img>(fb, Kimg, dt * 16, kc * 32, lane);
+      frag_col2<Img>(fb, Kimg, dt * 16, 32 * j, lane);
       mma16(dq[dt], fa, fb);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   float vq[4][4];
 #pragma unroll
@@ -457,16 +456,16 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
     const int q = q0 + 4 * g + r;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const int d = dt * 16 + (lane & 15);
+      const int d = dt * 16 + c;
       float x = dq[dt][r] * p.scale;
       if (p.rope_q) x = rope_back(x, q, d, p.rope_cos, p.rope_sin);
       vq[dt][r] = x;
     }
   }
-  store_tile16x64<T>(vq, S2, p.dq + ((tok0 + q0) * p.dq_ld + h * DH) * ESZ, p.dq_ld, lane);
+  store_tile16x64<T>(vq, scratch + w * 16 * RBK, p.dq + ((tok0 + q0) * p.dq_ld + h * DH) * ESZ, p.dq_ld, lane);
   if (bias_row) {
     wave_colsum16x64<T>(vq, red, w, lane);
-    if (last_to_arrive(arrived, BWD_NT / 64, lane)) wave_sum_out(red, BWD_NT / 64, bias_row + h * DH, lane);
+    if (last_to_arrive(arrived, NW, lane)) wave_sum_out(red, NW, bias_row + h * DH, lane);
   }
 }
 
@@ -476,23 +475,24 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
   constexpr int ESZ = (int)sizeof(T);
   constexpr int RBK = DH * ESZ;
   typedef ImgK<RBK> Img;
-  constexpr int RBS = 16 * ESZ;
-  typedef ImgPlain<RBS> ImgS;
+  constexpr int NW = BWD_NT / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int T_ = p.T, nkt = T_ / 16;
   char* Qimg = smem;
   char* Dimg = Qimg + T_ * RBK;
   float* lse_s = (float*)(Dimg + T_ * RBK);
   float* dq_s = lse_s + T_;
-  char* scratch = (char*)(dq_s + T_);
+  char* scratch = (char*)(dq_s + T_);              // [NW][16][RBK] output staging
+  float* red = (float*)(scratch + NW * 16 * RBK);  // [2][NW][64] bias partials
+  unsigned* arrived = (unsigned*)(red + 2 * NW * 64);
 
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int64_t tok0 = (int64_t)b * T_;
   const int k0 = blockIdx.x * BWD_ROWS + w * 16;
-  dma_rows<RBK, BWD_NT / 64>(Qimg, p.q + (tok0 * p.q_ld + h * DH) * ESZ, p.q_ld * ESZ, T_, w, lane);
-  dma_rows<RBK, BWD_NT / 64>(Dimg, p.dout + (tok0 * p.dout_ld + h * DH) * ESZ, p.dout_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, NW>(Qimg, p.q + (tok0 * p.q_ld + h * DH) * ESZ, p.q_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, NW>(Dimg, p.dout + (tok0 * p.dout_ld + h * DH) * ESZ, p.dout_ld * ESZ, T_, w, lane);
   for (int i = tid; i < T_; i += BWD_NT) {
     lse_s[i] = p.lse[(int64_t)bh * T_ + i] * LOG2E;
     dq_s[i] = p.dsum[(int64_t)bh * T_ + i];
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
   const bool act = k0 < T_;
   Frag fk[2], fv[2];
   if (act) {
-    const int kr = k0 + (lane & 15);
+    const int kr = k0 + c;
     const T* krow = (const T*)p.k + (tok0 + kr) * p.k_ld + h * DH;
     const T* vrow = (const T*)p.v + (tok0 + kr) * p.v_ld + h * DH;
 #pragma unroll
@@ -509,87 +509,73 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
       gload_frag<T>(fv[u], vrow, 32 * u + 8 * g);
     }
   }
-  float* red = (float*)(scratch + (BWD_NT / 64) * 2 * 32 * RBS);  // [2][8 waves][64] bias partials
-  unsigned* arrived = (unsigned*)(red + 2 * (BWD_NT / 64) * 64);
   if (tid == 0) *arrived = 0u;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  constexpr int NWB = BWD_NT / 64;
   float* bias_row = p.dbias ? p.dbias + (int64_t)(b * gridDim.x + blockIdx.x) * 3 * p.H * DH : nullptr;
   if (!act) {
     if (bias_row) {
       red[w * 64 + lane] = 0.f;
-      red[NWB * 64 + w * 64 + lane] = 0.f;
-      if (last_to_arrive(arrived, NWB, lane)) {
-        wave_sum_out(red, NWB, bias_row + p.H * DH + h * DH, lane);
-        wave_sum_out(red + NWB * 64, NWB, bias_row + 2 * p.H * DH + h * DH, lane);
+      red[NW * 64 + w * 64 + lane] = 0.f;
+      if (last_to_arrive(arrived, NW, lane)) {
+        wave_sum_out(red, NW, bias_row + p.H * DH + h * DH, lane);
+        wave_sum_out(red + NW * 64, NW, bias_row + 2 * p.H * DH + h * DH, lane);
       }
     }
     return;
   }
 
   const float c2 = p.scale * LOG2E;
-  char* S1 = scratch + w * 2 * 32 * RBS;  // [32 rows][16] images
   // stored keep bits for this wave's 16 keys: lane 4*qt + r holds word (qt, k0/16, r)
   const bool use_mask = p.thresh && p.mask;
   uint64_t mword = 0;
   if (use_mask && (lane >> 2) < nkt) mword = p.mask[mask_word(bh, nkt, lane >> 2, k0 >> 4, lane & 3)];
-  char* S2 = S1 + 32 * RBS;
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int qc = 0; qc < nkt / 2; ++qc) {
+  for (int j = 0; j < nkt / 2; ++j) {  // 32-query chunks
+    f32x4 pdv[2], dsv[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int qt = qc * 2 + u;
+      const int qt = 2 * j + u;
       f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
       Frag fb;
-      frag_row<Img>(fb, Qimg, qt * 16 + (lane & 15), 8 * g);
-      mma16(st, fk[0], fb);
-      frag_row<Img>(fb, Qimg, qt * 16 + (lane & 15), 32 + 8 * g);
-      mma16(st, fk[1], fb);
-      frag_row<Img>(fb, Dimg, qt * 16 + (lane & 15), 8 * g);
-      mma16(dpt, fv[0], fb);
-      frag_row<Img>(fb, Dimg, qt * 16 + (lane & 15), 32 + 8 * g);
-      mma16(dpt, fv[1], fb);
-      // accumulator: row = key (4g + r), col = query
-      const int q = qt * 16 + (lane & 15);
-      const float lq = lse_s[q], dqv = dq_s[q];
-      // query q's bits for keys k0 + 4g .. +3: 4 consecutive bits of word (qt, q % 4)
+      frag_row<Img>(fb, Qimg, qt * 16 + c, 8 * g);
+      mma16(st, fb, fk[0]);
+      frag_row<Img>(fb, Qimg, qt * 16 + c, 32 + 8 * g);
+      mma16(st, fb, fk[1]);
+      frag_row<Img>(fb, Dimg, qt * 16 + c, 8 * g);
+      mma16(dpt, fb, fv[0]);
+      frag_row<Img>(fb, Dimg, qt * 16 + c, 32 + 8 * g);
+      mma16(dpt, fb, fv[1]);
+      // st[r] / dpt[r]: S / dP at (query 16qt + 4g + r, key k0 + c)
+      // its keep bits: 4 consecutive bits of word (qt, k0/16, key % 4)
       uint32_t nib = 0;
-      if (use_mask) nib = (uint32_t)(shfl64(mword, 4 * qt + (lane & 3)) >> (16 * ((lane & 15) >> 2) + 4 * g));
-      float pd[4], ds[4];
+      if (use_mask) nib = (uint32_t)(shfl64(mword, 4 * qt + (lane & 3)) >> (16 * (c >> 2) + 4 * g));
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 4 * g + r;
-        const float pv = exp2f(st[r] * c2 - lq);
+        const int q = qt * 16 + 4 * g + r;
+        const float pv = exp2f(st[r] * c2 - lse_s[q]);
         float pdr = pv, dpd = dpt[r];
         if (p.thresh) {
-          const bool keep = use_mask ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, key), p.thresh);
+          const bool keep = use_mask ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
           pdr = keep ? pv * p.inv_keep : 0.f;
           dpd = keep ? dpd * p.inv_keep : 0.f;
         }
-        pd[r] = pdr;
-        ds[r] = pv * (dpd - dqv);
+        pdv[u][r] = pdr;
+        dsv[u][r] = pv * (dpd - dq_s[q]);
       }
-      // transposed images [query][key]: this lane's 4 keys are contiguous
-      const int qr = u * 16 + (lane & 15);
-      put4(S1 + qr * RBS + 4 * g * ESZ, pd[0], pd[1], pd[2], pd[3], T());
-      put4(S2 + qr * RBS + 4 * g * ESZ, ds[0], ds[1], ds[2], ds[3], T());
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    Frag fa1, fa2;
-    frag_col<ImgS>(fa1, S1, 0, 0, lane);  // A(i = key, r = query)
-    frag_col<ImgS>(fa2, S2, 0, 0, lane);
+    const Frag fa1 = acc_frag<T>(pdv[0], pdv[1]);  // P_drop^T, row = key k0 + c
+    const Frag fa2 = acc_frag<T>(dsv[0], dsv[1]);  // dS^T
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       Frag fb;
-      frag_col<Img>(fb, Dimg, dt * 16, qc * 32, lane);
+      frag_col2<Img>(fb, Dimg, dt * 16, 32 * j, lane);
       mma16(dv[dt], fa1, fb);
-      frag_col<Img>(fb, Qimg, dt * 16, qc * 32, lane);
+      frag_col2<Img>(fb, Qimg, dt * 16, 32 * j, lane);
       mma16(dk[dt], fa2, fb);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   float vk[4][4], vv[4][4];
 #pragma unroll
@@ -597,31 +583,32 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
     const int key = k0 + 4 * g + r;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const int d = dt * 16 + (lane & 15);
+      const int d = dt * 16 + c;
       float x = dk[dt][r] * p.scale;
       if (p.rope_k) x = rope_back(x, key, d, p.rope_cos, p.rope_sin);
       vk[dt][r] = x;
       vv[dt][r] = dv[dt][r];
     }
   }
-  store_tile16x64<T>(vk, S1, p.dk + ((tok0 + k0) * p.dk_ld + h * DH) * ESZ, p.dk_ld, lane);
-  store_tile16x64<T>(vv, S1, p.dv + ((tok0 + k0) * p.dv_ld + h * DH) * ESZ, p.dv_ld, lane);
+  char* scr = scratch + w * 16 * RBK;
+  store_tile16x64<T>(vk, scr, p.dk + ((tok0 + k0) * p.dk_ld + h * DH) * ESZ, p.dk_ld, lane);
+  store_tile16x64<T>(vv, scr, p.dv + ((tok0 + k0) * p.dv_ld + h * DH) * ESZ, p.dv_ld, lane);
   if (bias_row) {
     wave_colsum16x64<T>(vk, red, w, lane);
-    wave_colsum16x64<T>(vv, red + NWB * 64, w, lane);
-    if (last_to_arrive(arrived, NWB, lane)) {
-      wave_sum_out(red, NWB, bias_row + p.H * DH + h * DH, lane);
-      wave_sum_out(red + NWB * 64, NWB, bias_row + 2 * p.H * DH + h * DH, lane);
+    wave_colsum16x64<T>(vv, red + NW * 64, w, lane);
+    if (last_to_arrive(arrived, NW, lane)) {
+      wave_sum_out(red, NW, bias_row + p.H * DH + h * DH, lane);
+      wave_sum_out(red + NW * 64, NW, bias_row + 2 * p.H * DH + h * DH, lane);
     }
   }
 }
 
-size_t fwd_lds_bytes(int T, int esz) {
-  return (size_t)(2 * T + FWD_QB) * DH * esz + (FWD_NT / 64) * (size_t)std::max(T, 64) * 16 * esz;
+size_t fwd_lds_bytes(int T, int esz) {  // K, V images + per-wave output staging
+  return (size_t)2 * T * DH * esz + (FWD_NT / 64) * 16 * DH * (size_t)esz;
 }
 size_t bwd_lds_bytes(int T, int esz) {  // either backward kernel (+ 2 x [8][64] f32 bias partials + counter)
-  return (size_t)2 * T * DH * esz + 2 * T * 4 + (BWD_NT / 64) * 2 * 32 * 16 * (size_t)esz +
-         2 * (BWD_NT / 64) * 64 * 4 + 16;
+  return (size_t)2 * T * DH * esz + 2 * T * 4 + (BWD_NT / 64) * 16 * DH * (size_t)esz + 2 * (BWD_NT / 64) * 64 * 4 +
+         16;
 }
 
 // ---------------------------------------------------------------------------
