@@ -171,15 +171,18 @@ NSTL_DEV void store_tile16x64(const float (&v)[4][4], char* scr, char* gbase, in
 // dropout, then O = P V with P taken from the score registers (acc_frag).
 constexpr int FWD_NT = 512, FWD_QB = 16 * FWD_NT / 64;
 
-template <typename T>
-__global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
+// NKT = T/16 key tiles (score registers sized to T); T <= 128: 6 waves per SIMD (3
+// workgroups per CU) without spills; longer T: 4 / 3
+template <typename T, int NKT>
+__global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void attn_fwd_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
   constexpr int ESZ = (int)sizeof(T);
   constexpr int RBK = DH * ESZ;   // 128 (bf16) / 256 (f32)
   typedef ImgK<RBK> Img;
   constexpr int NW = FWD_NT / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int T_ = p.T, nkt = T_ / 16;
+  const int T_ = p.T;
+  constexpr int nkt = NKT;
   char* Kimg = smem;
   char* Vimg = Kimg + T_ * RBK;
   char* Ostage = Vimg + T_ * RBK;  // [NW][16][RBK]
@@ -206,9 +209,9 @@ __global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
   if (!act) return;
 
   // s[kt][r] = score(query q0 + c, key 16kt + 4g + r)
-  f32x4 s[16];
+  f32x4 s[NKT];
 #pragma unroll
-  for (int kt = 0; kt < 16; ++kt) {
+  for (int kt = 0; kt < NKT; ++kt) {
     s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
     if (kt < nkt) {
       Frag fk;
@@ -221,13 +224,13 @@ __global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
   const float c2 = p.scale * LOG2E;
   float m = -INFINITY;
 #pragma unroll
-  for (int kt = 0; kt < 16; ++kt)
+  for (int kt = 0; kt < NKT; ++kt)
     if (kt < nkt) m = fmaxf(fmaxf(fmaxf(m, s[kt][0]), fmaxf(s[kt][1], s[kt][2])), s[kt][3]);
   m = fmaxf(m, __shfl_xor(m, 16));
   m = fmaxf(m, __shfl_xor(m, 32));
   float sum = 0.f;
 #pragma unroll
-  for (int kt = 0; kt < 16; ++kt)
+  for (int kt = 0; kt < NKT; ++kt)
     if (kt < nkt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
     const int q = q0 + c;
     uint32_t mlo = 0, mhi = 0;  // lane kt*4 + r: keep bits of (kt, r)
 #pragma unroll
-    for (int kt = 0; kt < 16; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
       if (kt < nkt) {
         bool k[4];
         const uint64_t idx = drop_idx(bh, T_, q, kt * 16 + 4 * g);
@@ -270,8 +273,8 @@ __global__ __launch_bounds__(FWD_NT) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (2 * j < nkt) {
+  for (int j = 0; j < NKT / 2; ++j) {
+    {
       const Frag fp = acc_frag<T>(s[2 * j], s[2 * j + 1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -341,8 +344,9 @@ NSTL_DEV void wave_sum_out(const float* red, int nw, float* out, int lane) {
 //                 -> dV = P_drop^T dO, dK = dS^T Q (RoPE^T).
 constexpr int BWD_NT = 512, BWD_ROWS = 16 * BWD_NT / 64;  // 8 waves, 128 rows
 
+// (BWD_NT, 6): 6 waves per SIMD = 3 workgroups per CU (bf16: 78 VGPRs, no spill)
 template <typename T>
-__global__ __launch_bounds__(BWD_NT) void attn_bwd_dq_kernel(AttnParams p) {
+__global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
   constexpr int ESZ = (int)sizeof(T);
   constexpr int RBK = DH * ESZ;
@@ -902,8 +906,17 @@ extern "C" int nstl_attn_fwd(const nstl_attn_args* a, void* stream) {
   }
   dim3 grid((a->T + FWD_QB - 1) / FWD_QB, a->B * a->H);
   const size_t lds = fwd_lds_bytes(a->T, esz);
-  if (a->dtype == NSTL_BF16) return launch(attn_fwd_kernel<bf16>, grid, lds, st, p, "nstl_attn_fwd", FWD_NT);
-  return launch(attn_fwd_kernel<float>, grid, lds, st, p, "nstl_attn_fwd", FWD_NT);
+  // T % 32 == 0 and T <= 256 on this path: NKT in {2, 4, ..., 16}
+#define NSTL_FWD_CASE(N)                                                                              \
+  case N:                                                                                             \
+    return a->dtype == NSTL_BF16 ? launch(attn_fwd_kernel<bf16, N>, grid, lds, st, p, "nstl_attn_fwd", FWD_NT) \
+                                 : launch(attn_fwd_kernel<float, N>, grid, lds, st, p, "nstl_attn_fwd", FWD_NT);
+  switch (a->T / 16) {
+    NSTL_FWD_CASE(2) NSTL_FWD_CASE(4) NSTL_FWD_CASE(6) NSTL_FWD_CASE(8)
+    NSTL_FWD_CASE(10) NSTL_FWD_CASE(12) NSTL_FWD_CASE(14) NSTL_FWD_CASE(16)
+  }
+#undef NSTL_FWD_CASE
+  return nstl::fail((int)hipErrorInvalidValue, "nstl_attn_fwd: T=%d off the MFMA path", a->T);
 }
 
 extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
