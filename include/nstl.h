@@ -63,10 +63,16 @@ typedef struct nstl_gemm_args {
   float* colsum_part;                  /* optional [nstl_gemm_colsum_rows()][N] f32: per-128-row
                                           column sums of C as stored (DRELU_DROP on the 256
                                           kernel: the FFN1 bias gradient before nstl_reduce_rows) */
+  uint64_t* relu_mask;                 /* optional [nstl_gemm_relu_mask_words()]: BIAS_RELU_DROP
+                                          writes, DRELU_DROP reads (instead of aux) the bits
+                                          "kept and positive" of the FFN hidden, 1 bit/element */
 } nstl_gemm_args;
 int nstl_gemm(const nstl_gemm_args* args, void* stream);
 /* Rows of colsum_part for these arguments, or 0 when the call cannot produce it. */
 int nstl_gemm_colsum_rows(const nstl_gemm_args* args);
+/* 64-bit words of relu_mask for these arguments (the 256 kernel's ReLU-dropout or
+   dReLU epilogue, bf16), or 0 when the call cannot use it. */
+int64_t nstl_gemm_relu_mask_words(const nstl_gemm_args* args);
 
 /* Up to NSTL_GEMM_GROUP_MAX independent problems in ONE launch (grouped GEMM):
    each a bf16 problem for the 256x256 kernel (M, N >= 256, K % 64 == 0), no

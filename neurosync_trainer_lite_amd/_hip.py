@@ -37,6 +37,7 @@ class GemmArgs(ctypes.Structure):
         ("p_drop", _f32), ("seed", _u64),
         ("rope_cos", _vp), ("rope_sin", _vp), ("rope_T", _i32), ("rope_dim", _i32), ("rope_cols", _i32),
         ("split_k", _i32), ("workspace", _vp), ("workspace_bytes", _i64), ("colsum_part", _vp),
+        ("relu_mask", _vp),
     ]
 
 
@@ -87,7 +88,8 @@ class AdamArgs(ctypes.Structure):
 
 # every symbol include/nstl.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "nstl_gemm", "nstl_gemm_grouped", "nstl_gemm_colsum_rows", "nstl_gemm_workspace_bytes",
+    "nstl_gemm", "nstl_gemm_grouped", "nstl_gemm_colsum_rows", "nstl_gemm_relu_mask_words",
+    "nstl_gemm_workspace_bytes",
     "nstl_attn_fwd", "nstl_attn_bwd", "nstl_attn_bias_rows", "nstl_ln_fwd", "nstl_ln_bwd",
     "nstl_reduce_rows", "nstl_reduce_rows_strided", "nstl_reduce_rows3", "nstl_colsum", "nstl_rope",
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
@@ -112,6 +114,8 @@ def lib():
         L.nstl_gemm_grouped.argtypes = [P(GemmArgs), _i32, _vp]
         L.nstl_gemm_colsum_rows.argtypes = [P(GemmArgs)]
         L.nstl_gemm_colsum_rows.restype = _i32
+        L.nstl_gemm_relu_mask_words.argtypes = [P(GemmArgs)]
+        L.nstl_gemm_relu_mask_words.restype = _i64
         L.nstl_gemm_workspace_bytes.argtypes = [_i32, _i32, _i32]
         L.nstl_gemm_workspace_bytes.restype = _i64
         L.nstl_attn_fwd.argtypes = [P(AttnArgs), _vp]
@@ -174,6 +178,11 @@ def gemm(A, B, C, M, N, K, *, stream=None, **kw):
     check(lib().nstl_gemm(ctypes.byref(a), stream if stream is not None else stream_of()), "nstl_gemm")
 
 
+def gemm_relu_mask_words(A, B, C, M, N, K, **kw):
+    """64-bit words nstl_gemm would read/write as relu_mask for these arguments (0: unsupported)."""
+    return lib().nstl_gemm_relu_mask_words(ctypes.byref(gemm_args(A, B, C, M, N, K, **kw)))
+
+
 def gemm_colsum_rows(A, B, C, M, N, K, **kw):
     """Partial rows nstl_gemm would write to colsum_part for these arguments (0: unsupported)."""
     return lib().nstl_gemm_colsum_rows(ctypes.byref(gemm_args(A, B, C, M, N, K, **kw)))
@@ -194,7 +203,7 @@ def gemm_grouped(problems, stream=None):
 
 def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None,
               alpha=1.0, beta=0.0, epilogue=EPI_NONE, bias=None, aux=None, ld_aux=0, p_drop=0.0, seed=0,
-              rope=None, rope_cols=0, split_k=1, workspace=None, colsum_part=None):
+              rope=None, rope_cols=0, split_k=1, workspace=None, colsum_part=None, relu_mask=None):
     a = GemmArgs()
     a.dtype = dtype_code(A.dtype)
     a.c_dtype = dtype_code(C.dtype)
@@ -220,6 +229,7 @@ def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=N
         a.workspace = workspace.data_ptr()
         a.workspace_bytes = workspace.numel() * workspace.element_size()
     a.colsum_part = ptr(colsum_part)
+    a.relu_mask = ptr(relu_mask)
     return a
 
 

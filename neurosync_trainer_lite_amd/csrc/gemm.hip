@@ -40,6 +40,7 @@ struct GemmParams {
   float* ws;
   int debug_skip_epilogue; int k_chunk;  // split-K: partial slabs [z][M][N]
   float* colsum_part;  // [ceil(M/128)][N]: column sums of C as stored (dReLU ring epilogue)
+  uint64_t* relu_mask;  // ReLU-dropout keep&positive bits, ring epilogue layout (relu_mask_index)
 };
 
 // Epilogue over a wave's MT x 4 grid of 16x16 accumulators whose origin is
@@ -534,6 +535,13 @@ NSTL_DEV void stage_half(const f32x4 (&acc)[8][4], int half, float alpha, int la
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// ReLU mask word of (64-row block, lane row r0 in 0..7, 8-column group): byte k
+// = rows r0 + 8k of the block, bit e = column 8g + e -- one word per lane and
+// 64-row pass of the ring epilogue (bf16 output, 8 columns per lane).
+NSTL_DEV int64_t relu_mask_index(int N, int row_block64, int r0, int j) {
+  return ((int64_t)row_block64 * 8 + r0) * ((N + 7) >> 3) + (j >> 3);
+}
+
 template <int EM>
 NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, int col0, int lane, char* scr) {
   constexpr bool F32OUT = EM == EM_F32 || EM == EM_WS;
@@ -572,9 +580,14 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
   float csum[CW];
 #pragma unroll
   for (int e = 0; e < CW; ++e) csum[e] = 0.f;
+  const bool rmask = (EM == EM_RELU_DROP || EM == EM_DRELU) && p.relu_mask != nullptr;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
    const int ib = row0 + half * 64 + r0;
+   const int64_t midx = relu_mask_index(p.N, (row0 + half * 64) >> 6, r0, j);
+   // dReLU from the forward's mask word (8 B per lane and pass instead of 8 x 16 B of h)
+   uint64_t mword = 0;
+   if (EM == EM_DRELU && rmask && colok && ib < p.M) mword = p.relu_mask[midx];
 #pragma unroll
    for (int sub = 0; sub < SUBS; ++sub) {
     // Issue every input load of this (sub-)pass first: one memory latency per
@@ -607,7 +620,7 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
         inf[2 * iu + 1] = sn;
       } else if (EM == EM_DRELU) {
         bf16x8 a8 = {};
-        if (ok) {
+        if (ok && !rmask) {
           const bf16* ap = (const bf16*)p.aux + (int64_t)i * p.ld_aux + j;
           if (vec && (p.ld_aux % CW) == 0) {
             a8 = *(const bf16x8*)ap;
@@ -663,6 +676,12 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
               v[e + 1] = k1 ? v[e + 1] * p.inv_keep : 0.f;
             }
           }
+          if (rmask) {
+            uint32_t bits = 0;
+#pragma unroll
+            for (int e = 0; e < CW; ++e) bits |= ((bf16)v[e] > (bf16)0.f ? 1u : 0u) << e;  // as stored
+            mword |= (uint64_t)bits << (8 * it);
+          }
         } else if (EM == EM_ROPE) {
           if (rope_col) {
             const f32x4 cs = inf[(2 * iu) % NF], sn = inf[(2 * iu + 1) % NF];
@@ -674,9 +693,15 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
             }
           }
         } else if (EM == EM_DRELU) {
-          const bf16x8 a8 = ind[iu % ND];
+          if (rmask) {
+            const uint32_t bits = (uint32_t)(mword >> (8 * it));
 #pragma unroll
-          for (int e = 0; e < CW; ++e) v[e] = (float)a8[e % 8] > 0.f ? v[e] * p.inv_keep : 0.f;
+            for (int e = 0; e < CW; ++e) v[e] = ((bits >> e) & 1) ? v[e] * p.inv_keep : 0.f;
+          } else {
+            const bf16x8 a8 = ind[iu % ND];
+#pragma unroll
+            for (int e = 0; e < CW; ++e) v[e] = (float)a8[e % 8] > 0.f ? v[e] * p.inv_keep : 0.f;
+          }
           if (csum_on) {
 #pragma unroll
             for (int e = 0; e < CW; ++e) csum[e] += (float)(bf16)v[e];  // sum what is stored
@@ -715,6 +740,7 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
       for (int iu = 0; iu < NI; ++iu) body(iu);
     }
    }
+   if (EM == EM_RELU_DROP && rmask && colok && ib < p.M) p.relu_mask[midx] = mword;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   if (csum_on) {
@@ -1040,6 +1066,7 @@ int make_params(const nstl_gemm_args* a, GemmParams& p) {
   p.debug_skip_epilogue = getenv_debug_skip_epi();
   p.k_chunk = a->K;
   p.colsum_part = a->colsum_part;
+  p.relu_mask = a->relu_mask;
   return 0;
 }
 
@@ -1064,6 +1091,8 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   NSTL_CHECK_ARG(!a->colsum_part || (big && a->epilogue == NSTL_EPI_DRELU_DROP && a->split_k <= 1 &&
                                       ring_epi_mode(a, p) == EM_DRELU && getenv_ring()),
                  "nstl_gemm: colsum_part needs the 256 kernel's dReLU epilogue (nstl_gemm_colsum_rows)");
+  NSTL_CHECK_ARG(!a->relu_mask || nstl_gemm_relu_mask_words(a) > 0,
+                 "nstl_gemm: relu_mask needs the 256 kernel's ReLU-dropout / dReLU epilogue (nstl_gemm_relu_mask_words)");
   const int BKe = big ? 64 : 128 / esz;
   int splits = a->split_k > 1 ? a->split_k : 1;
   if (splits > 1) {
@@ -1104,7 +1133,7 @@ extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream
     if (int rc = make_params(a, gp.g[g])) return rc;
     NSTL_CHECK_ARG(a->dtype == NSTL_BF16 && a->K % 64 == 0 && a->M >= BIG && a->N >= BIG,
                    "nstl_gemm_grouped: problem %d is not a 256-kernel problem (bf16, M, N >= 256, K %% 64 == 0)", g);
-    NSTL_CHECK_ARG(a->epilogue == NSTL_EPI_NONE && a->split_k <= 1 && !a->colsum_part,
+    NSTL_CHECK_ARG(a->epilogue == NSTL_EPI_NONE && a->split_k <= 1 && !a->colsum_part && !a->relu_mask,
                    "nstl_gemm_grouped: problem %d: no epilogue, no split-K", g);
     NSTL_CHECK_ARG(a->a_kmajor == args[0].a_kmajor && a->b_kmajor == args[0].b_kmajor &&
                        a->c_dtype == args[0].c_dtype && (a->beta != 0.f) == (args[0].beta != 0.f),
@@ -1135,4 +1164,13 @@ extern "C" int nstl_gemm_colsum_rows(const nstl_gemm_args* a) {
   if (!big_ok(a) || a->epilogue != NSTL_EPI_DRELU_DROP || a->split_k > 1 || !getenv_ring()) return 0;
   if (ring_epi_mode(a, p) != EM_DRELU) return 0;
   return (a->M + 127) / 128;
+}
+
+extern "C" int64_t nstl_gemm_relu_mask_words(const nstl_gemm_args* a) {
+  GemmParams p;
+  if (a == nullptr || make_params(a, p) != 0) return 0;
+  if (!big_ok(a) || a->split_k > 1 || !getenv_ring() || a->dtype != NSTL_BF16 || a->c_dtype != NSTL_BF16) return 0;
+  const int em = ring_epi_mode(a, p);
+  if (em != EM_RELU_DROP && em != EM_DRELU) return 0;
+  return (int64_t)((a->M + 63) / 64) * 8 * ((a->N + 7) / 8);
 }

@@ -116,6 +116,12 @@ class _Buffers:
             self.abias = e(B * ((T + 127) // 128), 3 * D, dtype=f32)
             # FFN2 dX (dReLU epilogue): per-128-row column sums of dh (FFN1 bias grad)
             self.hpart = e((M + 127) // 128, Fd, dtype=f32)
+            # FFN hidden keep&positive bits (FFN1 epilogue -> FFN2 dX epilogue), 1 bit/element
+            nmw = ((M + 63) // 64) * 8 * ((Fd + 7) // 8)
+            self.e_rmask = [e(nmw, dtype=torch.int64) for _ in range(L)]
+            self.d_rmask = [e(nmw, dtype=torch.int64) for _ in range(L)]
+            self.e_rmask_ok = [False] * L
+            self.d_rmask_ok = [False] * L
             # attention dropout keep bits, written by the forward, read by the backward
             nw = max(1, B * eng.H * T * T // 64)
             self.e_mask = [e(nw, dtype=torch.int64) for _ in range(L)]
@@ -173,6 +179,9 @@ class Seq2SeqEngine:
         # instead of being written in the compute dtype and added by the next LN backward
         self.res_handoff_on = os.environ.get("NSTL_RES_HANDOFF", "1") != "0"
         self._dadd_pending = False
+        # NSTL_RELU_MASK=0: the FFN2 dX epilogue reads the saved hidden h for its
+        # dReLU instead of the 1-bit keep&positive mask the FFN1 epilogue writes
+        self.relu_mask_on = os.environ.get("NSTL_RELU_MASK", "1") != "0"
 
     # ------------------------------------------------------------------ setup
     def _check_shapes(self):
@@ -335,11 +344,17 @@ class Seq2SeqEngine:
         return s
 
     # ------------------------------------------------------------ primitives
-    def _gemm_fwd(self, x, wname, out, epi, rows=1, rope=None, rope_cols=0, p_drop=0.0, seed=0):
+    def _gemm_fwd(self, x, wname, out, epi, rows=1, rope=None, rope_cols=0, p_drop=0.0, seed=0, relu_mask=None):
+        """Projection forward; `relu_mask` (FFN1): also write the keep&positive bits of
+        the hidden for the backward's dReLU when the kernel can (returns whether)."""
         W = self.w(wname, rows)
         bias = self.b(wname.replace(".weight", ".bias"), rows)
-        K.gemm(x, W, out, x.shape[0], W.shape[0], W.shape[1], epilogue=epi, bias=bias, rope=rope,
-               rope_cols=rope_cols, p_drop=p_drop, seed=seed, stream=self.st)
+        kw = dict(epilogue=epi, bias=bias, rope=rope, rope_cols=rope_cols, p_drop=p_drop, seed=seed)
+        m, n, k = x.shape[0], W.shape[0], W.shape[1]
+        use = relu_mask is not None and self.relu_mask_on and \
+            0 < K.gemm_relu_mask_words(x, W, out, m, n, k, **kw) <= relu_mask.numel()
+        K.gemm(x, W, out, m, n, k, relu_mask=relu_mask if use else None, stream=self.st, **kw)
+        return use
 
     def _dw(self, dy, x, wname, rows, bf, ws, bias=True):
         """grad(W) (+)= dy^T x ; grad(b) (+)= colsum(dy) (unless the bias gradient
@@ -419,7 +434,7 @@ class Seq2SeqEngine:
             self._main.wait_stream(self._side)
             self._side_reads = []
 
-    def _dx(self, dy, wname, rows, out, beta, epi=K.EPI_NONE, aux=None, p_drop=0.0, colsum=None):
+    def _dx(self, dy, wname, rows, out, beta, epi=K.EPI_NONE, aux=None, p_drop=0.0, colsum=None, relu_mask=None):
         """out (+)= dy W  (W: [N][K] read as [r][j]).  colsum = (partials, grad(b), beta):
         the bias gradient of the Linear whose input gradient `out` is, from the
         epilogue's column sums; returns False when the kernel cannot produce them."""
@@ -428,6 +443,9 @@ class Seq2SeqEngine:
         self._guard(out)
         kw = dict(a_kmajor=True, b_kmajor=False, beta=beta, epilogue=epi, aux=aux,
                   ld_aux=aux.stride(0) if aux is not None else 0, p_drop=p_drop)
+        if relu_mask is not None and 0 < K.gemm_relu_mask_words(dy, W, out, dy.shape[0], k, n, **kw) \
+                <= relu_mask.numel():
+            kw["relu_mask"] = relu_mask
         m = dy.shape[0]
         nrows = K.gemm_colsum_rows(dy, W, out, m, k, n, **kw) if colsum is not None and self.fused_bias_on else 0
         fused = 0 < nrows <= (colsum[0].shape[0] if colsum is not None else 0)
@@ -536,7 +554,10 @@ class Seq2SeqEngine:
         x1 = bb.layer(bb.e_x1, l)
         self._ln(x, bb.y, x1, st[0:2], pre + "norm1", 2, (sd("resid"), sd("drop1")), bb.layer(bb.e_s1, l))
         h = bb.layer(bb.e_h, l)
-        self._gemm_fwd(x1, pre + "ffn.linear1.weight", h, K.EPI_BIAS_RELU_DROP, p_drop=self.p, seed=sd("ffn"))
+        ok = self._gemm_fwd(x1, pre + "ffn.linear1.weight", h, K.EPI_BIAS_RELU_DROP, p_drop=self.p, seed=sd("ffn"),
+                            relu_mask=bb.e_rmask[l] if bb.save else None)
+        if bb.save:
+            bb.e_rmask_ok[l] = ok
         self._gemm_fwd(h, pre + "ffn.linear2.weight", bb.y, K.EPI_BIAS)
         x2 = bb.layer(bb.e_x2, l)
         self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 1, (sd("drop2"), 0), bb.layer(bb.e_s2, l))
@@ -567,7 +588,10 @@ class Seq2SeqEngine:
         x2 = L_(bb.d_x2)
         self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 2, (sd("xresid"), sd("drop2x")), L_(bb.d_s2))
         h = L_(bb.d_h)
-        self._gemm_fwd(x2, pre + "ffn.linear1.weight", h, K.EPI_BIAS_RELU_DROP, p_drop=self.p, seed=sd("ffn"))
+        ok = self._gemm_fwd(x2, pre + "ffn.linear1.weight", h, K.EPI_BIAS_RELU_DROP, p_drop=self.p, seed=sd("ffn"),
+                            relu_mask=bb.d_rmask[l] if bb.save else None)
+        if bb.save:
+            bb.d_rmask_ok[l] = ok
         self._gemm_fwd(h, pre + "ffn.linear2.weight", bb.y, K.EPI_BIAS)
         x3 = L_(bb.d_x3)
         self._ln(x2, bb.y, x3, st[4:6], pre + "norm3", 1, (sd("drop3"), 0), L_(bb.d_s3))
@@ -703,7 +727,7 @@ class Seq2SeqEngine:
         self._dw(bb.dqkv, x_in, pre + "self_attn.q_linear.weight", 3, bf, ws, bias=not fused)
         self._dx_res(bb.dqkv, pre + "self_attn.q_linear.weight", 3, last=last)
 
-    def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf, dy=None):
+    def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf, dy=None, rmask=None):
         """Backward through x_out = LN(x_in + drop(FFN(x_in)))."""
         ws = self.cur.ws
         dy = bb.dy if dy is None else dy
@@ -711,7 +735,7 @@ class Seq2SeqEngine:
                      bias_of=pre + "ffn.linear2.bias")
         self._dw(dy, h, pre + "ffn.linear2.weight", 1, bf, ws, bias=False)
         fused = self._dx(dy, pre + "ffn.linear2.weight", 1, bb.dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p,
-                         colsum=(bb.hpart, self.gb(pre + "ffn.linear1.bias"), bf))
+                         colsum=(bb.hpart, self.gb(pre + "ffn.linear1.bias"), bf), relu_mask=rmask)
         self._dw(bb.dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws, bias=not fused)
         self._dx_res(bb.dh, pre + "ffn.linear1.weight", 1)
 
@@ -720,7 +744,8 @@ class Seq2SeqEngine:
         sd = lambda s: _seed(self.base_seed, True, l, s)
         st = bb.e_stats[l]
         x_in = bb.x0 if l == 0 else bb.e_x2[l - 1]
-        self._ffn_bwd(bb, pre, bb.e_x1[l], bb.e_h[l], bb.e_s2[l], st[2:4], "norm2", sd("drop2"), bf)
+        self._ffn_bwd(bb, pre, bb.e_x1[l], bb.e_h[l], bb.e_s2[l], st[2:4], "norm2", sd("drop2"), bf,
+                      rmask=bb.e_rmask[l] if bb.e_rmask_ok[l] else None)
         self._attn_block_bwd(bb, pre, x_in, bb.e_qkv[l], bb.e_o[l], bb.e_lse[l], st[0:2], bb.e_s1[l], "norm1",
                              (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.e_mask[l], last=(l == 0))
 
@@ -734,7 +759,7 @@ class Seq2SeqEngine:
         if grouped:
             self._defer = []
         self._ffn_bwd(bb, pre, bb.d_x2[l], bb.d_h[l], bb.d_s3[l], st[4:6], "norm3", sd("drop3"), bf,
-                      dy=bb.dy_f if grouped else None)
+                      dy=bb.dy_f if grouped else None, rmask=bb.d_rmask[l] if bb.d_rmask_ok[l] else None)
         # cross attention block: x2 = LN(x1 + drop(drop(out(attn(q(x1), kv(mem))))))
         m = pre + "multihead_attn."
         dyx = bb.dy_x if grouped else bb.dy

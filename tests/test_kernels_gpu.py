@@ -166,6 +166,36 @@ def test_gemm_drelu_colsum_partials(M, N):
         K.gemm(dY, W, out, M, N, Kd, a_kmajor=True, b_kmajor=False, colsum_part=part)
 
 
+@pytest.mark.parametrize("M,N", [(1024, 2048), (1000, 4096)])
+def test_gemm_relu_mask_roundtrip(M, N):
+    """relu_mask: the ReLU-dropout forward epilogue's keep&positive bits drive the
+    dReLU backward epilogue to exactly the result of reading the saved hidden."""
+    Kd = 512
+    X, W1 = rnd(M, Kd, dtype=torch.bfloat16, seed=140), rnd(N, Kd, dtype=torch.bfloat16, seed=141)
+    b1 = 0.1 * rnd(N, seed=142)
+    h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    fw = dict(epilogue=K.EPI_BIAS_RELU_DROP, bias=b1, p_drop=0.3, seed=31)
+    words = K.gemm_relu_mask_words(X, W1, h, M, N, Kd, **fw)
+    assert words == ((M + 63) // 64) * 8 * ((N + 7) // 8)
+    mask = torch.zeros(words, dtype=torch.int64, device=DEV)
+    K.gemm(X, W1, h, M, N, Kd, relu_mask=mask, **fw)
+    h2 = torch.empty_like(h)
+    K.gemm(X, W1, h2, M, N, Kd, **fw)
+    dY, W2 = rnd(M, Kd, dtype=torch.bfloat16, seed=143), rnd(Kd, N, dtype=torch.bfloat16, seed=144)
+    bw = dict(a_kmajor=True, b_kmajor=False, epilogue=K.EPI_DRELU_DROP, aux=h, ld_aux=N, p_drop=0.3)
+    assert K.gemm_relu_mask_words(dY, W2, h, M, N, Kd, **bw) == words
+    d1, d2 = torch.empty_like(h), torch.empty_like(h)
+    K.gemm(dY, W2, d1, M, N, Kd, relu_mask=mask, **bw)
+    K.gemm(dY, W2, d2, M, N, Kd, **bw)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h2)
+    assert torch.equal(d1, d2)
+    kept = (h.float() > 0).float().mean().item()
+    assert 0.2 < kept < 0.5, kept   # ~0.7 keep x ~0.5 positive
+    # the 128 kernel / other epilogues cannot use the mask
+    assert K.gemm_relu_mask_words(X, W1, h, M, N, Kd, epilogue=K.EPI_BIAS, bias=b1) == 0
+
+
 @pytest.mark.parametrize("beta", [0.0, 1.0])
 def test_gemm_grouped_weight_gradients(beta):
     """nstl_gemm_grouped: independent dW = dY^T X problems of different shapes in one
