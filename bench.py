@@ -112,8 +112,9 @@ def main():
     crit, opt, sched = prepare_training_components(cfg, model)
     eng = model.engine()
     if world > 1:
-        eng.grad_reducer = parallel.GradAllReducer(eng.g32)
-        eng.grad_scale_t = torch.full((1,), 1.0 / world, device=dev)
+        # sharded optimizer (ZeRO-1; NSTL_DP=allreduce: bucketed all-reduce during backward)
+        from neurosync_trainer_lite_amd.utils.training_utils import attach_data_parallel
+        attach_data_parallel(model, opt, world)
     W = sum(p.numel() for n, p in model.named_parameters() if n.endswith("weight") and p.dim() == 2)
 
     g = torch.Generator(device=dev).manual_seed(100 + rank)

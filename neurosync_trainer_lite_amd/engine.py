@@ -48,6 +48,9 @@ def _span(t):
     return lo, lo + n * t.element_size()
 
 
+ARENA_ALIGN = 64 * 840
+
+
 def _pad64(n):
     return (n + 63) // 64 * 64
 
@@ -226,18 +229,38 @@ class Seq2SeqEngine:
         return order
 
     def _build_arena(self):
+        """Two regions: the matrices (reverse backward order), padded to a multiple
+        of ARENA_ALIGN so they split into equal 64-aligned shards for 1..8 ranks
+        (sharded optimizer), then the vectors (biases, LayerNorm gamma/beta, ~0.1 %
+        of the parameters) that the kernels read in f32: the sharded optimizer
+        keeps those replicated (parallel.zero1_step)."""
         named = dict(self.model.named_parameters())
         order = self._arena_order()
         if sorted(order) != sorted(named):
             raise RuntimeError("unexpected parameter set: %s" % sorted(set(order) ^ set(named)))
+        mats = [n for n in order if named[n].dim() > 1]
+        vecs = [n for n in order if named[n].dim() <= 1]
         self.offsets = {}
         off = 0
-        for n in order:
+        for n in mats:
+            k = named[n].numel()
+            self.offsets[n] = (off, k, tuple(named[n].shape))
+            off += _pad64(k)
+        self.n_shardable = off = (off + ARENA_ALIGN - 1) // ARENA_ALIGN * ARENA_ALIGN
+        for n in vecs:
             k = named[n].numel()
             self.offsets[n] = (off, k, tuple(named[n].shape))
             off += _pad64(k)
         self.numel = off
-        self.end_of = {n: o + _pad64(k) for n, (o, k, _) in self.offsets.items()}
+        # gradient-bucket readiness (GradAllReducer): after the backward of the
+        # parameter `name` the matrices' prefix up to here is final
+        self.end_of, hi = {}, 0
+        for n in order:
+            o, k, _ = self.offsets[n]
+            if named[n].dim() > 1:
+                hi = o + _pad64(k)
+            self.end_of[n] = hi
+        self.master_stale = False  # sharded optimizer: p32 matrices outside this rank's shard are old
         dev = self.device
         self.p32 = torch.zeros(off, dtype=torch.float32, device=dev)
         self.g32 = torch.zeros(off, dtype=torch.float32, device=dev)

@@ -16,6 +16,17 @@ parameter is copied back, with nothing overlapped.  Here:
     >= bucket_bytes are all-reduced asynchronously as soon as they are complete,
     on RCCL's own stream, overlapping the remaining backward;
   * clip + Adam then run replicated on every rank on identical reduced grads.
+
+Default mode (NSTL_DP=zero1, ShardComm + utils.optim.FusedAdam.shard): no
+collective runs during backward -- a concurrent RCCL kernel holding even a few
+CUs turns the step's one-workgroup-per-CU GEMM rounds into two rounds
+(tools/cu_hog_bench.py: 4 held CUs cost +36 % step time).  After backward the
+gradient arena is reduce-scattered (f32), each rank clips with the global norm
+(one all-reduce of 1024 partial sums) and runs Adam on its 1/n shard, and the
+updated compute-dtype parameters are all-gathered.  Per step and rank that moves
+(n-1)/n of 4 + 2 bytes per parameter instead of an all-reduce's 2 * 4, and the
+optimizer's 30 B/param of HBM traffic drops to 1/n.  The f32 master weights and
+Adam moments outside a rank's shard go stale until consolidate() (checkpoints).
 """
 import os
 
@@ -85,3 +96,65 @@ class GradAllReducer:
         for w in self.works:
             w.wait()
         self.reset()
+
+
+class ShardComm:
+    """Equal contiguous shards of a flat arena over the ranks of `group`:
+    reduce-scatter / all-gather helpers (RCCL collectives on nccl; gloo, used by
+    the CPU tests, has neither, so there they are built from all_reduce /
+    all_gather)."""
+
+    def __init__(self, numel, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if numel % (self.world * 64):
+            raise ValueError("arena of %d elements does not split into %d 64-aligned shards" % (numel, self.world))
+        self.numel = numel
+        self.shard = numel // self.world
+        self.lo = self.rank * self.shard
+        self.hi = self.lo + self.shard
+        self._nccl = dist.get_backend(group) == "nccl"
+
+    def reduce_scatter(self, full, out):
+        """out (this rank's shard) = sum over ranks of full[lo:hi]."""
+        if self._nccl:
+            dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            t = full.clone()
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            out.copy_(t[self.lo:self.hi])
+
+    def all_gather(self, full):
+        """full[every shard] = the owning rank's full[lo:hi] (in place)."""
+        mine = full[self.lo:self.hi]
+        if self._nccl:
+            dist.all_gather_into_tensor(full, mine.clone(), group=self.group)
+        else:
+            parts = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(parts, mine.contiguous(), group=self.group)
+            full.copy_(torch.cat(parts))
+
+
+def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=None):
+    """One sharded clip + Adam step (the FusedAdam kernels passed in as callables,
+    so the orchestration is testable on CPU): reduce-scatter the gradients of
+    the shardable region [0, comm.numel), sum of squares of this shard, all-reduce
+    of the partial sums; `tail` = (lo, hi), a small replicated region (the f32
+    vectors), is all-reduced whole, its squares added once and updated on every
+    rank; Adam on this shard (+ tail), then all-gather each tensor of `gather`
+    over the shardable region."""
+    comm.reduce_scatter(g_full[:comm.numel], g_shard)
+    sumsq_fn(g_shard, partial)
+    dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=comm.group)
+    if tail is not None and tail[1] > tail[0]:
+        lo, hi = tail
+        gt = g_full[lo:hi]
+        dist.all_reduce(gt, op=dist.ReduceOp.SUM, group=comm.group)
+        part_t = torch.zeros_like(partial)
+        sumsq_fn(gt, part_t)
+        partial += part_t
+        adam_fn(lo, hi - lo, gt, partial)
+    adam_fn(comm.lo, comm.shard, g_shard, partial)
+    for t in gather:
+        comm.all_gather(t[:comm.numel])

@@ -70,10 +70,14 @@ def train_model(config, model_0, model_1, model_2, model_3, dataloader, val_data
                                              pbar=pbar, total_epochs=n_epochs, use_amp=use_amp, grad_scaler=scaler,
                                              val_dataloader=val_dataloader, validation_interval=20)
             scheduler.step()
+            if world > 1 and hasattr(optimizer, "consolidate"):
+                optimizer.consolidate()  # sharded optimizer: every rank, before rank 0 saves
             if rank == 0:
                 save_checkpoint_and_data(epoch, model_0, optimizer, scheduler, batch_step, config, lock, device0)
             if world > 1:
                 dist.barrier()
+        if world > 1 and hasattr(optimizer, "consolidate"):
+            optimizer.consolidate()
         if rank == 0:
             save_final_model(model_0)
     finally:

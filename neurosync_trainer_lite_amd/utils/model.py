@@ -218,6 +218,13 @@ class Seq2Seq(nn.Module):
         self._anchor = torch.zeros((), requires_grad=True)
         self._register_state_dict_hook(_compact_state_dict)
 
+    def state_dict(self, *args, **kwargs):
+        eng = self.__dict__.get("_engine")
+        if eng is not None and eng.master_stale:
+            raise RuntimeError("parameters are sharded across ranks (FusedAdam.shard): call "
+                               "optimizer.consolidate() on every rank before state_dict()")
+        return super().state_dict(*args, **kwargs)
+
     def engine(self, device=None):
         """The MI355X engine owning this model's parameter arena (built on first use)."""
         if self._engine is None:

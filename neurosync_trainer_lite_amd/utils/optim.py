@@ -30,6 +30,8 @@ class FusedAdam(torch.optim.Optimizer):
         self._engine = None
         self._nstl_step = 0
         self.last_norm = None
+        self._comm = None            # parallel.ShardComm when sharded (ZeRO-1)
+        self._moments_stale = False  # sharded: m/v outside this rank's shard are old
 
     # --------------------------------------------------------------- arena
     def _bind(self):
@@ -64,6 +66,33 @@ class FusedAdam(torch.optim.Optimizer):
                 "exp_avg_sq": self.v[o:o + k].view(shp)}
 
     # ---------------------------------------------------------------- step
+    # ------------------------------------------------------------ sharding
+    def shard(self, group=None):
+        """Data-parallel ZeRO-1 (parallel.zero1_step): from now on step() reduce-
+        scatters the gradients, clips with the global norm, updates this rank's
+        1/n of the parameters and all-gathers the compute-dtype weights.  The f32
+        master weights and Adam moments of the other shards go stale until
+        consolidate() -- a collective every rank must call (e.g. before rank 0
+        saves a checkpoint)."""
+        from .. import parallel
+        eng = self._bind()
+        eng.ensure_bound()
+        self._comm = parallel.ShardComm(eng.n_shardable, group)
+        self._gs = torch.empty(self._comm.shard, dtype=torch.float32, device=eng.device)
+        return self
+
+    @torch.no_grad()
+    def consolidate(self):
+        """All-gather the f32 master weights and the Adam moments (collective)."""
+        if self._comm is None:
+            return
+        eng = self._engine
+        for t in (eng.p32, self.m, self.v):
+            self._comm.all_gather(t[:eng.n_shardable])
+        eng.master_stale = False
+        self._moments_stale = False
+
+    # ---------------------------------------------------------------- step
     @torch.no_grad()
     def step(self, closure=None, max_norm=None):
         """One Adam step; with ``max_norm`` the global-norm clip (clip_grad_norm_)
@@ -78,19 +107,38 @@ class FusedAdam(torch.optim.Optimizer):
         self._nstl_step += 1
         st = K.stream_of(eng.device)
         a = K.AdamArgs()
-        a.p, a.g, a.m, a.v = eng.p32.data_ptr(), eng.g32.data_ptr(), self.m.data_ptr(), self.v.data_ptr()
-        if eng.p16 is not eng.p32:
-            a.p_lowp, a.lowp_dtype = eng.p16.data_ptr(), K.dtype_code(eng.p16.dtype)
-        a.n = eng.numel
+        a.lowp_dtype = K.dtype_code(eng.p16.dtype)
         a.lr, a.eps, a.weight_decay = g["lr"], g["eps"], g["weight_decay"]
         a.beta1, a.beta2 = g["betas"]
         a.step = self._nstl_step
         if max_norm is not None:
-            K.sumsq(eng.g32, eng.numel, self.partial, N_PARTIAL, stream=st)
             a.sumsq_partial, a.n_partial, a.max_norm = self.partial.data_ptr(), N_PARTIAL, float(max_norm)
             a.norm_out = self.norm.data_ptr()
             self.last_norm = self.norm
-        K.adam_step(a, stream=st)
+
+        def adam_fn(lo, n, grads, partial):
+            a.p, a.g, a.m, a.v = (eng.p32[lo:].data_ptr(), grads.data_ptr(), self.m[lo:].data_ptr(),
+                                  self.v[lo:].data_ptr())
+            if eng.p16 is not eng.p32:
+                a.p_lowp = eng.p16[lo:].data_ptr()
+            a.n = n
+            K.adam_step(a, stream=st)
+
+        def sumsq_fn(grads, partial):
+            if max_norm is not None:
+                K.sumsq(grads, grads.numel(), partial, N_PARTIAL, stream=st)
+
+        if self._comm is None:
+            sumsq_fn(eng.g32, self.partial)
+            adam_fn(0, eng.numel, eng.g32, self.partial)
+            return loss
+        from .. import parallel
+        if max_norm is None:
+            self.partial.zero_()
+        parallel.zero1_step(self._comm, eng.g32, self._gs, self.partial, sumsq_fn, adam_fn,
+                            [eng.p16] if eng.p16 is not eng.p32 else [eng.p32], tail=(eng.n_shardable, eng.numel))
+        eng.master_stale = eng.p16 is not eng.p32
+        self._moments_stale = True
         return loss
 
     def zero_grad(self, set_to_none=True):
@@ -104,6 +152,8 @@ class FusedAdam(torch.optim.Optimizer):
 
     # ------------------------------------------------------------ state io
     def state_dict(self):
+        if self._moments_stale:
+            raise RuntimeError("sharded FusedAdam: call consolidate() on every rank before state_dict()")
         if self._engine is not None:
             for p in self.param_groups[0]["params"]:
                 self.state[p]["step"] = torch.tensor(float(self._nstl_step))

@@ -164,15 +164,21 @@ def rank_batches(dataloader, rank, world):
         yield s, collate([ds[i] for i in order[s * world + rank]])
 
 
-def _attach_reducer(model, world):
+def attach_data_parallel(model, optimizer, world):
+    """Wire one rank's engine/optimizer for data parallelism (parallel.py): the
+    loss gradient pre-scaled by 1/world, per-rank dropout streams, and either the
+    sharded optimizer (NSTL_DP=zero1, default: no collective during backward) or
+    the bucketed gradient all-reduce overlapped with backward (NSTL_DP=allreduce)."""
     eng = _engine_of(model)
-    if eng is None or world == 1:
+    if eng is None or world == 1 or eng.grad_scale_t is not None:
         return
-    if eng.grad_reducer is None:
+    eng.grad_scale_t = torch.full((1,), 1.0 / world, device=eng.device)
+    eng.seed_salt = dist.get_rank()
+    if os.environ.get("NSTL_DP", "zero1") == "allreduce" or not hasattr(optimizer, "shard"):
         from ..parallel import GradAllReducer
         eng.grad_reducer = GradAllReducer(eng.g32)
-        eng.grad_scale_t = torch.full((1,), 1.0 / world, device=eng.device)
-        eng.seed_salt = dist.get_rank()
+    else:
+        optimizer.shard()
 
 
 def train_one_epoch_multi_gpu(epoch, models, dataloader, criterion, optimizer, devices, clip, batch_step=0,
@@ -199,7 +205,7 @@ def train_one_epoch_multi_gpu(epoch, models, dataloader, criterion, optimizer, d
     for m in models:
         m.train()
     if world > 1:
-        _attach_reducer(models[0], world)
+        attach_data_parallel(models[0], optimizer, world)
     pending = _Pending()
 
     def report(done):

@@ -91,3 +91,60 @@ def test_data_parallel_gloo(tmp_path, monkeypatch):
         opt.step()
     for k, v in model.state_dict().items():
         torch.testing.assert_close(a[k], v, rtol=1e-5, atol=1e-6)
+
+
+def _shard_worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from neurosync_trainer_lite_amd import parallel
+    parallel.init_from_env(backend="gloo")
+    ns = 64 * 840  # one ARENA_ALIGN unit: splits for 1..8 ranks
+    n = ns + 192   # + a replicated tail (the arena's f32 vectors)
+    comm = parallel.ShardComm(ns)
+    assert (comm.shard, comm.lo) == (ns // WORLD, rank * ns // WORLD)
+    g = torch.Generator().manual_seed(1)
+    p = torch.randn(n, generator=g)
+    m, v = torch.zeros(n), torch.zeros(n)
+    grads = torch.randn(n, generator=torch.Generator().manual_seed(10 + rank)) * (rank + 1)
+    gs = torch.empty(comm.shard)
+    partial = torch.zeros(4)
+
+    def sumsq_fn(x, part):
+        part.zero_()
+        part[0] = (x.double() ** 2).sum().float()
+
+    def adam_fn(lo, k, x, part):
+        coef = min(1.0, 2.0 / (float(part.sum()) ** 0.5 + 1e-6))
+        gg = x * coef + 1e-5 * p[lo:lo + k]
+        m[lo:lo + k] = 0.9 * m[lo:lo + k] + 0.1 * gg
+        v[lo:lo + k] = 0.999 * v[lo:lo + k] + 0.001 * gg * gg
+        p[lo:lo + k] -= 1e-3 / 0.1 * m[lo:lo + k] / ((v[lo:lo + k] / 0.001).sqrt() + 1e-8)
+
+    parallel.zero1_step(comm, grads, gs, partial, sumsq_fn, adam_fn, [p], tail=(ns, n))
+    for t in (m, v):
+        comm.all_gather(t[:ns])  # consolidate
+    torch.save({"p": p, "m": m, "v": v}, os.path.join(out_dir, "s%d.pt" % rank))
+    dist.destroy_process_group()
+
+
+def test_sharded_optimizer_step_gloo(tmp_path):
+    """ZeRO-1 orchestration (parallel.ShardComm / zero1_step, the FusedAdam
+    sharded path with CPU stand-ins for the two kernels): reduce-scatter, global
+    norm from per-shard partial sums, Adam on each shard, all-gather -- equal to
+    one process clipping and stepping the summed gradient."""
+    mp.spawn(_shard_worker, args=(_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    r0 = torch.load(tmp_path / "s0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "s1.pt", weights_only=True)
+    for k in r0:
+        torch.testing.assert_close(r0[k], r1[k], rtol=0, atol=0)
+    n = 64 * 840 + 192
+    p = torch.randn(n, generator=torch.Generator().manual_seed(1))
+    gsum = sum(torch.randn(n, generator=torch.Generator().manual_seed(10 + r)) * (r + 1) for r in range(WORLD))
+    coef = min(1.0, 2.0 / (float((gsum.double() ** 2).sum()) ** 0.5 + 1e-6))
+    gg = gsum * coef + 1e-5 * p
+    m, v = 0.1 * gg, 0.001 * gg * gg
+    p = p - 1e-3 / 0.1 * m / ((v / 0.001).sqrt() + 1e-8)
+    torch.testing.assert_close(r0["p"], p, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(r0["m"], m, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(r0["v"], v, rtol=1e-5, atol=1e-9)
