@@ -79,8 +79,9 @@ int64_t nstl_gemm_relu_mask_words(const nstl_gemm_args* args);
    epilogue, no split-K, all with the same a_kmajor / b_kmajor / c_dtype and
    beta use (0 / nonzero); alpha, beta, pointers and shapes per problem.  The
    weight gradients of one decoder layer (utils/model.py:193-216 Linears,
-   backward) are ~256 tiles: one full round with no split-K partials. */
-#define NSTL_GEMM_GROUP_MAX 8
+   backward) are 256 tiles: one full round with no split-K partials; those of
+   four encoder layers are 768 tiles: three. */
+#define NSTL_GEMM_GROUP_MAX 16
 int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream);
 int64_t nstl_gemm_workspace_bytes(int M, int N, int split_k);
 

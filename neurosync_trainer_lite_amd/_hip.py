@@ -188,7 +188,7 @@ def gemm_colsum_rows(A, B, C, M, N, K, **kw):
     return lib().nstl_gemm_colsum_rows(ctypes.byref(gemm_args(A, B, C, M, N, K, **kw)))
 
 
-GEMM_GROUP_MAX = 8
+GEMM_GROUP_MAX = 16
 
 
 def gemm_grouped(problems, stream=None):

@@ -49,6 +49,9 @@ def _span(t):
 
 
 ARENA_ALIGN = 64 * 840
+# encoder layers whose weight gradients share one grouped GEMM: 4 x 192 tiles of
+# 256^2 = 768 = three full rounds on 256 CUs (one layer alone: 0.75 of a round)
+ENC_GROUP = 4
 
 
 def _pad64(n):
@@ -106,6 +109,13 @@ class _Buffers:
             self.dmem = e(M, D, dtype=f32)
             self.dy = e(M, D)
             self.dy_f, self.dy_x = e(M, D), e(M, D)  # decoder: dy of FFN2 / cross out_linear (grouped dW)
+            # encoder: per-layer dy / dh / dqkv for ENC_GROUP layers whose weight
+            # gradients are one grouped launch (slot = layer % ENC_GROUP)
+            G = min(ENC_GROUP, L)
+            self.g_dyf = [e(M, D) for _ in range(G)]
+            self.g_dyo = [e(M, D) for _ in range(G)]
+            self.g_dh = [e(M, Fd) for _ in range(G)]
+            self.g_dqkv = [e(M, 3 * D) for _ in range(G)]
             self.dadd = e(M, D)  # a Linear's input gradient (dtype), added by the next LN backward
             self.dattn = e(M, D)
             self.dqkv = e(M, 3 * D)
@@ -172,6 +182,7 @@ class Seq2SeqEngine:
         self._side_reads = []      # (lo, hi, event): bytes a queued dW still reads
         # NSTL_DW_GROUP=0: one GEMM per weight gradient (split-K) instead of one
         # grouped launch per decoder layer (its 7 weight gradients are 256 tiles)
+        # and per ENC_GROUP encoder layers (4 x 4 weight gradients, 768 tiles)
         self.dw_group_on = os.environ.get("NSTL_DW_GROUP", "1") != "0"
         self._defer = None         # weight-gradient jobs of the current decoder layer
         # NSTL_FUSED_BIAS=0: q/k/v and FFN1 bias gradients by colsum() instead of
@@ -715,9 +726,16 @@ class Seq2SeqEngine:
         x_last = bb.layer(bb.e_x2, L - 1)
         self._ln_bwd(x_last, bb.encf_stats, "encoder.layer_norm", bb.dmem, dres, None, 0, (0, 0), bf)
         ready("encoder.layer_norm.bias")
+        # encoder weight gradients: one grouped launch per ENC_GROUP layers
+        enc_group = self.dw_group_on and self._side is None
         for l in reversed(range(L)):
-            self._enc_layer_bwd(bb, l, T, bf)
-            ready("encoder.transformer_encoder.%d.self_attn.v_linear.bias" % l)
+            if enc_group and self._defer is None:
+                self._defer = []
+            self._enc_layer_bwd(bb, l, T, bf, slot=(l % ENC_GROUP) if enc_group else None)
+            if enc_group and l % ENC_GROUP == 0:
+                self._dw_flush(ws)
+            if not enc_group or l % ENC_GROUP == 0:
+                ready("encoder.transformer_encoder.%d.self_attn.v_linear.bias" % l)
         # embedding + global PE: x0 = GPE(src W^T + b)
         self._guard(bb.demb)
         K.rope(dres, D, bb.demb, D, M, D, cs, sn, T, D, inverse=True, stream=self.st)
@@ -737,40 +755,48 @@ class Seq2SeqEngine:
         with torch.cuda.stream(self._side):
             red.ready(upto)
 
-    def _attn_block_bwd(self, bb, pre, x_in, qkv, o, lse, st, s1, norm, seeds, T, bf, mask, last=False):
+    def _attn_block_bwd(self, bb, pre, x_in, qkv, o, lse, st, s1, norm, seeds, T, bf, mask, last=False,
+                        dy=None, dqkv=None):
         """Backward through x1 = LN(x_in + drop(drop(out_linear(attn(x_in))))) (self-attention)."""
         D, ws = self.D, bb.ws
-        self._ln_bwd(s1, st, pre + norm, bb.dres, bb.dres, bb.dy, 2, seeds[0:2], bf,
+        dy = bb.dy if dy is None else dy
+        dqkv = bb.dqkv if dqkv is None else dqkv
+        self._ln_bwd(s1, st, pre + norm, bb.dres, bb.dres, dy, 2, seeds[0:2], bf,
                      bias_of=pre + "self_attn.out_linear.bias")
-        self._dw(bb.dy, o, pre + "self_attn.out_linear.weight", 1, bf, ws, bias=False)
-        self._dx(bb.dy, pre + "self_attn.out_linear.weight", 1, bb.dattn, 0.0)
+        self._dw(dy, o, pre + "self_attn.out_linear.weight", 1, bf, ws, bias=False)
+        self._dx(dy, pre + "self_attn.out_linear.weight", 1, bb.dattn, 0.0)
         fused = self._attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, bb.dattn,
-                               bb.dqkv[:, :D], bb.dqkv[:, D:2 * D], bb.dqkv[:, 2 * D:], seeds[2], T, bb.B, mask=mask,
+                               dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], seeds[2], T, bb.B, mask=mask,
                                bias=[(0, 3 * D, self.gb(pre + "self_attn.q_linear.bias", 3))], bf=bf)
-        self._dw(bb.dqkv, x_in, pre + "self_attn.q_linear.weight", 3, bf, ws, bias=not fused)
-        self._dx_res(bb.dqkv, pre + "self_attn.q_linear.weight", 3, last=last)
+        self._dw(dqkv, x_in, pre + "self_attn.q_linear.weight", 3, bf, ws, bias=not fused)
+        self._dx_res(dqkv, pre + "self_attn.q_linear.weight", 3, last=last)
 
-    def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf, dy=None, rmask=None):
+    def _ffn_bwd(self, bb, pre, x_in, h, s_out, st, norm, seed_drop, bf, dy=None, rmask=None, dh=None):
         """Backward through x_out = LN(x_in + drop(FFN(x_in)))."""
         ws = self.cur.ws
         dy = bb.dy if dy is None else dy
+        dh = bb.dh if dh is None else dh
         self._ln_bwd(s_out, st, pre + norm, bb.dres, bb.dres, dy, 1, (seed_drop, 0), bf,
                      bias_of=pre + "ffn.linear2.bias")
         self._dw(dy, h, pre + "ffn.linear2.weight", 1, bf, ws, bias=False)
-        fused = self._dx(dy, pre + "ffn.linear2.weight", 1, bb.dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p,
+        fused = self._dx(dy, pre + "ffn.linear2.weight", 1, dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p,
                          colsum=(bb.hpart, self.gb(pre + "ffn.linear1.bias"), bf), relu_mask=rmask)
-        self._dw(bb.dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws, bias=not fused)
-        self._dx_res(bb.dh, pre + "ffn.linear1.weight", 1)
+        self._dw(dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws, bias=not fused)
+        self._dx_res(dh, pre + "ffn.linear1.weight", 1)
 
-    def _enc_layer_bwd(self, bb, l, T, bf):
+    def _enc_layer_bwd(self, bb, l, T, bf, slot=None):
+        """`slot`: this layer's weight gradients are queued for a grouped launch,
+        so its dy / dh / dqkv live in per-slot buffers until then."""
         pre = "encoder.transformer_encoder.%d." % l
         sd = lambda s: _seed(self.base_seed, True, l, s)
         st = bb.e_stats[l]
         x_in = bb.x0 if l == 0 else bb.e_x2[l - 1]
+        sl = (lambda lst: lst[slot]) if slot is not None else (lambda lst: None)
         self._ffn_bwd(bb, pre, bb.e_x1[l], bb.e_h[l], bb.e_s2[l], st[2:4], "norm2", sd("drop2"), bf,
-                      rmask=bb.e_rmask[l] if bb.e_rmask_ok[l] else None)
+                      rmask=bb.e_rmask[l] if bb.e_rmask_ok[l] else None, dy=sl(bb.g_dyf), dh=sl(bb.g_dh))
         self._attn_block_bwd(bb, pre, x_in, bb.e_qkv[l], bb.e_o[l], bb.e_lse[l], st[0:2], bb.e_s1[l], "norm1",
-                             (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.e_mask[l], last=(l == 0))
+                             (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.e_mask[l], last=(l == 0),
+                             dy=sl(bb.g_dyo), dqkv=sl(bb.g_dqkv))
 
     def _dec_layer_bwd(self, bb, l, T, bf, first):
         D, ws = self.D, bb.ws
