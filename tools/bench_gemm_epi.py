@@ -72,5 +72,12 @@ G = torch.zeros(4096, 4096, dtype=torch.float32, device=dev)
 for beta in (0.0, 1.0):
     s = t(lambda: K.gemm(dY, X, G, 4096, 4096, M, a_kmajor=False, b_kmajor=False, beta=beta))
     rows.append(("dW  4096^2 nosplit b%d" % beta, 2 * M * 4096 * 4096, s))
+# the same problem with K-major operands (forward layout): isolates the cost of
+# the MN-major (transpose-read) operand path
+At, Bt = dY.t().contiguous(), X.t().contiguous()
+s = t(lambda: K.gemm(At, Bt, G, 4096, 4096, M, a_kmajor=True, b_kmajor=True))
+rows.append(("TT  4096^2 K=16384", 2 * M * 4096 * 4096, s))
+s = t(lambda: K.gemm(At, X, G, 4096, 4096, M, a_kmajor=True, b_kmajor=False))
+rows.append(("TN  4096^2 K=16384", 2 * M * 4096 * 4096, s))
 for nm, fl, s in rows:
     print("%-22s %8.1f TF/s %9.1f us" % (nm, fl / s / 1e12, s * 1e6))
