@@ -2,7 +2,8 @@
 
 One step = one reference training step (utils/training_utils.py:56-80) on one
 batch of B=128 windows x T=128 frames per GPU: zero_grad -> forward -> fused
-Loss -> backward (+ RCCL gradient all-reduce when n>1) -> clip(2.0) + Adam.
+Loss -> backward -> clip(2.0) + Adam; when n>1 the optimizer is sharded
+(RCCL reduce-scatter of the gradients, Adam on 1/n, all-gather of the weights).
 bf16 compute, dropout 0.3 on, synthetic seeded inputs of the reference shapes
 (features [B,T,256] f32, targets [B,T,61] f32, already resident in HBM).
 
@@ -14,7 +15,9 @@ kernel (nstl GEMM: ~97% of the step's FLOPs): HIP events around every GEMM launc
 of the last --gemm-sample-steps timed steps (events on all ~270 launches of every
 step would add ~1.7 ms/step), on the stream it runs on; achieved = algorithmic
 GEMM FLOPs / GEMM time.  `cpu_baseline` times the fp32 CPU oracle step (the reference step
-restated in torch-CPU) on a bounded sample on rank 0.
+restated in torch-CPU) on a bounded sample on rank 0.  `parity` is the metric's
+"MSE vs ref": forward output of the full 228M config vs the fp32 CPU oracle on
+the same 2-window batch and seeded weights (fp32 mode gated at 1e-3; bf16 reported).
 """
 import argparse
 import json
@@ -81,6 +84,37 @@ def cpu_baseline(cfg, T, budget_s=20.0):
                       % (B, T, n)}
 
 
+def fwd_parity(cfg, dev, T, windows=2):
+    """BASELINE metric's "MSE vs ref" (SURVEY.md 8(d)(i)): forward output of the
+    full 228M config (all 8+8 layers) vs the fp32 CPU oracle on the same batch
+    and the same seeded weights, in fp32 parity mode (gate <= 1e-3) and in the
+    bf16 mode the bench trains in (reported, not gated)."""
+    from oracle import model_ref
+    from neurosync_trainer_lite_amd.utils.model_utils import build_model
+    H = cfg["num_heads"]
+    params = model_ref.seeded_params(model_ref.param_shapes(cfg["input_dim"], cfg["hidden_dim"], cfg["n_layers"],
+                                                            cfg["output_dim"]), 11)
+    g = torch.Generator().manual_seed(12)
+    src = torch.randn(windows, T, cfg["input_dim"], generator=g)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        ref = model_ref.seq2seq_forward(params, src, H).double()
+    out = {"windows": windows, "frames": windows * T, "oracle_s": round(time.perf_counter() - t0, 2), "gate": 1e-3}
+    for tag, amp in (("fp32", False), ("bf16", True)):
+        c = dict(cfg, use_amp=amp, dropout=0.0)
+        m = build_model(c, dev)
+        m.load_state_dict(params, strict=True)
+        m.eval()
+        with torch.no_grad():
+            pred = m(src.to(dev)).double().cpu()
+        out["mse_" + tag] = float(((pred - ref) ** 2).mean())
+        out["rel_" + tag] = float((pred - ref).norm() / ref.norm())
+        del m
+        torch.cuda.empty_cache()
+    out["pass"] = out["mse_fp32"] <= out["gate"]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,6 +123,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the forward-MSE-vs-oracle field")
     ap.add_argument("--gemm-sample-steps", type=int, default=2,
                     help="timed steps (the last ones) whose GEMM launches carry HIP timing events")
     ap.add_argument("--feature-steps", type=int, default=10,
@@ -286,6 +321,9 @@ def main():
         }
         if feat is not None:
             out["feature_inclusive"] = feat
+        if world == 1 and not args.no_parity:
+            out["parity"] = fwd_parity(cfg, dev, T)
+            log("parity: %s" % out["parity"])
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, T)
         print(json.dumps(out), flush=True)
