@@ -47,7 +47,12 @@ def gemm_traffic():
     """Per-launch HBM bytes of the GEMM family from the committed PMC summary
     (tools/run_pmc_traffic.sh -> profiles/*_gemm_traffic.json), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_gemm_traffic.json")))
+    import re
+
+    def version(f):  # r1_v10 after r1_v9 (natural order); untagged files first
+        m = re.search(r"r(\d+)_v(\d+)_gemm_traffic", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_gemm_traffic.json")), key=version)
     if not files:
         return None, None
     d = json.load(open(files[-1]))

@@ -38,6 +38,8 @@ x, x4 = r(M, D), r(M, F)
 for name, n, k, kw in (
         ("fwd out  BIAS", D, D, dict(epilogue=K.EPI_BIAS)),
         ("fwd ffn2 BIAS", D, F, dict(epilogue=K.EPI_BIAS)),
+        ("fwd ffn1 BIAS", F, D, dict(epilogue=K.EPI_BIAS)),
+        ("fwd ffn1 RELU p0", F, D, dict(epilogue=K.EPI_BIAS_RELU_DROP, p_drop=0.0, seed=5)),
         ("fwd ffn1 RELU_DROP", F, D, dict(epilogue=K.EPI_BIAS_RELU_DROP, p_drop=0.3, seed=5)),
         ("fwd qkv  ROPE", 3 * D, D, dict(epilogue=K.EPI_BIAS_ROPE, rope=(cs, sn, T, 64), rope_cols=2 * D)),
         ("fwd kvc  ROPE", 2 * D, D, dict(epilogue=K.EPI_BIAS_ROPE, rope=(cs, sn, T, 64), rope_cols=D))):
@@ -46,9 +48,15 @@ for name, n, k, kw in (
     Y = torch.empty(M, n, dtype=bf, device=dev)
     s = t(lambda: K.gemm(X, W, Y, M, n, k, bias=b, **kw))
     rows.append((name, 2 * M * n * k, s))
+    if "RELU_DROP" in name:
+        nw = K.gemm_relu_mask_words(X, W, Y, M, n, k, bias=b, **kw)
+        rm = torch.empty(nw, dtype=torch.int64, device=dev)
+        s = t(lambda: K.gemm(X, W, Y, M, n, k, bias=b, relu_mask=rm, **kw))
+        rows.append((name + "+mask", 2 * M * n * k, s))
 h = torch.relu(r(M, F))
 for name, n, k, out_dt, kw in (
         ("dX  out  bf16", D, D, bf, dict(beta=0.0)),
+        ("dX  ffn2 bf16", D, F, bf, dict(beta=0.0)),
         ("dX  ffn2 DRELU", D, F, bf, dict(beta=0.0, epilogue=K.EPI_DRELU_DROP, aux=h, ld_aux=F, p_drop=0.3)),
         ("dX  ffn1 F32 beta1", F, D, torch.float32, dict(beta=1.0)),
         ("dX  qkv  F32 beta1", 3 * D, D, torch.float32, dict(beta=1.0)),
@@ -58,6 +66,16 @@ for name, n, k, out_dt, kw in (
     dX = torch.zeros(M, k, dtype=out_dt, device=dev)
     s = t(lambda: K.gemm(dY, W, dX, M, k, n, a_kmajor=True, b_kmajor=False, **kw))
     rows.append((name, 2 * M * n * k, s))
+    if "DRELU" in name:
+        nw = K.gemm_relu_mask_words(dY, W, dX, M, k, n, a_kmajor=True, b_kmajor=False, **kw)
+        rm = torch.zeros(nw, dtype=torch.int64, device=dev) - 1
+        kw2 = dict(kw, relu_mask=rm)
+        s = t(lambda: K.gemm(dY, W, dX, M, k, n, a_kmajor=True, b_kmajor=False, **kw2))
+        rows.append((name + "+mask", 2 * M * n * k, s))
+        nr = K.gemm_colsum_rows(dY, W, dX, M, k, n, a_kmajor=True, b_kmajor=False, **kw2)
+        cp = torch.empty(nr, k, dtype=torch.float32, device=dev)
+        s = t(lambda: K.gemm(dY, W, dX, M, k, n, a_kmajor=True, b_kmajor=False, colsum_part=cp, **kw2))
+        rows.append((name + "+mask+csum", 2 * M * n * k, s))
 ws = torch.empty(16 * D * D, dtype=torch.float32, device=dev)
 for name, n, k, split in (("dW  out  split8", D, D, 8), ("dW  out  split16", D, D, 16),
                           ("dW  qkv  split5", 3 * D, D, 5), ("dW  ffn1 split4", F, D, 4)):
