@@ -607,6 +607,217 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused backward (bf16, T <= 128): ONE workgroup per (b, h) produces dQ, dK and
+// dV, so Q, dO, K and V are read once (the split kernels read Q, K, V and dO
+// twice: 384 -> 256 MB per call at the 228M shape).  A wave owns 16 keys, as in
+// attn_bwd_dkv: S / dP with query rows, P^T / dS^T in registers -> dV, dK.  The
+// dS^T fragments (bf16, what the dK product consumed) stay in registers until
+// every wave is done with the Q / dO images, then go to an LDS image over them
+// (rows = keys, the reduction index of dQ = dS K), and each wave computes dQ for
+// 16 queries from that image and the K image.  LDS: Q | dO (later dS^T, 32 KB),
+// K (16 KB), lse / D (1 KB); the output staging and bias partials reuse the
+// first 22 KB once dQ is done.  49 KB: up to 3 workgroups per CU by LDS.
+//   prologue: DMA Q, dO, K images; own K / V rows and own-query O rows from
+//             global; lse -> LDS; barrier; D = rowsum(dO * O) of own queries
+//             (dO from its image) -> LDS; barrier
+//   phase 1 : S, dP over the 8 query tiles; dV += P_drop^T dO, dK += dS^T Q
+//   phase 2 : barrier; dS^T -> image; barrier; dQ = dS K
+//   stores  : barrier; dQ, dK, dV rows (+ bias column sums, last wave out)
+constexpr int FUSED_MAX_T = 128;
+constexpr int FUSED_DS_RB = FUSED_MAX_T * 2;  // dS^T image row: 128 queries (bf16)
+typedef ImgMN<FUSED_DS_RB> DsImg;
+
+__global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p) {
+  typedef bf16x8 Frag;
+  constexpr int RBK = DH * 2;
+  typedef ImgK<RBK> Img;
+  constexpr int NW = BWD_NT / 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int T_ = p.T, nkt = T_ / 16;
+  char* Qimg = smem;                                           // [128][128 B]
+  char* Dimg = Qimg + FUSED_MAX_T * RBK;                       // [128][128 B]
+  char* DSimg = smem;                                          // over Q | dO after phase 1
+  char* Kimg = smem + 2 * FUSED_MAX_T * RBK;                   // [128][128 B]
+  float* lse_s = (float*)(Kimg + FUSED_MAX_T * RBK);
+  float* d_s = lse_s + FUSED_MAX_T;
+  unsigned* arrived = (unsigned*)(d_s + FUSED_MAX_T);
+  char* scratch = smem;                                        // after phase 2: [NW][16][RBK]
+  float* red = (float*)(smem + NW * 16 * RBK);                 // after phase 2: [3][NW][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int64_t tok0 = (int64_t)b * T_;
+  const int k0 = w * 16;     // this wave's keys (phase 1) and queries (D, phase 2)
+  const bool act = k0 < T_;
+  dma_rows<RBK, NW>(Qimg, p.q + (tok0 * p.q_ld + h * DH) * 2, p.q_ld * 2, T_, w, lane);
+  dma_rows<RBK, NW>(Dimg, p.dout + (tok0 * p.dout_ld + h * DH) * 2, p.dout_ld * 2, T_, w, lane);
+  dma_rows<RBK, NW>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * 2, p.k_ld * 2, T_, w, lane);
+  for (int i = tid; i < T_; i += BWD_NT) lse_s[i] = p.lse[(int64_t)bh * T_ + i] * LOG2E;
+  if (tid == 0) *arrived = 0u;
+  Frag fk[2], fv[2], oo[2];
+  if (act) {
+    const int r = k0 + c;
+    const bf16* krow = (const bf16*)p.k + (tok0 + r) * p.k_ld + h * DH;
+    const bf16* vrow = (const bf16*)p.v + (tok0 + r) * p.v_ld + h * DH;
+    const bf16* orow = (const bf16*)p.o + (tok0 + r) * p.o_ld + h * DH;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      gload_frag<bf16>(fk[u], krow, 32 * u + 8 * g);
+      gload_frag<bf16>(fv[u], vrow, 32 * u + 8 * g);
+      gload_frag<bf16>(oo[u], orow, 32 * u + 8 * g);
+    }
+  }
+  // stored keep bits for this wave's 16 keys: lane 4*qt + r holds word (qt, k0/16, r)
+  const bool use_mask = p.thresh && p.mask;
+  uint64_t mword = 0;
+  if (act && use_mask && (lane >> 2) < nkt) mword = p.mask[mask_word(bh, nkt, lane >> 2, k0 >> 4, lane & 3)];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (act) {  // D of queries k0 + c (dO from its image, O from registers)
+    float dpart = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      Frag fo;
+      frag_row<Img>(fo, Dimg, k0 + c, 32 * u + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dpart += (float)fo[e] * (float)oo[u][e];
+    }
+    dpart += __shfl_xor(dpart, 16);
+    dpart += __shfl_xor(dpart, 32);
+    if (g == 0) d_s[k0 + c] = dpart;
+  }
+  __syncthreads();
+
+  const float c2 = p.scale * LOG2E;
+  f32x4 dk[4], dv[4];
+  Frag dsf[FUSED_MAX_T / 32];  // dS^T fragments (acc_frag order), kept for dQ
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < FUSED_MAX_T / 32; ++j) {  // 32-query chunks
+      if (j < nkt / 2) {
+        f32x4 pdv[2], dsv[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int qt = 2 * j + u;
+          f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+          Frag fb;
+          frag_row<Img>(fb, Qimg, qt * 16 + c, 8 * g);
+          mma16(st, fb, fk[0]);
+          frag_row<Img>(fb, Qimg, qt * 16 + c, 32 + 8 * g);
+          mma16(st, fb, fk[1]);
+          frag_row<Img>(fb, Dimg, qt * 16 + c, 8 * g);
+          mma16(dpt, fb, fv[0]);
+          frag_row<Img>(fb, Dimg, qt * 16 + c, 32 + 8 * g);
+          mma16(dpt, fb, fv[1]);
+          // st[r] / dpt[r]: S / dP at (query 16qt + 4g + r, key k0 + c)
+          uint32_t nib = 0;
+          if (use_mask) nib = (uint32_t)(shfl64(mword, 4 * qt + (lane & 3)) >> (16 * (c >> 2) + 4 * g));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = qt * 16 + 4 * g + r;
+            const float pv = exp2f(st[r] * c2 - lse_s[q]);
+            float pdr = pv, dpd = dpt[r];
+            if (p.thresh) {
+              const bool keep = use_mask ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
+              pdr = keep ? pv * p.inv_keep : 0.f;
+              dpd = keep ? dpd * p.inv_keep : 0.f;
+            }
+            pdv[u][r] = pdr;
+            dsv[u][r] = pv * (dpd - d_s[q]);
+          }
+        }
+        const Frag fa1 = acc_frag<bf16>(pdv[0], pdv[1]);  // P_drop^T, row = key k0 + c
+        dsf[j] = acc_frag<bf16>(dsv[0], dsv[1]);          // dS^T
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          Frag fb;
+          frag_col2<Img>(fb, Dimg, dt * 16, 32 * j, lane);
+          mma16(dv[dt], fa1, fb);
+          frag_col2<Img>(fb, Qimg, dt * 16, 32 * j, lane);
+          mma16(dk[dt], dsf[j], fb);
+        }
+      }
+    }
+  }
+  __syncthreads();  // every wave is done with the Q / dO images
+  if (act) {
+    // dS^T row = key k0 + c; fragment j holds queries 32j + 4g + 0..3 and 32j + 16 + 4g + 0..3
+#pragma unroll
+    for (int j = 0; j < FUSED_MAX_T / 32; ++j) {
+      if (j < nkt / 2) {
+        const bf16x8 f = dsf[j];
+        *(bf16x4*)(DSimg + DsImg::off(k0 + c, (32 * j + 4 * g) * 2)) = (bf16x4){f[0], f[1], f[2], f[3]};
+        *(bf16x4*)(DSimg + DsImg::off(k0 + c, (32 * j + 16 + 4 * g) * 2)) = (bf16x4){f[4], f[5], f[6], f[7]};
+      }
+    }
+  }
+  __syncthreads();
+  // dQ(query k0 + 4g + r, d = 16dt + c) = sum_key dS(query, key) K(key, d)
+  f32x4 dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < FUSED_MAX_T / 32; ++j) {
+      if (j < nkt / 2) {
+        Frag fa;
+        frag_col2<DsImg>(fa, DSimg, k0, 32 * j, lane);  // dS, row = query k0 + c
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          Frag fb;
+          frag_col2<Img>(fb, Kimg, dt * 16, 32 * j, lane);
+          mma16(dq[dt], fa, fb);
+        }
+      }
+    }
+  }
+  __syncthreads();  // the dS^T / K images become output staging
+  float vq[4][4], vk[4][4], vv[4][4];
+  float* bias_row = p.dbias ? p.dbias + (int64_t)b * 3 * p.H * DH : nullptr;
+  if (act) {  // wave-uniform: rope_back's lane shuffles see the whole wave
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = k0 + 4 * g + r;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int d = dt * 16 + c;
+        float xq = dq[dt][r] * p.scale, xk = dk[dt][r] * p.scale;
+        if (p.rope_q) xq = rope_back(xq, row, d, p.rope_cos, p.rope_sin);
+        if (p.rope_k) xk = rope_back(xk, row, d, p.rope_cos, p.rope_sin);
+        vq[dt][r] = xq;
+        vk[dt][r] = xk;
+        vv[dt][r] = dv[dt][r];
+      }
+    }
+    char* scr = scratch + w * 16 * RBK;
+    const int64_t r0 = tok0 + k0;
+    store_tile16x64<bf16>(vq, scr, p.dq + (r0 * p.dq_ld + h * DH) * 2, p.dq_ld, lane);
+    store_tile16x64<bf16>(vk, scr, p.dk + (r0 * p.dk_ld + h * DH) * 2, p.dk_ld, lane);
+    store_tile16x64<bf16>(vv, scr, p.dv + (r0 * p.dv_ld + h * DH) * 2, p.dv_ld, lane);
+  }
+  if (bias_row) {
+    if (act) {
+      wave_colsum16x64<bf16>(vq, red, w, lane);
+      wave_colsum16x64<bf16>(vk, red + NW * 64, w, lane);
+      wave_colsum16x64<bf16>(vv, red + 2 * NW * 64, w, lane);
+    } else {
+      red[w * 64 + lane] = 0.f;
+      red[NW * 64 + w * 64 + lane] = 0.f;
+      red[2 * NW * 64 + w * 64 + lane] = 0.f;
+    }
+    if (last_to_arrive(arrived, NW, lane)) {
+#pragma unroll
+      for (int m = 0; m < 3; ++m) wave_sum_out(red + m * NW * 64, NW, bias_row + m * p.H * DH + h * DH, lane);
+    }
+  }
+}
+constexpr size_t FUSED_LDS = 3 * FUSED_MAX_T * DH * 2 + 2 * FUSED_MAX_T * 4 + 16;
+static_assert(8 * 16 * DH * 2 + 3 * 8 * 64 * 4 <= 3 * FUSED_MAX_T * DH * 2, "staging must fit in the images");
+
 size_t fwd_lds_bytes(int T, int esz) {  // K, V images + per-wave output staging
   return (size_t)2 * T * DH * esz + (FWD_NT / 64) * 16 * DH * (size_t)esz;
 }
@@ -835,6 +1046,14 @@ bool use_fast(const nstl_attn_args* a) {
   return a->dh == DH && a->T % 32 == 0 && a->T <= (a->dtype == NSTL_BF16 ? 256 : 128);
 }
 
+// the fused backward (bf16, T <= 128); NSTL_ATTN_BWD=split selects the two
+// kernels (A/B comparisons; read per call so a test can switch it)
+bool use_fused_bwd(const nstl_attn_args* a) {
+  const char* e = getenv("NSTL_ATTN_BWD");
+  if (e && e[0] == 's') return false;
+  return use_fast(a) && a->dtype == NSTL_BF16 && a->T <= FUSED_MAX_T;
+}
+
 int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   NSTL_CHECK_ARG(a != nullptr, "nstl_attn: null args");
   NSTL_CHECK_ARG(a->dtype == NSTL_F32 || a->dtype == NSTL_BF16, "nstl_attn: bad dtype");
@@ -935,6 +1154,8 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
     if ((rc = launch(attn_bwd_dq_generic<float>, grid, lq, st, p, "nstl_attn_bwd generic dq"))) return rc;
     return launch(attn_bwd_dkv_generic<float>, grid, lkv, st, p, "nstl_attn_bwd generic dkv");
   }
+  if (use_fused_bwd(a))
+    return launch(attn_bwd_fused_kernel, dim3(1, a->B * a->H), FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
   dim3 grid((a->T + BWD_ROWS - 1) / BWD_ROWS, a->B * a->H);
   const size_t lds = bwd_lds_bytes(a->T, esz);
   if (a->dtype == NSTL_BF16) {

@@ -414,6 +414,48 @@ def test_attention_bias_partials(dt, T):
     assert K.attn_bias_rows(a) == 0
 
 
+@pytest.mark.parametrize("T", [32, 96, 128])
+def test_attention_bwd_fused_matches_split(T, monkeypatch):
+    """The fused one-workgroup-per-(b, h) backward (bf16, T <= 128) against the split
+    dQ / dK+dV kernels on the same forward: dropout from stored keep bits, RoPE^T,
+    bias partials.  T=96 leaves two waves of the workgroup without keys."""
+    B, H, dh, p = 3, 2, 64, 0.3
+    M, D = B * T, H * dh
+    dt = torch.bfloat16
+    qkv = rnd(M, 3 * D, dtype=dt, scale=0.5, seed=120)
+    do = rnd(M, D, dtype=dt, seed=121)
+    o = torch.empty(M, D, dtype=dt, device=DEV)
+    lse = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
+    mask = torch.zeros(B * H * T * T // 64, dtype=torch.int64, device=DEV)
+    cs, sn = rotation_tables(T, dh, DEV)
+    a = K.attn_args(K.BF16, B, T, H, qkv.data_ptr(), 3 * D, qkv[:, D:].data_ptr(), 3 * D,
+                    qkv[:, 2 * D:].data_ptr(), 3 * D, o.data_ptr(), D, lse.data_ptr(), p, 7, dh=dh)
+    a.mask_bits = mask.data_ptr()
+    K.attn_fwd(a)
+    dsum = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
+    a.dout, a.dout_ld = do.data_ptr(), D
+    a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
+    a.dsum = dsum.data_ptr()
+    rows = K.attn_bias_rows(a)
+    res = []
+    for mode in ("split", "fused"):
+        monkeypatch.setenv("NSTL_ATTN_BWD", mode)
+        dqkv = torch.full((M, 3 * D), float("nan"), dtype=dt, device=DEV)
+        part = torch.full((rows, 3 * D), float("nan"), device=DEV)
+        a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dqkv.data_ptr(), 3 * D, dqkv[:, D:].data_ptr(), 3 * D,
+                                                        dqkv[:, 2 * D:].data_ptr(), 3 * D)
+        a.dbias_part = part.data_ptr()
+        K.attn_bwd(a)
+        torch.cuda.synchronize()
+        res.append((dqkv, part))
+    (ds, ps), (df, pf) = res
+    assert torch.isfinite(f64(df)).all() and torch.isfinite(f64(pf)).all()
+    for i, nm in enumerate(("dq", "dk", "dv")):
+        check(df[:, i * D:(i + 1) * D], ds[:, i * D:(i + 1) * D], 1e-2, "fused " + nm)
+    check(pf, f64(df).view(B, T, 3 * D).sum(1), 1e-5, "fused bias partials = column sums of the stored grads")
+    check(pf, ps, 1e-2, "fused vs split bias partials")
+
+
 def test_attention_rejects_bad_shapes():
     t = torch.zeros(64, 3 * 64, device=DEV)
     lse = torch.zeros(64, device=DEV)
