@@ -156,6 +156,13 @@ int nstl_reduce_rows(const float* part, int n_part, int cols, float* out, float 
 /* the same over a column window of a wider matrix: rows ld floats apart */
 int nstl_reduce_rows_strided(const float* part, int64_t ld, int n_part, int cols, float* out, float beta,
                              void* stream);
+/* Several independent row reductions in ONE launch (a backward layer's LayerNorm
+ * and bias-gradient partials): out[j] = beta*out[j] + sum_p part[p*ld + j]. */
+#define NSTL_REDUCE_BATCH_MAX 16
+typedef struct nstl_reduce_job {
+  const float* part; int64_t ld; int n_part; int cols; float* out; float beta;
+} nstl_reduce_job;
+int nstl_reduce_rows_batch(const nstl_reduce_job* jobs, int n, void* stream);
 /* Three such reductions in one launch: matrix m at part + m*mat_stride -> out_m
  * (LayerNorm backward's dgamma / dbeta / fused bias-grad partials). */
 int nstl_reduce_rows3(const float* part, int64_t mat_stride, int n_mat, int n_part, int cols, float* out0,

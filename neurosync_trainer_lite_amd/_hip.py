@@ -86,12 +86,19 @@ class AdamArgs(ctypes.Structure):
     ]
 
 
+class ReduceJob(ctypes.Structure):
+    _fields_ = [("part", _vp), ("ld", _i64), ("n_part", _i32), ("cols", _i32), ("out", _vp), ("beta", _f32)]
+
+
+REDUCE_BATCH_MAX = 16
+
 # every symbol include/nstl.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "nstl_gemm", "nstl_gemm_grouped", "nstl_gemm_colsum_rows", "nstl_gemm_relu_mask_words",
     "nstl_gemm_workspace_bytes",
     "nstl_attn_fwd", "nstl_attn_bwd", "nstl_attn_bias_rows", "nstl_ln_fwd", "nstl_ln_bwd",
-    "nstl_reduce_rows", "nstl_reduce_rows_strided", "nstl_reduce_rows3", "nstl_colsum", "nstl_rope",
+    "nstl_reduce_rows", "nstl_reduce_rows_strided", "nstl_reduce_rows3", "nstl_reduce_rows_batch",
+    "nstl_colsum", "nstl_rope",
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
     "nstl_features", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
     "nstl_version",
@@ -127,6 +134,7 @@ def lib():
         L.nstl_reduce_rows.argtypes = [_vp, _i32, _i32, _vp, _f32, _vp]
         L.nstl_reduce_rows_strided.argtypes = [_vp, _i64, _i32, _i32, _vp, _f32, _vp]
         L.nstl_reduce_rows3.argtypes = [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]
+        L.nstl_reduce_rows_batch.argtypes = [P(ReduceJob), _i32, _vp]
         L.nstl_colsum.argtypes = [_i32, _vp, _i64, _i32, _i32, _vp, _vp, _f32, _vp]
         L.nstl_rope.argtypes = [_i32, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _vp]
         L.nstl_loss_fwd_bwd.argtypes = [P(LossArgs), _vp]
@@ -268,6 +276,19 @@ def reduce_rows3(part, n_part, cols, outs, beta, stream=None):
     ptrs = [o.data_ptr() for o in outs] + [None] * (3 - len(outs))
     check(lib().nstl_reduce_rows3(part.data_ptr(), part.stride(0), len(outs), n_part, cols, ptrs[0], ptrs[1], ptrs[2],
                                   beta, stream if stream is not None else stream_of()), "nstl_reduce_rows3")
+
+
+def reduce_rows_batch(jobs, stream=None):
+    """jobs: (part, ld, n_part, cols, out, beta) with part a tensor (its first
+    element is row 0, column 0 of the job) and out an f32 tensor; one launch."""
+    if not jobs:
+        return
+    if len(jobs) > REDUCE_BATCH_MAX:
+        raise RuntimeError("nstl_reduce_rows_batch: at most %d jobs (got %d)" % (REDUCE_BATCH_MAX, len(jobs)))
+    arr = (ReduceJob * len(jobs))(*[ReduceJob(ptr(part), ld, n_part, cols, out.data_ptr(), beta)
+                                    for part, ld, n_part, cols, out, beta in jobs])
+    check(lib().nstl_reduce_rows_batch(arr, len(jobs), stream if stream is not None else stream_of()),
+          "nstl_reduce_rows_batch")
 
 
 def reduce_rows(part, n_part, cols, out, beta, stream=None):

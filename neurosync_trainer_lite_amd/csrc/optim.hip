@@ -159,14 +159,22 @@ __global__ __launch_bounds__(NT) void colsum_vec_kernel(const T* x, int64_t ld, 
   }
 }
 
+// any cols / ld (e.g. the 61-column head gradient): block = 64 columns x 4 row
+// groups over a 256-row chunk, loads unrolled so several rows are in flight
 template <typename T>
-__global__ void colsum_kernel(const T* x, int64_t ld, int rows, int cols, float* partial) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= cols) return;
+__global__ __launch_bounds__(NT) void colsum_kernel(const T* x, int64_t ld, int rows, int cols, float* partial) {
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cl;
   const int r0 = blockIdx.y * COLSUM_ROWS, r1 = min(rows, r0 + COLSUM_ROWS);
   float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += to_f32(x[(int64_t)r * ld + j]);
-  partial[(int64_t)blockIdx.y * cols + j] = s;
+  if (j < cols) {
+#pragma unroll 8
+    for (int r = r0 + rg; r < r1; r += NT / 64) s += to_f32(x[(int64_t)r * ld + j]);
+  }
+  __shared__ float red[NT / 64][64];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && j < cols) partial[(int64_t)blockIdx.y * cols + j] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
 }
 
 // out[j] = beta*out[j] + sum_k part[k][j]: block = 64 columns x 4 row groups
@@ -285,7 +293,7 @@ extern "C" int nstl_colsum(int dtype, const void* x, int64_t ld, int rows, int c
     else
       hipLaunchKernelGGL(colsum_vec_kernel<float>, grid, dim3(NT), 0, st, (const float*)x, ld, rows, cols, partial);
   } else {
-    dim3 grid((cols + NT - 1) / NT, nchunk);
+    dim3 grid((cols + 63) / 64, nchunk);
     if (dtype == NSTL_BF16)
       hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(NT), 0, st, (const bf16*)x, ld, rows, cols, partial);
     else
@@ -329,6 +337,65 @@ extern "C" int nstl_reduce_rows3(const float* part, int64_t mat_stride, int n_ma
   hipLaunchKernelGGL(reduce_rows3_kernel, dim3((cols + 63) / 64, n_mat), dim3(1024), 0, (hipStream_t)stream, part,
                      mat_stride, n_part, cols, out0, out1, out2, beta);
   NSTL_LAUNCH_CHECK("nstl_reduce_rows3");
+  return 0;
+}
+
+// Up to NSTL_REDUCE_BATCH_MAX such reductions (any part / ld / rows / cols)
+// in one launch: block b -> job j with block_end[j-1] <= b < block_end[j]; each
+// block reduces 64 columns of its job with reduce_rows3's order (16 row groups,
+// then the groups in order), so results do not depend on the batching.
+struct ReduceBatch {
+  const float* part[NSTL_REDUCE_BATCH_MAX];
+  int64_t ld[NSTL_REDUCE_BATCH_MAX];
+  float* out[NSTL_REDUCE_BATCH_MAX];
+  int n_part[NSTL_REDUCE_BATCH_MAX];
+  int cols[NSTL_REDUCE_BATCH_MAX];
+  float beta[NSTL_REDUCE_BATCH_MAX];
+  int block_end[NSTL_REDUCE_BATCH_MAX];
+  int n;
+};
+
+__global__ __launch_bounds__(1024) void reduce_batch_kernel(ReduceBatch rb) {
+  int jb = 0;
+  while (jb + 1 < rb.n && (int)blockIdx.x >= rb.block_end[jb]) ++jb;
+  const int blk = blockIdx.x - (jb > 0 ? rb.block_end[jb - 1] : 0);
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = blk * 64 + cl, cols = rb.cols[jb], n_part = rb.n_part[jb];
+  const float* pm = rb.part[jb];
+  const int64_t ld = rb.ld[jb];
+  float s = 0.f;
+  if (j < cols)
+    for (int k = rg; k < n_part; k += 16) s += pm[(int64_t)k * ld + j];
+  __shared__ float red[16][64];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && j < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][cl];
+    float* out = rb.out[jb];
+    const float beta = rb.beta[jb];
+    out[j] = beta != 0.f ? beta * out[j] + t : t;
+  }
+}
+
+extern "C" int nstl_reduce_rows_batch(const nstl_reduce_job* jobs, int n, void* stream) {
+  NSTL_CHECK_ARG(jobs && n >= 1 && n <= NSTL_REDUCE_BATCH_MAX, "nstl_reduce_rows_batch: 1..%d jobs (got %d)",
+                 NSTL_REDUCE_BATCH_MAX, n);
+  ReduceBatch rb;
+  rb.n = n;
+  int blocks = 0;
+  for (int k = 0; k < n; ++k) {
+    const nstl_reduce_job& jb = jobs[k];
+    NSTL_CHECK_ARG(jb.part && jb.out && jb.n_part > 0 && jb.cols > 0 && jb.ld >= jb.cols,
+                   "nstl_reduce_rows_batch: bad job %d", k);
+    rb.part[k] = jb.part; rb.ld[k] = jb.ld; rb.out[k] = jb.out;
+    rb.n_part[k] = jb.n_part; rb.cols[k] = jb.cols; rb.beta[k] = jb.beta;
+    blocks += (jb.cols + 63) / 64;
+    rb.block_end[k] = blocks;
+  }
+  hipLaunchKernelGGL(reduce_batch_kernel, dim3(blocks), dim3(1024), 0, (hipStream_t)stream, rb);
+  NSTL_LAUNCH_CHECK("nstl_reduce_rows_batch");
   return 0;
 }
 

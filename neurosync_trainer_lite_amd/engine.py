@@ -126,7 +126,9 @@ class _Buffers:
             self.dpred = torch.zeros(M, 64, dtype=dt, device=dev)
             self.dsum = e(B * eng.H * T, dtype=f32)  # attention backward rowsum(dO * O)
             # attention backward: per-(batch, 128 rows) column sums of dq | dk | dv (bias grads)
-            self.abias = e(B * ((T + 127) // 128), 3 * D, dtype=f32)
+            # (two: a decoder layer's cross and self attention reduce in one batch)
+            self.abias_slots = [e(B * ((T + 127) // 128), 3 * D, dtype=f32) for _ in range(2)]
+            self.abias = self.abias_slots[0]
             # FFN2 dX (dReLU epilogue): per-128-row column sums of dh (FFN1 bias grad)
             self.hpart = e((M + 127) // 128, Fd, dtype=f32)
             # FFN hidden keep&positive bits (FFN1 epilogue -> FFN2 dX epilogue), 1 bit/element
@@ -141,7 +143,9 @@ class _Buffers:
             self.d_mask = [e(nw, dtype=torch.int64) for _ in range(L)]
             self.d_maskc = [e(nw, dtype=torch.int64) for _ in range(L)]
             self.n_part = max(1, min(256, M // 8))  # LN backward: >= 1 row per wave (8 waves)
-            self.ln_part = e(3, self.n_part, D, dtype=f32)
+            # one per LayerNorm of a layer (3 in a decoder layer): batched reduction
+            self.ln_parts = [e(3, self.n_part, D, dtype=f32) for _ in range(3)]
+            self.ln_part = self.ln_parts[0]
             self.col_part = e((M + 255) // 256, max(Fd, 3 * D, 64), dtype=f32)
             self.ws = e(eng.splitk_ws_elems(M), dtype=f32)
 
@@ -196,6 +200,12 @@ class Seq2SeqEngine:
         # NSTL_RELU_MASK=0: the FFN2 dX epilogue reads the saved hidden h for its
         # dReLU instead of the 1-bit keep&positive mask the FFN1 epilogue writes
         self.relu_mask_on = os.environ.get("NSTL_RELU_MASK", "1") != "0"
+        # NSTL_REDUCE_BATCH=0: each LayerNorm / bias-gradient partial reduction is
+        # its own launch instead of one batched launch per backward layer
+        self.reduce_batch_on = os.environ.get("NSTL_REDUCE_BATCH", "1") != "0"
+        self._red = None           # pending (part, ld, n_part, cols, out, beta) jobs
+        self._ln_slot = 0          # next LayerNorm partial buffer of the layer
+        self._ab_slot = 0          # next attention bias partial buffer of the layer
 
     # ------------------------------------------------------------------ setup
     def _check_shapes(self):
@@ -485,7 +495,7 @@ class Seq2SeqEngine:
         fused = 0 < nrows <= (colsum[0].shape[0] if colsum is not None else 0)
         K.gemm(dy, W, out, m, k, n, colsum_part=colsum[0] if fused else None, stream=self.st, **kw)
         if fused:
-            K.reduce_rows(colsum[0], nrows, k, colsum[1], colsum[2], stream=self.st)
+            self._reduce(colsum[0], k, nrows, k, colsum[1], colsum[2])
         return fused
 
     def _dx_res(self, dy, wname, rows, last=False):
@@ -531,14 +541,22 @@ class Seq2SeqEngine:
         if self._dadd_pending:
             a.dout2 = bb.dadd.data_ptr()
             self._dadd_pending = False
-        a.dgamma_part, a.dbeta_part, a.n_part = bb.ln_part[0].data_ptr(), bb.ln_part[1].data_ptr(), bb.n_part
+        part = bb.ln_part
+        if self._red is not None:
+            part = bb.ln_parts[self._ln_slot]
+            self._ln_slot += 1
+        a.dgamma_part, a.dbeta_part, a.n_part = part[0].data_ptr(), part[1].data_ptr(), bb.n_part
         if bias_of is not None:
-            a.dbranch_part = bb.ln_part[2].data_ptr()
+            a.dbranch_part = part[2].data_ptr()
         K.ln_bwd(a, stream=self.st)
         outs = [self.gb(prefix + ".weight"), self.gb(prefix + ".bias")]
         if bias_of is not None:
             outs.append(self.gb(bias_of))
-        K.reduce_rows3(bb.ln_part, bb.n_part, self.D, outs, bf, stream=self.st)
+        if self._red is not None:
+            for m, out in enumerate(outs):
+                self._reduce(part[m], self.D, bb.n_part, self.D, out, bf)
+        else:
+            K.reduce_rows3(part, bb.n_part, self.D, outs, bf, stream=self.st)
 
     def _attn(self, q, k, v, o, lse, seed, T, B, mask=None):
         a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
@@ -563,6 +581,9 @@ class Seq2SeqEngine:
         a.dsum = self.cur.dsum.data_ptr()
         a.mask_bits = K.ptr(mask)
         part = self.cur.abias
+        if self._red is not None:
+            part = self.cur.abias_slots[self._ab_slot]
+            self._ab_slot += 1
         rows = K.attn_bias_rows(a) if bias and self.fused_bias_on else 0
         fused = 0 < rows <= part.shape[0]
         if fused:
@@ -570,8 +591,30 @@ class Seq2SeqEngine:
         self._guard(dq, dk, dv)
         K.attn_bwd(a, stream=self.st)
         for off, n, out in (bias if fused else ()):
-            K.reduce_rows_strided(part[:, off:], part.stride(0), rows, n, out, bf, stream=self.st)
+            self._reduce(part[:, off:], part.stride(0), rows, n, out, bf)
         return fused
+
+    # ---------------------------------------------- batched row reductions
+    def _reduce(self, part, ld, n_part, cols, out, beta):
+        """out = beta*out + rowsum(part): queued for the layer's batched launch, or now."""
+        if self._red is None:
+            K.reduce_rows_strided(part, ld, n_part, cols, out, beta, stream=self.st)
+            return
+        if len(self._red) == K.REDUCE_BATCH_MAX:
+            self._red_flush(reopen=True)
+        self._red.append((part, ld, n_part, cols, out, beta))
+
+    def _red_open(self):
+        if self.reduce_batch_on:
+            self._red, self._ln_slot, self._ab_slot = [], 0, 0
+
+    def _red_flush(self, reopen=False):
+        """Launch the queued reductions (their partial buffers are free afterwards)."""
+        jobs, self._red = self._red, None
+        if jobs:
+            K.reduce_rows_batch(jobs, stream=self.st)
+        if reopen:
+            self._red = []
 
     # --------------------------------------------------------------- forward
     def _enc_layer(self, bb, l, x, T):
@@ -701,6 +744,7 @@ class Seq2SeqEngine:
         self._side_reads = []
         self.p, self.base_seed = sv["p"], sv["seed"]
         self._dadd_pending = False
+        self._red = None
         bf = 0.0 if self.grads_fresh else 1.0
         M, D, L = bb.M, self.D, self.L
         ws = bb.ws
@@ -718,7 +762,9 @@ class Seq2SeqEngine:
         self._ln_bwd(x_last, bb.decf_stats, "decoder.layer_norm", dres, dres, None, 0, (0, 0), bf)
         ready("decoder.layer_norm.bias")
         for l in reversed(range(L)):
+            self._red_open()
             self._dec_layer_bwd(bb, l, T, bf, first=(l == L - 1))
+            self._red_flush()
             ready("decoder.transformer_decoder.%d.self_attn.v_linear.bias" % l)
         # decoder input x = GPE(mem): dmem += GPE^T(dres)
         cs, sn = self.rope(T, D)
@@ -731,7 +777,9 @@ class Seq2SeqEngine:
         for l in reversed(range(L)):
             if enc_group and self._defer is None:
                 self._defer = []
+            self._red_open()
             self._enc_layer_bwd(bb, l, T, bf, slot=(l % ENC_GROUP) if enc_group else None)
+            self._red_flush()
             if enc_group and l % ENC_GROUP == 0:
                 self._dw_flush(ws)
             if not enc_group or l % ENC_GROUP == 0:

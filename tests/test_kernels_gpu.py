@@ -785,3 +785,21 @@ def test_gemm256_epilogues():
     kept = h[pos] != 0
     assert abs(kept.double().mean().item() - 0.7) < 0.01
     torch.testing.assert_close(h[pos][kept], (torch.relu(y)[pos][kept] / 0.7), rtol=1e-2, atol=1e-3)
+
+
+def test_reduce_rows_batch():
+    """nstl_reduce_rows_batch: jobs of different shapes, strides and betas in one
+    launch give exactly the per-job column sums (reduce_rows3's order)."""
+    jobs, refs = [], []
+    for k, (n_part, cols, ld, beta) in enumerate([(256, 1024, 1024, 0.0), (128, 3072, 3072, 1.0),
+                                                  (17, 61, 64, 0.5), (128, 1024, 3072, 0.0)]):
+        part = rnd(n_part, ld, seed=200 + k)
+        out = rnd(cols, seed=300 + k)
+        refs.append(beta * f64(out) + f64(part[:, :cols]).sum(0))
+        jobs.append((part, ld, n_part, cols, out, beta))
+    K.reduce_rows_batch(jobs)
+    torch.cuda.synchronize()
+    for k, (job, ref) in enumerate(zip(jobs, refs)):
+        check(job[4], ref, 1e-6, "batched reduce job %d" % k)
+    with pytest.raises(RuntimeError, match="jobs"):
+        K.reduce_rows_batch(jobs * 5)

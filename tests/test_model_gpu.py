@@ -223,3 +223,58 @@ def test_bf16_grouped_weight_gradients_match_split_k(monkeypatch):
     assert worst < 1e-5, worst
     dec = [k for k in grads[0] if k.startswith("decoder.transformer_decoder.") and k.endswith("weight")]
     assert len(dec) > 0 and all(grads[0][k].abs().sum() > 0 for k in dec)
+
+
+def test_bf16_batched_reductions_match_per_call(monkeypatch):
+    """LayerNorm and bias-gradient partials reduced in one batched launch per backward
+    layer (default) equal the per-call reductions: LayerNorm gamma/beta bit-exact
+    (same summation order), bias gradients up to f32 summation order."""
+    grads = []
+    for batch in ("1", "0"):
+        monkeypatch.setenv("NSTL_REDUCE_BATCH", batch)
+        cfg, model, crit, opt, params = make(256, 4, 2, 11, amp=True, dropout=0.1)
+        torch.manual_seed(5)
+        g = torch.Generator().manual_seed(6)
+        src = torch.randn(4, 128, 256, generator=g).to(DEV)
+        trg = (torch.randn(4, 128, 61, generator=g) * 20).to(DEV)
+        model.train()
+        opt.zero_grad()
+        crit(model(src), trg).backward()
+        torch.cuda.synchronize()
+        grads.append({k: p.grad.detach().double().cpu().clone() for k, p in model.named_parameters()})
+    worst = max(rel(grads[0][k], grads[1][k]) for k in grads[0])
+    assert worst < 1e-5, worst
+    ln = [k for k in grads[0] if ".norm" in k]
+    assert len(ln) > 0 and all(torch.equal(grads[0][k], grads[1][k]) for k in ln)
+
+
+def test_long_clip_t256_parity():
+    """BASELINE config C5's sequence length (T=256, 2x the 228M config's window) at
+    full width (D=1024, H=16), one layer: the fp32 parity-mode forward against the
+    oracle (the generic attention kernels) and a bf16 training step (the MFMA
+    attention kernels, T=256 scores per query) against the oracle's gradients."""
+    D, H, L, T = 1024, 16, 1, 256
+    rng = np.random.default_rng(3)
+    src = torch.tensor(rng.standard_normal((2, T, 256)).astype(np.float32))
+    trg = torch.tensor((rng.standard_normal((2, T, 61)) * 20).astype(np.float32))
+    cfg, model, crit, opt, params = make(D, H, L, 7, amp=False)
+    model.eval()
+    with torch.no_grad():
+        pred = model(src.to(DEV))
+        ref = model_ref.seq2seq_forward(params, src, H)
+    assert rel(pred, ref) < 1e-4
+    assert ((pred.cpu().double() - ref.double()) ** 2).mean().item() < 1e-3
+    cfg, model, crit, opt, params = make(D, H, L, 7, amp=True)
+    model.train()
+    opt.zero_grad()
+    pred = model(src.to(DEV))
+    loss = crit(pred, trg.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    oracle = model_ref.OracleTrainer(params, H)
+    o_loss, o_norm, o_pred = oracle.step(src, trg)
+    assert rel(pred.detach(), o_pred) < 3e-2
+    assert abs(loss.item() - o_loss.item()) < 2e-2 * abs(o_loss.item())
+    named = dict(model.named_parameters())
+    for k, og in oracle_grads(oracle, list(params)).items():
+        assert rel(named[k].grad, og) < 0.1, k
