@@ -18,6 +18,9 @@ GEMM FLOPs / GEMM time.  `cpu_baseline` times the fp32 CPU oracle step (the refe
 restated in torch-CPU) on a bounded sample on rank 0.  `parity` is the metric's
 "MSE vs ref": forward output of the full 228M config vs the fp32 CPU oracle on
 the same 2-window batch and seeded weights (fp32 mode gated at 1e-3; bf16 reported).
+--fp8 is BASELINE config C5 (e4m3 q/k/v + FFN forward GEMMs; add --seq 256
+--batch 64 for its doubled clip length): its fp8 GEMM launches are reported as
+`roofline_fp8` against the fp8 dense peak, and `parity` adds the fp8 forward MSE.
 """
 import argparse
 import json
@@ -31,6 +34,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 BF16_DENSE_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (MI355X_MICROARCH.md)
+FP8_DENSE_PEAK_TFLOPS = 5033.2   # scaled f8f6f4 MFMA: 2x bf16 per clock (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -105,8 +109,9 @@ def fwd_parity(cfg, dev, T, windows=2):
     with torch.no_grad():
         ref = model_ref.seq2seq_forward(params, src, H).double()
     out = {"windows": windows, "frames": windows * T, "oracle_s": round(time.perf_counter() - t0, 2), "gate": 1e-3}
-    for tag, amp in (("fp32", False), ("bf16", True)):
-        c = dict(cfg, use_amp=amp, dropout=0.0)
+    modes = [("fp32", False, False), ("bf16", True, False)] + ([("fp8", True, True)] if cfg.get("use_fp8") else [])
+    for tag, amp, fp8 in modes:
+        c = dict(cfg, use_amp=amp, dropout=0.0, use_fp8=fp8)
         m = build_model(c, dev)
         m.load_state_dict(params, strict=True)
         m.eval()
@@ -133,6 +138,9 @@ def main():
                     help="timed steps (the last ones) whose GEMM launches carry HIP timing events")
     ap.add_argument("--feature-steps", type=int, default=10,
                     help="steps of the feature-inclusive variant (raw audio -> GPU features -> step); 0 = skip")
+    ap.add_argument("--fp8", action="store_true",
+                    help="BASELINE config C5: q/k/v + FFN forward GEMMs on e4m3 operands (row-wise scales); "
+                         "C5 also doubles the clip length: --seq 256 --batch 64")
     args = ap.parse_args()
 
     from neurosync_trainer_lite_amd import _hip as K
@@ -145,7 +153,7 @@ def main():
     dev = torch.device("cuda", local)
     cfg = dict(training_config)
     B, T = args.batch, args.seq
-    cfg.update(micro_batch_size=T, frame_size=T, batch_size=B)
+    cfg.update(micro_batch_size=T, frame_size=T, batch_size=B, use_fp8=args.fp8)
     torch.manual_seed(1234)  # identical init on every rank
     model = build_model(cfg, dev)
     model.train()
@@ -188,9 +196,9 @@ def main():
         e0.record(st)
         real_gemm(A, B_, C, M, N, Kd, **kw)
         e1.record(st)
-        ebytes = 2 if A.dtype == torch.bfloat16 else 4
-        cbytes = 2 if C.dtype == torch.bfloat16 else 4
-        gemm_events.append((e0, e1, 2.0 * M * N * Kd, (M * Kd + N * Kd) * ebytes + M * N * cbytes))
+        ebytes = A.element_size()
+        cbytes = C.element_size()
+        gemm_events.append((e0, e1, 2.0 * M * N * Kd, (M * Kd + N * Kd) * ebytes + M * N * cbytes, ebytes == 1))
 
     # Timing events around every launch cost ~1.7 ms per step (228M), so they are
     # recorded in the last `--gemm-sample-steps` timed steps only.
@@ -208,7 +216,7 @@ def main():
         e1.record(st)
         fl = sum(2.0 * M * N * Kd for _, _, _, M, N, Kd, _ in problems)
         by = sum((M * Kd + N * Kd) * A.element_size() + M * N * C.element_size() for A, _, C, M, N, Kd, _ in problems)
-        gemm_events.append((e0, e1, fl, by))
+        gemm_events.append((e0, e1, fl, by, False))
 
     K.gemm = timed_gemm
     K.gemm_grouped = timed_grouped
@@ -234,11 +242,25 @@ def main():
     if not (loss_v == loss_v):
         raise RuntimeError("non-finite loss %r" % loss_v)
 
-    gemm_ms = sum(a.elapsed_time(b) for a, b, _, _ in gemm_events)
-    gemm_flops = sum(f for _, _, f, _ in gemm_events)
-    gemm_alg_bytes = sum(x for _, _, _, x in gemm_events) / max(1, len(gemm_events))
+    # bf16 launches -> `roofline` (vs the bf16 peak); fp8 launches (--fp8) -> `roofline_fp8`
+    ev16 = [e for e in gemm_events if not e[4]]
+    ev8 = [e for e in gemm_events if e[4]]
+    all_ms = sum(a.elapsed_time(b) for a, b, _, _, _ in gemm_events)
+    gemm_ms = sum(a.elapsed_time(b) for a, b, _, _, _ in ev16)
+    gemm_flops = sum(f for _, _, f, _, _ in ev16)
+    gemm_alg_bytes = sum(x for _, _, _, x, _ in ev16) / max(1, len(ev16))
     traffic, traffic_src = gemm_traffic()
-    n_launch = len(gemm_events)
+    n_launch = len(ev16)
+    fp8_roof = None
+    if ev8:
+        ms8 = sum(a.elapsed_time(b) for a, b, _, _, _ in ev8)
+        tf8 = sum(f for _, _, f, _, _ in ev8) / (ms8 * 1e-3) / 1e12
+        fp8_roof = {"bound": "mfma", "kernel": "gemm256f8_kernel (e4m3 q/k/v + FFN forward, row scales)",
+                    "achieved": round(tf8, 1), "peak": FP8_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(tf8 / FP8_DENSE_PEAK_TFLOPS, 4), "launches": len(ev8),
+                    "avg_launch_us": round(ms8 * 1e3 / len(ev8), 2),
+                    "algorithmic_bytes_per_launch": round(sum(x for _, _, _, x, _ in ev8) / len(ev8)),
+                    "share_of_step": round(ms8 / (max(1, min(args.steps, args.gemm_sample_steps)) * elapsed / args.steps * 1e3), 3)}
     n_sampled = max(1, min(args.steps, args.gemm_sample_steps))
     achieved_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
     ms_step = elapsed / args.steps * 1e3
@@ -319,11 +341,16 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": round(gemm_alg_bytes),
                          "launches": n_launch, "avg_launch_us": round(gemm_ms * 1e3 / max(1, n_launch), 2),
-                         "gemm_share_of_step": round(gemm_ms / (n_sampled * ms_step), 3)},
+                         "gemm_share_of_step": round(all_ms / (n_sampled * ms_step), 3)},
             "step_tflops_per_gpu": round(step_tf, 1),
             "step_mfma_frac": round(step_tf / BF16_DENSE_PEAK_TFLOPS, 4),
             "final_loss": round(loss_v, 4),
         }
+        if fp8_roof is not None:
+            out["roofline_fp8"] = fp8_roof
+            out["dtype"] = "bf16 + e4m3 (q/k/v + FFN forward GEMMs, row-wise scales)"
+            out["config"]["workload"] = ("C5: 228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam), "
+                                         "fp8 q/k/v + FFN forward, T=%d" % T)
         if feat is not None:
             out["feature_inclusive"] = feat
         if world == 1 and not args.no_parity:

@@ -14,7 +14,9 @@
  *   - `stream` is a hipStream_t passed as void*; every launch goes on it.
  *   - return 0 on success, a hipError_t value otherwise (1 = invalid value);
  *     nstl_last_error_string() describes the last failure on this thread.
- *   - dtype codes: NSTL_F32 = 0, NSTL_BF16 = 1.  Row-major everywhere.
+ *   - dtype codes: NSTL_F32 = 0, NSTL_BF16 = 1, NSTL_FP8 = 2 (GEMM operands
+ *     only: OCP e4m3 bytes + f32 row scales, see nstl_fp8_quant_rows).
+ *     Row-major everywhere.
  */
 #ifndef NSTL_H
 #define NSTL_H
@@ -25,7 +27,7 @@
 extern "C" {
 #endif
 
-enum { NSTL_F32 = 0, NSTL_BF16 = 1 };
+enum { NSTL_F32 = 0, NSTL_BF16 = 1, NSTL_FP8 = 2 };
 
 enum {
   NSTL_EPI_NONE = 0,           /* C = alpha*acc + beta*C                        */
@@ -66,6 +68,8 @@ typedef struct nstl_gemm_args {
   uint64_t* relu_mask;                 /* optional [nstl_gemm_relu_mask_words()]: BIAS_RELU_DROP
                                           writes, DRELU_DROP reads (instead of aux) the bits
                                           "kept and positive" of the FFN hidden, 1 bit/element */
+  const float* a_scale;                /* dtype NSTL_FP8: f32 row scales of A [M] and of B [N]   */
+  const float* b_scale;                /* (nstl_fp8_quant_rows); C = a_scale[i] b_scale[j] acc   */
 } nstl_gemm_args;
 int nstl_gemm(const nstl_gemm_args* args, void* stream);
 /* Rows of colsum_part for these arguments, or 0 when the call cannot produce it. */
@@ -84,6 +88,25 @@ int64_t nstl_gemm_relu_mask_words(const nstl_gemm_args* args);
 #define NSTL_GEMM_GROUP_MAX 16
 int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream);
 int64_t nstl_gemm_workspace_bytes(int M, int N, int split_k);
+
+/* Row-wise fp8 quantization (BASELINE config C5: fp8 QKV/FFN projections; the
+ * reference computes these Linears under fp16 autocast, utils/training_utils.py
+ * :64, so fp8 is a precision choice of C5, not a restatement).
+ * Row i of X[rows][cols] gets amax_i = max_j |x_ij|, the f32 scale
+ * s_i = amax_i / 448 (448 = the largest e4m3 value; 1 for an all-zero row) and
+ * q_ij = e4m3(x_ij * (448 / amax_i)) (OCP e4m3fn, round to nearest even), so
+ * x_ij ~ s_i q_ij.  An fp8 GEMM (dtype NSTL_FP8) takes A's scales as a_scale and
+ * B's as b_scale.  Constraints: cols % 16 == 0, ldx % 8 == 0, ldq % 16 == 0,
+ * 16-byte aligned rows.  Up to NSTL_FP8_BATCH_MAX independent jobs of one
+ * source dtype per launch (all the projection weights after an optimizer step). */
+#define NSTL_FP8_BATCH_MAX 64
+typedef struct nstl_fp8_job {
+  const void* x; int64_t ldx;   /* source (x_dtype) */
+  void* q; int64_t ldq;         /* e4m3 out [rows][ldq] */
+  float* scale;                 /* f32 out [rows] */
+  int rows, cols;
+} nstl_fp8_job;
+int nstl_fp8_quant_rows(int x_dtype, const nstl_fp8_job* jobs, int n, void* stream);
 
 /* Non-causal multi-head attention with per-head RoPE already applied to q,k
  * (by the projection epilogue), softmax scale 1/sqrt(dh), attention-probability

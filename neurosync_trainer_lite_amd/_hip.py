@@ -16,7 +16,7 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 LIB_PATH = os.environ.get("NSTL_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                             "libnstl_hip.so")
 
-F32, BF16 = 0, 1
+F32, BF16, FP8 = 0, 1, 2
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU_DROP, EPI_BIAS_ROPE, EPI_DRELU_DROP = 0, 1, 2, 3, 4
 
 _vp = ctypes.c_void_p
@@ -37,8 +37,15 @@ class GemmArgs(ctypes.Structure):
         ("p_drop", _f32), ("seed", _u64),
         ("rope_cos", _vp), ("rope_sin", _vp), ("rope_T", _i32), ("rope_dim", _i32), ("rope_cols", _i32),
         ("split_k", _i32), ("workspace", _vp), ("workspace_bytes", _i64), ("colsum_part", _vp),
-        ("relu_mask", _vp),
+        ("relu_mask", _vp), ("a_scale", _vp), ("b_scale", _vp),
     ]
+
+
+class Fp8Job(ctypes.Structure):
+    _fields_ = [("x", _vp), ("ldx", _i64), ("q", _vp), ("ldq", _i64), ("scale", _vp), ("rows", _i32), ("cols", _i32)]
+
+
+FP8_BATCH_MAX = 64
 
 
 class AttnArgs(ctypes.Structure):
@@ -101,7 +108,7 @@ EXPORTS = [
     "nstl_colsum", "nstl_rope",
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
     "nstl_features", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
-    "nstl_version",
+    "nstl_version", "nstl_fp8_quant_rows",
 ]
 
 _lib = None
@@ -119,6 +126,7 @@ def lib():
         P = ctypes.POINTER
         L.nstl_gemm.argtypes = [P(GemmArgs), _vp]
         L.nstl_gemm_grouped.argtypes = [P(GemmArgs), _i32, _vp]
+        L.nstl_fp8_quant_rows.argtypes = [_i32, P(Fp8Job), _i32, _vp]
         L.nstl_gemm_colsum_rows.argtypes = [P(GemmArgs)]
         L.nstl_gemm_colsum_rows.restype = _i32
         L.nstl_gemm_relu_mask_words.argtypes = [P(GemmArgs)]
@@ -174,7 +182,9 @@ def dtype_code(dt):
         return F32
     if dt == torch.bfloat16:
         return BF16
-    raise TypeError("unsupported dtype %s (float32 / bfloat16)" % dt)
+    if dt == torch.float8_e4m3fn:
+        return FP8
+    raise TypeError("unsupported dtype %s (float32 / bfloat16 / float8_e4m3fn)" % dt)
 
 
 # ---------------------------------------------------------------------------
@@ -211,7 +221,8 @@ def gemm_grouped(problems, stream=None):
 
 def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None,
               alpha=1.0, beta=0.0, epilogue=EPI_NONE, bias=None, aux=None, ld_aux=0, p_drop=0.0, seed=0,
-              rope=None, rope_cols=0, split_k=1, workspace=None, colsum_part=None, relu_mask=None):
+              rope=None, rope_cols=0, split_k=1, workspace=None, colsum_part=None, relu_mask=None,
+              a_scale=None, b_scale=None):
     a = GemmArgs()
     a.dtype = dtype_code(A.dtype)
     a.c_dtype = dtype_code(C.dtype)
@@ -238,7 +249,26 @@ def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=N
         a.workspace_bytes = workspace.numel() * workspace.element_size()
     a.colsum_part = ptr(colsum_part)
     a.relu_mask = ptr(relu_mask)
+    a.a_scale, a.b_scale = ptr(a_scale), ptr(b_scale)
     return a
+
+
+def fp8_quant_rows(jobs, stream=None):
+    """Row-wise e4m3 quantization (nstl_fp8_quant_rows): `jobs` is a list of
+    (x, rows, cols, q, scale) with x f32/bf16 [rows, >= cols], q float8_e4m3fn
+    [rows, >= cols] and scale f32 [rows]; all jobs share x's dtype."""
+    if not jobs:
+        return
+    dt = jobs[0][0].dtype
+    for lo in range(0, len(jobs), FP8_BATCH_MAX):
+        chunk = jobs[lo:lo + FP8_BATCH_MAX]
+        arr = (Fp8Job * len(chunk))()
+        for i, (x, rows, cols, q, scale) in enumerate(chunk):
+            if x.dtype != dt or q.dtype != torch.float8_e4m3fn or scale.dtype != torch.float32:
+                raise TypeError("fp8_quant_rows: x of one dtype, q float8_e4m3fn, scale float32")
+            arr[i] = Fp8Job(x.data_ptr(), x.stride(0), q.data_ptr(), q.stride(0), scale.data_ptr(), rows, cols)
+        check(lib().nstl_fp8_quant_rows(dtype_code(dt), arr, len(chunk), stream if stream is not None else stream_of()),
+              "nstl_fp8_quant_rows")
 
 
 def attn_args(dtype, B, T, H, q, q_ld, k, k_ld, v, v_ld, o, o_ld, lse, p_drop, seed, dh=64):

@@ -1,7 +1,8 @@
 """Drop-in for the reference ``config.py`` (/root/reference/config.py:26-55): same keys,
 same defaults.  Hidden keys the reference reads with defaults are listed explicitly:
 ``use_amp`` (train.py:25; here: bf16 compute when True, fp32 parity mode when False)
-and ``overlap`` (audio_processing.py:53).  ``num_gpus`` is no longer capped at 4: the
+and ``overlap`` (audio_processing.py:53).  ``use_fp8`` (not a reference key, default
+False) selects BASELINE config C5's fp8 q/k/v and FFN forward GEMMs.  ``num_gpus`` is no longer capped at 4: the
 data-parallel path is one process per GPU (torchrun), see parallel.py."""
 import os
 import shutil

@@ -19,6 +19,8 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 template <typename T> struct FragT;
 template <> struct FragT<bf16> { typedef bf16x8 type; };
@@ -176,3 +178,4 @@ NSTL_DEV int xcd_remap(int bid, int nwg) {
   const int x = bid & 7, k = bid >> 3;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
+

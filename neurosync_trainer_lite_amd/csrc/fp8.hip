@@ -1,0 +1,96 @@
+// Row-wise fp8 quantization of GEMM operands (BASELINE config C5: fp8 QKV/FFN
+// projections; nstl.h nstl_fp8_quant_rows).  One wave per row: pass 1 takes
+// max |x| over the row (16-byte loads, wave max), pass 2 re-reads the row (an
+// L2 hit: a row is 2-8 KB) and writes e4m3 bytes, 8 per lane and chunk, plus
+// the row's f32 scale.  HBM-bound: (2 or 4) + 1 bytes per element.
+#include <algorithm>
+
+#include "../../include/nstl.h"
+
+#include "common.h"
+#include "status.h"
+
+namespace {
+
+struct Fp8Batch {
+  nstl_fp8_job j[NSTL_FP8_BATCH_MAX];
+  int n;
+};
+
+// two f32 -> two e4m3 bytes (OCP e4m3fn on gfx950, round to nearest even)
+NSTL_DEV uint32_t pk_fp8(float a, float b) {
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xffffu;
+}
+
+template <bool XF32>
+NSTL_DEV void load8(const nstl_fp8_job& J, int i, int c0, float (&v)[8]) {
+  if (XF32) {
+    const float* src = (const float*)J.x + (int64_t)i * J.ldx + c0;
+    const f32x4 a = *(const f32x4*)src, b = *(const f32x4*)(src + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = b[e]; }
+  } else {
+    const bf16x8 a = *(const bf16x8*)((const bf16*)J.x + (int64_t)i * J.ldx + c0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)a[e];
+  }
+}
+
+template <bool XF32>
+__global__ __launch_bounds__(256) void fp8_quant_rows_kernel(Fp8Batch b) {
+  const nstl_fp8_job& J = b.j[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int nchunk = J.cols >> 3;  // 8-element chunks per row
+  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < J.rows; i += gridDim.x * 4) {
+    float am = 0.f;
+    for (int c = lane; c < nchunk; c += 64) {
+      float v[8];
+      load8<XF32>(J, i, c * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(v[e]));
+    }
+    am = wave_max(am);
+    const float inv = am > 0.f ? 448.f / am : 1.f;
+    if (lane == 0) J.scale[i] = am > 0.f ? am / 448.f : 1.f;
+    for (int c = lane; c < nchunk; c += 64) {
+      float v[8];
+      load8<XF32>(J, i, c * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fminf(fmaxf(v[e] * inv, -448.f), 448.f);
+      const uint32_t lo = pk_fp8(v[0], v[1]) | (pk_fp8(v[2], v[3]) << 16);
+      const uint32_t hi = pk_fp8(v[4], v[5]) | (pk_fp8(v[6], v[7]) << 16);
+      *(uint2*)((uint8_t*)J.q + (int64_t)i * J.ldq + c * 8) = make_uint2(lo, hi);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int nstl_fp8_quant_rows(int x_dtype, const nstl_fp8_job* jobs, int n, void* stream) {
+  NSTL_CHECK_ARG(jobs != nullptr && n >= 1 && n <= NSTL_FP8_BATCH_MAX, "nstl_fp8_quant_rows: 1..%d jobs (got %d)",
+                 NSTL_FP8_BATCH_MAX, n);
+  NSTL_CHECK_ARG(x_dtype == NSTL_F32 || x_dtype == NSTL_BF16, "nstl_fp8_quant_rows: bad source dtype %d", x_dtype);
+  Fp8Batch b;
+  b.n = n;
+  int most = 0;
+  for (int k = 0; k < n; ++k) {
+    const nstl_fp8_job& J = jobs[k];
+    NSTL_CHECK_ARG(J.x && J.q && J.scale, "nstl_fp8_quant_rows: job %d: null pointer", k);
+    NSTL_CHECK_ARG(J.rows > 0 && J.cols > 0 && J.cols % 16 == 0,
+                   "nstl_fp8_quant_rows: job %d: cols must be a positive multiple of 16 (got %d x %d)", k, J.rows,
+                   J.cols);
+    NSTL_CHECK_ARG(J.ldx >= J.cols && J.ldx % 8 == 0 && ((uintptr_t)J.x % 16) == 0,
+                   "nstl_fp8_quant_rows: job %d: source rows must be 16-byte aligned (ldx %% 8 == 0)", k);
+    NSTL_CHECK_ARG(J.ldq >= J.cols && J.ldq % 16 == 0 && ((uintptr_t)J.q % 16) == 0,
+                   "nstl_fp8_quant_rows: job %d: ldq must be a multiple of 16 >= cols", k);
+    b.j[k] = J;
+    most = std::max(most, J.rows);
+  }
+  const int blocks = std::min((most + 3) / 4, 4096);
+  dim3 grid(blocks, n), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (x_dtype == NSTL_F32) hipLaunchKernelGGL((fp8_quant_rows_kernel<true>), grid, block, 0, st, b);
+  else hipLaunchKernelGGL((fp8_quant_rows_kernel<false>), grid, block, 0, st, b);
+  NSTL_LAUNCH_CHECK("nstl_fp8_quant_rows");
+  return 0;
+}

@@ -41,6 +41,7 @@ struct GemmParams {
   int debug_skip_epilogue; int k_chunk;  // split-K: partial slabs [z][M][N]
   float* colsum_part;  // [ceil(M/128)][N]: column sums of C as stored (dReLU ring epilogue)
   uint64_t* relu_mask;  // ReLU-dropout keep&positive bits, ring epilogue layout (relu_mask_index)
+  const float* a_scale; const float* b_scale;  // fp8: row scales of A [M] and of B [N]
 };
 
 // Epilogue over a wave's MT x 4 grid of 16x16 accumulators whose origin is
@@ -525,7 +526,8 @@ enum { EM_GENERIC = 0, EM_BF16 = 1, EM_RELU_DROP = 2, EM_ROPE = 3, EM_DRELU = 4,
 constexpr int RING_EPI_RB = 64 * 4 + 16;          // padded f32 scratch row
 constexpr int RING_EPI_WAVE = 64 * RING_EPI_RB;   // 17 KB per wave (8 waves: 136 KB)
 
-NSTL_DEV void stage_half(const f32x4 (&acc)[8][4], int half, float alpha, int lane, char* scr) {
+NSTL_DEV void stage_half(const f32x4 (&acc)[8][4], int half, const GemmParams& p, int row0, int lane, char* scr) {
+  const float alpha = p.alpha;
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -542,8 +544,31 @@ NSTL_DEV int64_t relu_mask_index(int N, int row_block64, int r0, int j) {
   return ((int64_t)row_block64 * 8 + r0) * ((N + 7) >> 3) + (j >> 3);
 }
 
-template <int EM>
-NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, int col0, int lane, char* scr) {
+// the same for the fp8 kernel's 32x32 accumulators (v_mfma_scale_f32_32x32x64,
+// operands swapped): acc[a][b] register r of lane l is row 32a + (l & 31),
+// column 32b + 8(r >> 2) + 4(l >> 5) + (r & 3) of the wave's 128 x 64 block
+// (fp8 operands: the row scale a_scale[row] is applied here, per lane and row)
+NSTL_DEV void stage_half(const f32x16 (&acc)[4][2], int half, const GemmParams& p, int row0, int lane, char* scr) {
+#pragma unroll
+  for (int a2 = 0; a2 < 2; ++a2) {
+    const int r = 32 * a2 + (lane & 31);
+    const int i = row0 + 64 * half + r;
+    const float sc = (i < p.M ? p.a_scale[i] : 0.f) * p.alpha;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x16& x = acc[half * 2 + a2][b];
+        *(f32x4*)(scr + r * RING_EPI_RB + (32 * b + 8 * g + 4 * (lane >> 5)) * 4) =
+            (f32x4){x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]} * sc;
+      }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// SC: fp8 operands -- values come scaled by a_scale[row] (stage_half); times b_scale[col] here
+template <int EM, bool SC, typename ACC>
+NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, int lane, char* scr) {
   constexpr bool F32OUT = EM == EM_F32 || EM == EM_WS;
   constexpr int ESZ = F32OUT ? 4 : 2;
   constexpr int CW = 16 / ESZ;   // columns per lane per store (8 bf16 / 4 f32)
@@ -563,9 +588,13 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
   const bool colok = j < p.N;
   const bool vec = j + CW <= p.N && (ldc % CW) == 0;
   const bool use_beta = EM == EM_F32 && p.beta != 0.f;
-  float bias[CW];
+  float bias[CW], csc[CW];
 #pragma unroll
   for (int e = 0; e < CW; ++e) bias[e] = 0.f;
+  if (SC) {
+#pragma unroll
+    for (int e = 0; e < CW; ++e) csc[e] = j + e < p.N ? p.b_scale[j + e] : 0.f;
+  }
   if ((EM == EM_BF16 || EM == EM_RELU_DROP || EM == EM_ROPE) && p.bias != nullptr) {
 #pragma unroll
     for (int e = 0; e < CW; ++e) bias[e] = j + e < p.N ? p.bias[j + e] : 0.f;
@@ -644,7 +673,7 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
         inf[iu % NF] = o;
       }
     }
-    if (sub == 0) stage_half(acc, half, p.alpha, lane, scr);
+    if (sub == 0) stage_half(acc, half, p, row0, lane, scr);
     auto body = [&](int iu) {
       const int it = sub * NI + iu;
       const int i = ib + it * RPI;
@@ -661,6 +690,10 @@ NSTL_DEV void ring_epi(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, 
         }
       }
       if (i < p.M && colok) {
+        if (SC) {
+#pragma unroll
+          for (int e = 0; e < CW; ++e) v[e] *= csc[e];
+        }
 #pragma unroll
         for (int e = 0; e < CW; ++e) v[e] += bias[e];
         if (EM == EM_RELU_DROP) {
@@ -764,7 +797,7 @@ NSTL_DEV void ring_epi_generic(const GemmParams& p, const f32x4 (&acc)[8][4], in
                                char* scr) {
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
-    stage_half(acc, half, p.alpha, lane, scr);
+    stage_half(acc, half, p, row0, lane, scr);
 #pragma unroll 1
     for (int it = 0; it < 16; ++it) {
       const int r = it * 4 + (lane >> 4), c = (lane & 15) * 4;
@@ -866,7 +899,7 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
   char* scr = smem + wave * RING_EPI_WAVE;
   const int row0 = m0 + wm * 128, col0 = n0 + wn * 64;
   if (EM == EM_GENERIC) ring_epi_generic(p, acc, row0, col0, lane, scr);
-  else ring_epi<EM>(p, acc, row0, col0, lane, scr);
+  else ring_epi<EM, false>(p, acc, row0, col0, lane, scr);
 }
 
 template <bool AK, bool BKM, int EM>
@@ -893,6 +926,166 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm256r_group_kernel(GroupParams g
   int g = 0;
   while (g + 1 < gp.n && gid >= gp.tile_end[g]) ++g;
   ring_tile<AK, BKM, EM>(gp.g[g], gid - (g > 0 ? gp.tile_end[g - 1] : 0), 0, smem);
+}
+
+// ===========================================================================
+// FP8 forward GEMM (BASELINE config C5: fp8 QKV/FFN projections):
+//   C[i][j] = sa[i] * sb[j] * sum_r qa[i][r] qb[j][r]  (+ epilogue)
+// with A [M][K], B [N][K] OCP e4m3 bytes (K-major) and f32 row scales sa (per
+// row of A = token) and sb (per row of B = output channel) from
+// nstl_fp8_quant_rows.  The products run on v_mfma_scale_f32_32x32x64_f8f6f4
+// with unit E8M0 block scales (K = 64 per instruction: twice the bf16 rate per
+// clock, MI355X_MICROARCH.md "Matrix cores"; the non-scaled fp8 MFMAs only run
+// at the bf16 rate); the row scales are applied by the epilogue, so the K loop
+// moves nothing but operand bytes.
+// The bf16 ring kernel's structure is kept as is: 256x256 tile, 8 waves (2 x 4,
+// 128 x 64 each), a ring of five 32 KB LDS-DMA stages issued three ahead, the
+// two wave groups one barrier apart, the same vmcnt/barrier protocol.  A stage
+// holds 64 K-bytes of A and of B (256 rows x 64 B each; 16-byte chunk c of row
+// r sits at c ^ ((r >> 2) & 3), which puts every ds_read_b128 lane group of the
+// fragment reads on 16 distinct bank slots).  Per stage a wave issues 8 MFMAs
+// (4 A fragments of 32 rows x 2 B fragments of 32 columns): the same 512 MFMA
+// cycles as a bf16 stage, for twice the K.
+constexpr int F8_BK = 64;        // K bytes (= elements) per fp8 stage
+constexpr int F8_UNIT = 0x7f7f7f7f;  // E8M0 127 = 2^0 in every byte
+
+NSTL_DEV void glds_stage_f8(char* img, const char* base, int64_t ld, int row0, int rows_total, int k0, int wave,
+                            int lane) {
+  // 16 KB operand image = 16 wave-instructions of 1 KB (16 rows of 64 B), 2 per wave
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int q = wave * 2 + s;
+    const int row = 16 * q + (lane >> 2);
+    const int c = (lane & 3) ^ ((row >> 2) & 3);
+    const int gi = min(row0 + row, rows_total - 1);
+    const char* src = base + (int64_t)gi * ld + k0 + c * 16;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)(img + q * 1024), 16, 0, 0);
+  }
+}
+
+NSTL_DEV void ring_stage_f8(char* slot, const GemmParams& p, int m0, int n0, int k0, int wave, int lane) {
+  glds_stage_f8(slot, p.A, p.lda, m0, p.M, k0, wave, lane);
+  glds_stage_f8(slot + R_SLOT / 2, p.B, p.ldb, n0, p.N, k0, wave, lane);
+}
+
+// one 32 x 64 fp8 fragment: lane l holds row (l & 31), K bytes 32 (l >> 5) .. +31
+NSTL_DEV void asm_frag_f8(i32x8& f, uint32_t img, int row, int lane) {
+  const int h = lane >> 5, x = (row >> 2) & 3;
+  i32x4_t v0, v1;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v0) : "v"(img + row * 64 + (((2 * h) ^ x) << 4)));
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v1) : "v"(img + row * 64 + (((2 * h + 1) ^ x) << 4)));
+  f = (i32x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+}
+
+// operands swapped as in the bf16 kernel (weights first, so acc takes C^T's layout)
+NSTL_DEV void mma_f8(f32x16& acc, const i32x8& w, const i32x8& x) {
+  acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(w, x, acc, 0, 0, 0, F8_UNIT, 0, F8_UNIT);
+}
+
+template <int EM>
+NSTL_DEV void ring_tile_f8(const GemmParams& p, int id, char* smem) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nt_n = (p.N + BIG - 1) / BIG, nt_m = (p.M + BIG - 1) / BIG;
+  constexpr int GROUP_M = 4;
+  const int per_group = GROUP_M * nt_n;
+  const int first_m = (id / per_group) * GROUP_M;
+  const int gm = min(nt_m - first_m, GROUP_M);
+  const int in_g = id % per_group;
+  const int tm = first_m + in_g % gm, tn = in_g / gm;
+  const int m0 = tm * BIG, n0 = tn * BIG;
+  const int nk = p.K / F8_BK;
+  const uint32_t smem_u32 = lds_u32(smem);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+    if (s < nk) ring_stage_f8(smem + s * R_SLOT, p, m0, n0, s * F8_BK, wave, lane);
+  if (nk >= 3) NSTL_VMCNT(8);
+  else if (nk == 2) NSTL_VMCNT(4);
+  else NSTL_VMCNT(0);
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // the stagger
+
+  // Branch-free steps: both groups retire stage kt+1 at both of their waits
+  // (the earlier is group 1's, the later group 0's; the other is then already
+  // satisfied or nearly so), with the count a constant of each call (8 while a
+  // stage is issued three ahead, then 4, 0, 0).  With a branch between the MFMAs
+  // and the barrier, LLVM sinks the scaled MFMAs (unlike the bf16 ones) past it,
+  // out of the prioritised phase.
+  int slot = 0;
+  // wait: the vmcnt both groups use (-1: the per-group retire_next, short K)
+  auto step = [&](int kt, bool stage3, int wait) {
+    // ---- R(kt)
+    const uint32_t Ai = smem_u32 + slot * R_SLOT;
+    const uint32_t Bi = Ai + R_SLOT / 2;
+    i32x8 fb[2], fa[4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) asm_frag_f8(fb[t], Bi, wn * 64 + t * 32 + (lane & 31), lane);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) asm_frag_f8(fa[a], Ai, wm * 128 + a * 32 + (lane & 31), lane);
+    if (stage3) {
+      int s3 = slot + 3;
+      if (s3 >= R_STAGES) s3 -= R_STAGES;
+      ring_stage_f8(smem + s3 * R_SLOT, p, m0, n0, (kt + 3) * F8_BK, wave, lane);
+    }
+    if (wait == 8) NSTL_VMCNT(8);
+    else if (wait == 4) NSTL_VMCNT(4);
+    else if (wait == 0) NSTL_VMCNT(0);
+    else if (wm == 1) retire_next(kt, nk);
+    __builtin_amdgcn_s_barrier();
+    // ---- M(kt)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) mma_f8(acc[a][b], fb[b], fa[a]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    if (wait == 8) NSTL_VMCNT(8);
+    else if (wait == 4) NSTL_VMCNT(4);
+    else if (wait == 0) NSTL_VMCNT(0);
+    else if (wm == 0) retire_next(kt, nk);
+    __builtin_amdgcn_s_barrier();
+    slot = slot + 1 == R_STAGES ? 0 : slot + 1;
+  };
+  if (nk >= 3) {
+    for (int kt = 0; kt + 3 < nk; ++kt) step(kt, true, 8);
+    step(nk - 3, false, 4);
+    step(nk - 2, false, 0);
+    step(nk - 1, false, 0);
+  } else {
+    for (int kt = 0; kt < nk; ++kt) step(kt, false, -1);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger
+  if (p.debug_skip_epilogue == 1) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) asm volatile("" ::"v"(acc[a][b]));
+    return;
+  }
+  __syncthreads();  // every wave is done with the ring: it becomes scratch
+  char* scr = smem + wave * RING_EPI_WAVE;
+  ring_epi<EM, true>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, scr);
+}
+
+template <int EM>
+__global__ __launch_bounds__(BIG_NT, 1) void gemm256f8_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[R_SMEM];
+  const int nt = ((p.M + BIG - 1) / BIG) * ((p.N + BIG - 1) / BIG);
+  ring_tile_f8<EM>(p, xcd_remap(blockIdx.x, nt), smem);
 }
 
 // which lean epilogue fits this call (EM_GENERIC when none does)
@@ -1024,10 +1217,11 @@ namespace {
 // validate one problem and fill its kernel parameters (no split-K decisions)
 int make_params(const nstl_gemm_args* a, GemmParams& p) {
   NSTL_CHECK_ARG(a != nullptr, "nstl_gemm: null args");
-  NSTL_CHECK_ARG(a->dtype == NSTL_F32 || a->dtype == NSTL_BF16, "nstl_gemm: bad dtype %d", a->dtype);
+  NSTL_CHECK_ARG(a->dtype == NSTL_F32 || a->dtype == NSTL_BF16 || a->dtype == NSTL_FP8, "nstl_gemm: bad dtype %d",
+                 a->dtype);
   NSTL_CHECK_ARG(a->c_dtype == NSTL_F32 || a->c_dtype == NSTL_BF16, "nstl_gemm: bad c_dtype");
   NSTL_CHECK_ARG(a->M > 0 && a->N > 0 && a->K > 0, "nstl_gemm: empty problem %dx%dx%d", a->M, a->N, a->K);
-  const int esz = a->dtype == NSTL_F32 ? 4 : 2;
+  const int esz = a->dtype == NSTL_F32 ? 4 : a->dtype == NSTL_BF16 ? 2 : 1;
   const int vec = 16 / esz;
   NSTL_CHECK_ARG(((uintptr_t)a->A % 16) == 0 && ((uintptr_t)a->B % 16) == 0,
                  "nstl_gemm: A and B must be 16-byte aligned");
@@ -1067,6 +1261,31 @@ int make_params(const nstl_gemm_args* a, GemmParams& p) {
   p.k_chunk = a->K;
   p.colsum_part = a->colsum_part;
   p.relu_mask = a->relu_mask;
+  p.a_scale = a->a_scale;
+  p.b_scale = a->b_scale;
+  return 0;
+}
+
+// FP8 operands: the fp8 ring kernel (K-major A and B, K % 64 == 0, no split-K)
+int gemm_f8(const nstl_gemm_args* a, GemmParams& p, hipStream_t st) {
+  NSTL_CHECK_ARG(a->a_kmajor && a->b_kmajor, "nstl_gemm: FP8 needs K-major A and B (Y = X W^T)");
+  NSTL_CHECK_ARG(a->K % 64 == 0, "nstl_gemm: FP8 needs K %% 64 == 0 (got %d)", a->K);
+  NSTL_CHECK_ARG(a->a_scale && a->b_scale, "nstl_gemm: FP8 needs the row scales a_scale [M] and b_scale [N]");
+  NSTL_CHECK_ARG(a->split_k <= 1 && !a->colsum_part, "nstl_gemm: FP8: no split-K, no colsum_part");
+  const int em = ring_epi_mode(a, p);
+  NSTL_CHECK_ARG(em == EM_BF16 || em == EM_RELU_DROP || em == EM_ROPE || em == EM_F32,
+                 "nstl_gemm: FP8 supports the NONE / BIAS / BIAS_RELU_DROP / BIAS_ROPE epilogues "
+                 "(bf16 out without beta, or f32 out without epilogue)");
+  NSTL_CHECK_ARG(!a->relu_mask || em == EM_RELU_DROP, "nstl_gemm: relu_mask needs the ReLU-dropout epilogue");
+  const int nt = ((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
+  dim3 grid(nt), block(BIG_NT);
+  switch (em) {
+    case EM_BF16: hipLaunchKernelGGL((gemm256f8_kernel<EM_BF16>), grid, block, 0, st, p); break;
+    case EM_RELU_DROP: hipLaunchKernelGGL((gemm256f8_kernel<EM_RELU_DROP>), grid, block, 0, st, p); break;
+    case EM_ROPE: hipLaunchKernelGGL((gemm256f8_kernel<EM_ROPE>), grid, block, 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm256f8_kernel<EM_F32>), grid, block, 0, st, p); break;
+  }
+  NSTL_LAUNCH_CHECK("nstl_gemm (FP8)");
   return 0;
 }
 
@@ -1081,6 +1300,7 @@ bool big_ok(const nstl_gemm_args* a) {
 extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   GemmParams p;
   if (int rc = make_params(a, p)) return rc;
+  if (a->dtype == NSTL_FP8) return gemm_f8(a, p, (hipStream_t)stream);
   const int esz = a->dtype == NSTL_F32 ? 4 : 2;
 
   // the 256x256 LDS-DMA kernel: bf16, K a multiple of its 64-deep K tile, and at
@@ -1169,6 +1389,10 @@ extern "C" int nstl_gemm_colsum_rows(const nstl_gemm_args* a) {
 extern "C" int64_t nstl_gemm_relu_mask_words(const nstl_gemm_args* a) {
   GemmParams p;
   if (a == nullptr || make_params(a, p) != 0) return 0;
+  if (a->dtype == NSTL_FP8) {
+    if (a->split_k > 1 || a->c_dtype != NSTL_BF16 || ring_epi_mode(a, p) != EM_RELU_DROP) return 0;
+    return (int64_t)((a->M + 63) / 64) * 8 * ((a->N + 7) / 8);
+  }
   if (!big_ok(a) || a->split_k > 1 || !getenv_ring() || a->dtype != NSTL_BF16 || a->c_dtype != NSTL_BF16) return 0;
   const int em = ring_epi_mode(a, p);
   if (em != EM_RELU_DROP && em != EM_DRELU) return 0;

@@ -203,6 +203,12 @@ class Seq2SeqEngine:
         # NSTL_REDUCE_BATCH=0: each LayerNorm / bias-gradient partial reduction is
         # its own launch instead of one batched launch per backward layer
         self.reduce_batch_on = os.environ.get("NSTL_REDUCE_BATCH", "1") != "0"
+        # BASELINE config C5: the q/k/v and FFN projections' forward GEMMs take e4m3
+        # operands with row-wise scales (oracle/fp8_ref.py; Seq2Seq.set_fp8 or the
+        # config key 'use_fp8').  Backward keeps the bf16 weights and activations.
+        self.fp8 = False
+        self._fp8_w = None         # (weight name, rows) -> (e4m3 [rows*N, K], f32 scales [rows*N])
+        self._fp8_act = {}         # M -> (e4m3 scratch [M, max(D, Fd)], scales [M], e4m3 mem, mem scales)
         self._red = None           # pending (part, ld, n_part, cols, out, beta) jobs
         self._ln_slot = 0          # next LayerNorm partial buffer of the layer
         self._ab_slot = 0          # next attention bias partial buffer of the layer
@@ -387,14 +393,74 @@ class Seq2SeqEngine:
             s -= 1
         return s
 
+    # ------------------------------------------------------------------ fp8
+    def fp8_groups(self):
+        """(weight name, rows) of the projections whose forward runs in fp8 (C5:
+        q/k/v and FFN): self-attention q|k|v (3 matrices, one GEMM), the decoder's
+        cross-attention q and k|v, FFN linear1 and linear2."""
+        out = []
+        for l in range(self.L):
+            pre = "encoder.transformer_encoder.%d." % l
+            out += [(pre + "self_attn.q_linear.weight", 3), (pre + "ffn.linear1.weight", 1),
+                    (pre + "ffn.linear2.weight", 1)]
+        for l in range(self.L):
+            pre = "decoder.transformer_decoder.%d." % l
+            out += [(pre + "self_attn.q_linear.weight", 3), (pre + "multihead_attn.q_linear.weight", 1),
+                    (pre + "multihead_attn.k_linear.weight", 2), (pre + "ffn.linear1.weight", 1),
+                    (pre + "ffn.linear2.weight", 1)]
+        return out
+
+    def set_fp8(self, on):
+        if on and self.dt != torch.bfloat16:
+            raise ValueError("fp8 projections need the bf16 compute dtype (use_amp=True)")
+        self.fp8 = bool(on)
+
+    def _fp8_weights(self):
+        """Quantize the fp8 projections' weights from the bf16 shadow (one batched
+        launch; every forward, so an optimizer step or a load is always seen)."""
+        if self._fp8_w is None:
+            self._fp8_w = {}
+            for name, rows in self.fp8_groups():
+                n, k = self.w(name, rows).shape
+                self._fp8_w[(name, rows)] = (torch.empty(n, k, dtype=torch.float8_e4m3fn, device=self.device),
+                                             torch.empty(n, dtype=torch.float32, device=self.device))
+        jobs = []
+        for (name, rows), (q, sc) in self._fp8_w.items():
+            W = self.w(name, rows)
+            jobs.append((W, W.shape[0], W.shape[1], q, sc))
+        K.fp8_quant_rows(jobs, stream=self.st)
+
+    def _fp8_bufs(self, M):
+        if M not in self._fp8_act:
+            e8 = lambda *s: torch.empty(*s, dtype=torch.float8_e4m3fn, device=self.device)
+            f = lambda n: torch.empty(n, dtype=torch.float32, device=self.device)
+            self._fp8_act = {M: (e8(M, max(self.D, self.Fd)), f(M), e8(M, self.D), f(M))}
+        return self._fp8_act[M]
+
+    def _fp8_quant(self, x, mem=False):
+        """Row-wise e4m3 copy of activation x [M, cols] (the scratch, or the decoder's
+        memory buffer that all cross-attention k|v projections share)."""
+        M, cols = x.shape
+        q, sc, qm, sm = self._fp8_bufs(M)
+        q, sc = (qm, sm) if mem else (q[:, :cols], sc)
+        K.fp8_quant_rows([(x, M, cols, q, sc)], stream=self.st)
+        return q, sc
+
     # ------------------------------------------------------------ primitives
-    def _gemm_fwd(self, x, wname, out, epi, rows=1, rope=None, rope_cols=0, p_drop=0.0, seed=0, relu_mask=None):
+    def _gemm_fwd(self, x, wname, out, epi, rows=1, rope=None, rope_cols=0, p_drop=0.0, seed=0, relu_mask=None,
+                  xq=None):
         """Projection forward; `relu_mask` (FFN1): also write the keep&positive bits of
-        the hidden for the backward's dReLU when the kernel can (returns whether)."""
+        the hidden for the backward's dReLU when the kernel can (returns whether).
+        In fp8 mode the C5 projections take e4m3 operands (`xq`: x already quantized)."""
         W = self.w(wname, rows)
         bias = self.b(wname.replace(".weight", ".bias"), rows)
         kw = dict(epilogue=epi, bias=bias, rope=rope, rope_cols=rope_cols, p_drop=p_drop, seed=seed)
         m, n, k = x.shape[0], W.shape[0], W.shape[1]
+        if self.fp8 and (wname, rows) in self._fp8_w:
+            qw, sw = self._fp8_w[(wname, rows)]
+            x, sx = xq if xq is not None else self._fp8_quant(x)
+            W = qw
+            kw.update(a_scale=sx, b_scale=sw)
         use = relu_mask is not None and self.relu_mask_on and \
             0 < K.gemm_relu_mask_words(x, W, out, m, n, k, **kw) <= relu_mask.numel()
         K.gemm(x, W, out, m, n, k, relu_mask=relu_mask if use else None, stream=self.st, **kw)
@@ -658,7 +724,7 @@ class Seq2SeqEngine:
         self._gemm_fwd(x1, pre + "multihead_attn.q_linear.weight", qc, K.EPI_BIAS_ROPE,
                        rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D)
         self._gemm_fwd(mem, pre + "multihead_attn.k_linear.weight", kvc, K.EPI_BIAS_ROPE, rows=2,
-                       rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D)
+                       rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D, xq=self._mem_q)
         self._attn(qc, kvc[:, :D], kvc[:, D:], L_(bb.d_oc), L_(bb.d_lsec), sd("xattn"), T, B,
                    mask=bb.d_maskc[l] if bb.save else None)
         self._gemm_fwd(L_(bb.d_oc), pre + "multihead_attn.out_linear.weight", bb.y, K.EPI_BIAS)
@@ -678,6 +744,8 @@ class Seq2SeqEngine:
         self.ensure_bound()
         self.st = K.stream_of(self.device)
         self.p = float(self.dropout) if training else 0.0
+        if self.fp8:
+            self._fp8_weights()
 
     def encode(self, bb, src, T):
         """Encoder forward; returns the encoder output `mem` (compute dtype)."""
@@ -703,6 +771,7 @@ class Seq2SeqEngine:
             K.rope(mem, self.D, bb.xdec0, self.D, bb.M, self.D, *self.rope(T, self.D), T, self.D, stream=self.st)
             xdec0 = bb.xdec0
         x = xdec0
+        self._mem_q = self._fp8_quant(mem, mem=True) if self.fp8 else None
         for l in range(self.L):
             x = self._dec_layer(bb, l, x, mem, T)
         self._ln(None, x, bb.xf, bb.decf_stats, "decoder.layer_norm", 0, (0, 0), None)

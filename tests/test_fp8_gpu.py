@@ -1,0 +1,210 @@
+"""fp8 operand path of BASELINE config C5 on the MI355X: row-wise e4m3
+quantization (bit-exact against oracle/fp8_ref.py) and the fp8 GEMM
+(v_mfma_scale_f32_32x32x64_f8f6f4 ring kernel) against the float64 product of
+the same quantized operands, with each fused epilogue.
+
+Tolerance of the GEMM: the e4m3 products are exact, but the scaled f8f6f4
+MFMA does not accumulate its 64-product blocks as an exact f32 fma chain
+(measured 1.9e-5 of max|C| at K = 1024), so 1e-4 relative to max|C| for f32
+output and 1e-2 for bf16 output (8 mantissa bits); a layout or scaling error
+is O(1)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from neurosync_trainer_lite_amd import _hip as K
+    from neurosync_trainer_lite_amd.engine import rotation_tables
+
+from oracle import fp8_ref
+
+DEV = "cuda:0"
+
+
+def rnd(*shape, dtype=torch.float32, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g, dtype=torch.float64) * scale).to(dtype)
+
+
+def quant_gpu(x):
+    rows, cols = x.shape
+    q = torch.empty(rows, cols, dtype=torch.float8_e4m3fn, device=DEV)
+    s = torch.empty(rows, dtype=torch.float32, device=DEV)
+    K.fp8_quant_rows([(x, rows, cols, q, s)])
+    return q, s
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,cols", [(300, 1024), (64, 4096), (5, 16)])
+def test_quant_rows_bit_exact(dtype, rows, cols):
+    x = rnd(rows, cols, dtype=dtype, seed=rows + cols)
+    x[0] = 0                                   # all-zero row: scale 1, q 0
+    if rows > 2:
+        x[1] *= 1e-6                           # tiny row (subnormal e4m3 codes)
+        x[2, : cols // 2] *= 1e4               # wide dynamic range inside one row
+    q, s = quant_gpu(x.to(DEV))
+    torch.cuda.synchronize()
+    q_ref, s_ref = fp8_ref.quant_rows(x)
+    assert torch.equal(s.cpu(), s_ref), "row scales differ"
+    qb, qrb = q.cpu().view(torch.uint8), q_ref.view(torch.uint8)
+    bad = (qb != qrb).nonzero()
+    assert bad.numel() == 0, "%d codes differ, first at %s: %d vs %d" % (
+        bad.shape[0], bad[0].tolist(), qb[tuple(bad[0])], qrb[tuple(bad[0])])
+
+
+def test_quant_rows_batch_and_strides():
+    xs = [rnd(256, 1088, dtype=torch.bfloat16, seed=s).to(DEV) for s in range(3)]
+    jobs, outs = [], []
+    for x in xs:
+        q = torch.zeros(256, 1104, dtype=torch.float8_e4m3fn, device=DEV)  # ldq > cols
+        s = torch.empty(256, dtype=torch.float32, device=DEV)
+        jobs.append((x[:, :1024], 256, 1024, q, s))
+        outs.append((q, s))
+    K.fp8_quant_rows(jobs)
+    torch.cuda.synchronize()
+    for x, (q, s) in zip(xs, outs):
+        q_ref, s_ref = fp8_ref.quant_rows(x[:, :1024].cpu())
+        assert torch.equal(s.cpu(), s_ref)
+        assert torch.equal(q[:, :1024].cpu().view(torch.uint8), q_ref.view(torch.uint8))
+        assert (q[:, 1024:].cpu().view(torch.uint8) == 0).all(), "wrote past cols"
+
+
+def fp8_operands(M, N, K_, seed):
+    a = rnd(M, K_, dtype=torch.bfloat16, seed=seed).to(DEV)
+    b = rnd(N, K_, dtype=torch.bfloat16, seed=seed + 1, scale=0.05).to(DEV)
+    qa, sa = quant_gpu(a)
+    qb, sb = quant_gpu(b)
+    return qa, sa, qb, sb
+
+
+def close(got, ref, rel, what):
+    got, ref = got.double().cpu(), ref.double().cpu()
+    scale = ref.abs().max().item() + 1e-30
+    err = (got - ref).abs().max().item()
+    assert err <= rel * scale, "%s: max err %.3e vs scale %.3e (rel %.1e)" % (what, err, scale, rel)
+
+
+@pytest.mark.parametrize("M,N,K_", [(512, 768, 1024), (300, 256, 64), (512, 512, 128), (256, 512, 192),
+                                    (1024, 1024, 4096), (257, 300, 256)])
+def test_fp8_gemm_f32(M, N, K_):
+    qa, sa, qb, sb = fp8_operands(M, N, K_, M + N + K_)
+    c = torch.full((M, N), float("nan"), dtype=torch.float32, device=DEV)
+    K.gemm(qa, qb, c, M, N, K_, a_scale=sa, b_scale=sb)
+    torch.cuda.synchronize()
+    close(c, fp8_ref.gemm(qa.cpu(), sa.cpu(), qb.cpu(), sb.cpu()), 1e-4, "fp8 gemm %dx%dx%d" % (M, N, K_))
+
+
+def test_fp8_gemm_bias_relu_rope():
+    M, N, K_ = 512, 1024, 1024
+    qa, sa, qb, sb = fp8_operands(M, N, K_, 7)
+    ref = fp8_ref.gemm(qa.cpu(), sa.cpu(), qb.cpu(), sb.cpu())
+    bias = rnd(N, seed=3, scale=0.1).to(DEV)
+    ref_b = ref + bias.double().cpu()
+    c = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    K.gemm(qa, qb, c, M, N, K_, a_scale=sa, b_scale=sb, epilogue=K.EPI_BIAS, bias=bias)
+    torch.cuda.synchronize()
+    close(c, ref_b, 1e-2, "bias")
+    K.gemm(qa, qb, c, M, N, K_, a_scale=sa, b_scale=sb, epilogue=K.EPI_BIAS_RELU_DROP, bias=bias, p_drop=0.0)
+    torch.cuda.synchronize()
+    close(c, ref_b.clamp_min(0), 1e-2, "bias+relu")
+    # RoPE over the first 512 columns (dh 64), T = 128 positions
+    T, dh = 128, 64
+    cos_t, sin_t = rotation_tables(T, dh, DEV)
+    K.gemm(qa, qb, c, M, N, K_, a_scale=sa, b_scale=sb, epilogue=K.EPI_BIAS_ROPE, bias=bias,
+           rope=(cos_t, sin_t, T, dh), rope_cols=512)
+    torch.cuda.synchronize()
+    r = ref_b.clone()
+    t = torch.arange(M) % T
+    cs, sn = cos_t.double().cpu()[t], sin_t.double().cpu()[t]          # [M, dh/2]
+    x = r[:, :512].view(M, 8, dh // 2, 2)
+    x0, x1 = x[..., 0].clone(), x[..., 1].clone()
+    x[..., 0] = x0 * cs[:, None, :] - x1 * sn[:, None, :]
+    x[..., 1] = x0 * sn[:, None, :] + x1 * cs[:, None, :]
+    close(c, r, 1e-2, "bias+rope")
+
+
+def test_fp8_relu_dropout_keep_bits_match_bf16_kernel():
+    """The fp8 ReLU-dropout epilogue draws the same keep pattern (seed, element)
+    as the bf16 kernel: with every pre-activation positive, the keep&positive bit
+    words of both kernels are identical (M = 2048: the bf16 ring kernel needs
+    >= 32 tiles)."""
+    M, N, K_ = 2048, 1024, 1024
+    a = rnd(M, K_, dtype=torch.bfloat16, seed=11).to(DEV)
+    b = rnd(N, K_, dtype=torch.bfloat16, seed=12, scale=0.01).to(DEV)
+    bias = torch.full((N,), 50.0, device=DEV)
+    qa, sa = quant_gpu(a)
+    qb, sb = quant_gpu(b)
+    c8 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    c16 = torch.empty_like(c8)
+    kw = dict(epilogue=K.EPI_BIAS_RELU_DROP, bias=bias, p_drop=0.3, seed=1234)
+    words = K.gemm_relu_mask_words(a, b, c16, M, N, K_, **kw)
+    assert words > 0 and K.gemm_relu_mask_words(qa, qb, c8, M, N, K_, a_scale=sa, b_scale=sb, **kw) == words
+    m8 = torch.zeros(words, dtype=torch.int64, device=DEV)
+    m16 = torch.zeros_like(m8)
+    K.gemm(qa, qb, c8, M, N, K_, a_scale=sa, b_scale=sb, relu_mask=m8, **kw)
+    K.gemm(a, b, c16, M, N, K_, relu_mask=m16, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(m8, m16)
+    assert torch.equal(c8 == 0, c16 == 0)
+    keep = (c16 != 0).float().mean().item()
+    assert 0.65 < keep < 0.75
+
+
+def test_fp8_gemm_rejects_bad_layouts():
+    qa, sa, qb, sb = fp8_operands(256, 256, 128, 1)
+    c = torch.empty(256, 256, dtype=torch.float32, device=DEV)
+    with pytest.raises(RuntimeError, match="K-major"):
+        K.gemm(qa, qb, c, 256, 256, 128, a_scale=sa, b_scale=sb, a_kmajor=False, lda=256)
+    with pytest.raises(RuntimeError, match="row scales"):
+        K.gemm(qa, qb, c, 256, 256, 128, a_scale=sa)
+    with pytest.raises(RuntimeError, match="K % 64"):
+        K.gemm(qa[:, :96], qb[:, :96], c, 256, 256, 96, a_scale=sa, b_scale=sb, lda=128, ldb=128)
+
+
+def test_fp8_model_forward_and_step():
+    """Whole model in fp8 mode (C5): the forward stays within a few percent of the
+    fp32 oracle (reported tolerance: relative L2 error < 5e-2; bf16 mode sits near
+    1e-2), differs from bf16 mode (the fp8 GEMMs ran), and a training step runs
+    and re-quantizes the updated weights on the next forward."""
+    from neurosync_trainer_lite_amd.config import training_config
+    from neurosync_trainer_lite_amd.utils.model_utils import build_model, prepare_training_components
+    from oracle import model_ref
+    D, H, L, B, T = 256, 4, 2, 4, 64
+    cfg = dict(training_config, hidden_dim=D, num_heads=H, n_layers=L, dropout=0.0, use_amp=True, use_fp8=True)
+    model = build_model(cfg, DEV)
+    params = model_ref.seeded_params(model_ref.param_shapes(256, D, L, 61), 21)
+    model.load_state_dict(params, strict=True)
+    g = torch.Generator().manual_seed(5)
+    src = torch.randn(B, T, 256, generator=g)
+    trg = torch.randn(B, T, 61, generator=g) * 20
+    with torch.no_grad():
+        ref = model_ref.seq2seq_forward(params, src, H).double()
+        model.eval()
+        p8 = model(src.to(DEV)).double().cpu()
+        model.set_fp8(False)
+        p16 = model(src.to(DEV)).double().cpu()
+        model.set_fp8(True)
+    rel8 = ((p8 - ref).norm() / ref.norm()).item()
+    rel16 = ((p16 - ref).norm() / ref.norm()).item()
+    assert rel8 < 5e-2, (rel8, rel16)
+    assert not torch.equal(p8, p16)
+    model.train()
+    crit, opt, _ = prepare_training_components(cfg, model)
+    losses = []
+    for _ in range(2):
+        opt.zero_grad()
+        loss = crit(model(src.to(DEV)), trg.to(DEV))
+        loss.backward()
+        opt.step(max_norm=2.0)
+        losses.append(loss.item())
+    assert all(l == l for l in losses)
+    eng = model.engine()
+    q, sc = eng._fp8_w[("encoder.transformer_encoder.0.ffn.linear1.weight", 1)]
+    w = eng.w("encoder.transformer_encoder.0.ffn.linear1.weight")
+    q_ref, s_ref = fp8_ref.quant_rows(w.cpu())
+    with torch.no_grad():
+        model.eval()
+        model(src.to(DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(sc.cpu(), s_ref) and torch.equal(q.cpu().view(torch.uint8), q_ref.view(torch.uint8))
