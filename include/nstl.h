@@ -170,6 +170,10 @@ typedef struct nstl_ln_args {
   const void* dout2;       /* optional dtype [rows][D], added to dout: the input gradient
                               of a Linear fed by this LN's output, kept in dtype as the
                               reference's autocast casts it (utils/model.py Linears) */
+  /* forward, optional (bf16 only): the row-wise e4m3 copy of `out` [rows][ldq8] and
+     its row scales, exactly nstl_fp8_quant_rows(out) (the fp8 q/k/v / FFN GEMM
+     operand of BASELINE config C5) */
+  void* q8; int64_t ldq8; float* q8_scale;
 } nstl_ln_args;
 int nstl_ln_fwd(const nstl_ln_args* args, void* stream);
 int nstl_ln_bwd(const nstl_ln_args* args, void* stream);

@@ -71,6 +71,7 @@ class LnArgs(ctypes.Structure):
         ("rot_out", _vp), ("rope_cos", _vp), ("rope_sin", _vp), ("rope_T", _i32),
         ("s_in", _vp), ("dout", _vp), ("ds", _vp), ("dbranch", _vp),
         ("dgamma_part", _vp), ("dbeta_part", _vp), ("n_part", _i32), ("dbranch_part", _vp), ("dout2", _vp),
+        ("q8", _vp), ("ldq8", _i64), ("q8_scale", _vp),
     ]
 
 

@@ -64,6 +64,7 @@ struct LnParams {
   const char* s_in; const float* dout; float* ds; char* dbranch;
   const char* dout2;  // optional dtype addend of dout
   float* dgp; float* dbp; float* dyp;
+  uint8_t* q8; int64_t ldq8; float* q8_scale;  // forward: row-wise e4m3 copy of out (fp8.hip rule)
 };
 
 // dropout scale of the element pair (idx, idx+1), idx even: 1 or 2 stacked masks
@@ -420,6 +421,40 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel_il(LnParams p) {
     p.mean[row] = mean;
     p.rstd[row] = rstd;
   }
+  if (p.q8) {  // the same arithmetic as nstl_fp8_quant_rows on the stored row
+    float am = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) am = fmaxf(am, fabsf(o[j]));
+    am = wave_max(am);
+    const float inv = am > 0.f ? 448.f / am : 1.f;
+    if (lane == 0) p.q8_scale[row] = am > 0.f ? am / 448.f : 1.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fminf(fmaxf(o[4 * k + e] * inv, -448.f), 448.f);
+      const uint32_t b = ((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false) & 0xffffu) |
+                         (((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], 0, false) & 0xffffu) << 16);
+      *(uint32_t*)(p.q8 + (int64_t)row * p.ldq8 + k * 256 + 4 * lane) = b;
+    }
+  }
+  if (p.q8) {  // the same arithmetic as nstl_fp8_quant_rows on the stored row
+    float am = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) am = fmaxf(am, fabsf(o[j]));
+    am = wave_max(am);
+    const float inv = am > 0.f ? 448.f / am : 1.f;
+    if (lane == 0) p.q8_scale[row] = am > 0.f ? am / 448.f : 1.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fminf(fmaxf(o[4 * k + e] * inv, -448.f), 448.f);
+      const uint32_t b = ((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false) & 0xffffu) |
+                         (((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], 0, false) & 0xffffu) << 16);
+      *(uint32_t*)(p.q8 + (int64_t)row * p.ldq8 + k * 256 + 4 * lane) = b;
+    }
+  }
   if (p.rot_out) {
     const int t = row % p.rope_T, half = p.D >> 1;
 #pragma unroll
@@ -479,6 +514,7 @@ int fill(LnParams& p, const nstl_ln_args* a) {
   p.s_in = (const char*)a->s_in; p.dout = a->dout; p.ds = a->ds; p.dbranch = (char*)a->dbranch;
   p.dgp = a->dgamma_part; p.dbp = a->dbeta_part; p.dyp = a->dbranch_part;
   p.dout2 = (const char*)a->dout2;
+  p.q8 = (uint8_t*)a->q8; p.ldq8 = a->ldq8; p.q8_scale = a->q8_scale;
   return 0;
 }
 
@@ -490,6 +526,9 @@ extern "C" int nstl_ln_fwd(const nstl_ln_args* a, void* stream) {
   if (rc) return rc;
   NSTL_CHECK_ARG(a->y && a->out && a->mean && a->rstd, "nstl_ln_fwd: null tensor");
   NSTL_CHECK_ARG(!a->rot_out || (a->rope_cos && a->rope_sin && a->rope_T > 0), "nstl_ln_fwd: rope tables");
+  NSTL_CHECK_ARG(!a->q8 || (a->dtype == NSTL_BF16 && a->q8_scale && a->D % 256 == 0 && a->ldq8 >= a->D &&
+                            a->ldq8 % 16 == 0 && ((uintptr_t)a->q8 % 16) == 0),
+                 "nstl_ln_fwd: q8 needs bf16, D %% 256 == 0, q8_scale and a 16-byte aligned ldq8 >= D");
   const int grid = (a->rows + NT / 64 - 1) / (NT / 64);
   return a->dtype == NSTL_BF16 ? dispatch<bf16, false>(p, grid, (hipStream_t)stream)
                                : dispatch<float, false>(p, grid, (hipStream_t)stream);

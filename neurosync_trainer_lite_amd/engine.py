@@ -209,6 +209,7 @@ class Seq2SeqEngine:
         self.fp8 = False
         self._fp8_w = None         # (weight name, rows) -> (e4m3 [rows*N, K], f32 scales [rows*N])
         self._fp8_act = {}         # M -> (e4m3 scratch [M, max(D, Fd)], scales [M], e4m3 mem, mem scales)
+        self._xq = {}              # data_ptr of an activation -> its live e4m3 copy (q, scales)
         self._red = None           # pending (part, ld, n_part, cols, out, beta) jobs
         self._ln_slot = 0          # next LayerNorm partial buffer of the layer
         self._ab_slot = 0          # next attention bias partial buffer of the layer
@@ -437,13 +438,22 @@ class Seq2SeqEngine:
             self._fp8_act = {M: (e8(M, max(self.D, self.Fd)), f(M), e8(M, self.D), f(M))}
         return self._fp8_act[M]
 
-    def _fp8_quant(self, x, mem=False):
-        """Row-wise e4m3 copy of activation x [M, cols] (the scratch, or the decoder's
-        memory buffer that all cross-attention k|v projections share)."""
+    def _fp8_target(self, x, mem):
+        """Where the e4m3 copy of x goes: the scratch (valid until the next copy
+        into it) or the decoder memory's own buffer (all cross-attention k|v
+        projections of a forward share it)."""
         M, cols = x.shape
         q, sc, qm, sm = self._fp8_bufs(M)
-        q, sc = (qm, sm) if mem else (q[:, :cols], sc)
-        K.fp8_quant_rows([(x, M, cols, q, sc)], stream=self.st)
+        if mem:
+            return qm, sm
+        self._xq = {p: v for p, v in self._xq.items() if v[0].data_ptr() != q.data_ptr()}
+        return q[:, :cols], sc
+
+    def _fp8_quant(self, x, mem=False):
+        """Row-wise e4m3 copy of activation x [M, cols] by the standalone kernel."""
+        q, sc = self._fp8_target(x, mem)
+        K.fp8_quant_rows([(x, x.shape[0], x.shape[1], q, sc)], stream=self.st)
+        self._xq[x.data_ptr()] = (q, sc)
         return q, sc
 
     # ------------------------------------------------------------ primitives
@@ -458,7 +468,9 @@ class Seq2SeqEngine:
         m, n, k = x.shape[0], W.shape[0], W.shape[1]
         if self.fp8 and (wname, rows) in self._fp8_w:
             qw, sw = self._fp8_w[(wname, rows)]
-            x, sx = xq if xq is not None else self._fp8_quant(x)
+            if xq is None:
+                xq = self._xq.get(x.data_ptr()) or self._fp8_quant(x)
+            x, sx = xq
             W = qw
             kw.update(a_scale=sx, b_scale=sw)
         use = relu_mask is not None and self.relu_mask_on and \
@@ -577,7 +589,9 @@ class Seq2SeqEngine:
         else:
             self._dx(dy, wname, rows, bb.dres, 1.0)
 
-    def _ln(self, x, y, out, stats, prefix, n_masks, seeds, s_out, rot=None, T=None):
+    def _ln(self, x, y, out, stats, prefix, n_masks, seeds, s_out, rot=None, T=None, q8=None):
+        """LayerNorm tail; in fp8 mode (q8 = 'scratch' / 'mem') it also writes the
+        row-wise e4m3 copy of `out` that the next fp8 projection reads."""
         a = K.LnArgs()
         a.dtype = K.dtype_code(self.dt)
         a.rows, a.D = out.shape[0], self.D
@@ -589,7 +603,12 @@ class Seq2SeqEngine:
         if rot is not None:
             cs, sn = self.rope(T, self.D)
             a.rot_out, a.rope_cos, a.rope_sin, a.rope_T = rot.data_ptr(), cs.data_ptr(), sn.data_ptr(), T
+        if self.fp8 and q8 is not None:
+            q, sc = self._fp8_target(out, q8 == "mem")
+            a.q8, a.ldq8, a.q8_scale = q.data_ptr(), q.stride(0), sc.data_ptr()
         K.ln_fwd(a, stream=self.st)
+        if self.fp8 and q8 is not None:
+            self._xq[out.data_ptr()] = (q, sc)
 
     def _ln_bwd(self, s_in, stats, prefix, dres_in, dres_out, dbranch, n_masks, seeds, bf, bias_of=None):
         """LayerNorm(+dropout+residual) backward; with `bias_of`, the column sums of
@@ -695,7 +714,8 @@ class Seq2SeqEngine:
         self._gemm_fwd(o, pre + "self_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         st = bb.layer(bb.e_stats, l)
         x1 = bb.layer(bb.e_x1, l)
-        self._ln(x, bb.y, x1, st[0:2], pre + "norm1", 2, (sd("resid"), sd("drop1")), bb.layer(bb.e_s1, l))
+        self._ln(x, bb.y, x1, st[0:2], pre + "norm1", 2, (sd("resid"), sd("drop1")), bb.layer(bb.e_s1, l),
+                 q8="scratch")
         h = bb.layer(bb.e_h, l)
         ok = self._gemm_fwd(x1, pre + "ffn.linear1.weight", h, K.EPI_BIAS_RELU_DROP, p_drop=self.p, seed=sd("ffn"),
                             relu_mask=bb.e_rmask[l] if bb.save else None)
@@ -703,7 +723,8 @@ class Seq2SeqEngine:
             bb.e_rmask_ok[l] = ok
         self._gemm_fwd(h, pre + "ffn.linear2.weight", bb.y, K.EPI_BIAS)
         x2 = bb.layer(bb.e_x2, l)
-        self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 1, (sd("drop2"), 0), bb.layer(bb.e_s2, l))
+        self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 1, (sd("drop2"), 0), bb.layer(bb.e_s2, l),
+                 q8="scratch" if l + 1 < self.L else None)
         return x2
 
     def _dec_layer(self, bb, l, x, mem, T):
@@ -719,7 +740,7 @@ class Seq2SeqEngine:
                    mask=bb.d_mask[l] if bb.save else None)
         self._gemm_fwd(L_(bb.d_o), pre + "self_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         x1 = L_(bb.d_x1)
-        self._ln(x, bb.y, x1, st[0:2], pre + "norm1", 2, (sd("resid"), sd("drop1")), L_(bb.d_s1))
+        self._ln(x, bb.y, x1, st[0:2], pre + "norm1", 2, (sd("resid"), sd("drop1")), L_(bb.d_s1), q8="scratch")
         qc, kvc = L_(bb.d_qc), L_(bb.d_kvc)
         self._gemm_fwd(x1, pre + "multihead_attn.q_linear.weight", qc, K.EPI_BIAS_ROPE,
                        rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D)
@@ -729,7 +750,7 @@ class Seq2SeqEngine:
                    mask=bb.d_maskc[l] if bb.save else None)
         self._gemm_fwd(L_(bb.d_oc), pre + "multihead_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         x2 = L_(bb.d_x2)
-        self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 2, (sd("xresid"), sd("drop2x")), L_(bb.d_s2))
+        self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 2, (sd("xresid"), sd("drop2x")), L_(bb.d_s2), q8="scratch")
         h = L_(bb.d_h)
         ok = self._gemm_fwd(x2, pre + "ffn.linear1.weight", h, K.EPI_BIAS_RELU_DROP, p_drop=self.p, seed=sd("ffn"),
                             relu_mask=bb.d_rmask[l] if bb.save else None)
@@ -737,13 +758,15 @@ class Seq2SeqEngine:
             bb.d_rmask_ok[l] = ok
         self._gemm_fwd(h, pre + "ffn.linear2.weight", bb.y, K.EPI_BIAS)
         x3 = L_(bb.d_x3)
-        self._ln(x2, bb.y, x3, st[4:6], pre + "norm3", 1, (sd("drop3"), 0), L_(bb.d_s3))
+        self._ln(x2, bb.y, x3, st[4:6], pre + "norm3", 1, (sd("drop3"), 0), L_(bb.d_s3),
+                 q8="scratch" if l + 1 < self.L else None)
         return x3
 
     def _prologue(self, training):
         self.ensure_bound()
         self.st = K.stream_of(self.device)
         self.p = float(self.dropout) if training else 0.0
+        self._xq = {}  # e4m3 activation copies never outlive a forward
         if self.fp8:
             self._fp8_weights()
 
@@ -762,7 +785,7 @@ class Seq2SeqEngine:
         x = bb.x0
         for l in range(self.L):
             x = self._enc_layer(bb, l, x, T)
-        self._ln(None, x, bb.mem, bb.encf_stats, "encoder.layer_norm", 0, (0, 0), None, rot=bb.xdec0, T=T)
+        self._ln(None, x, bb.mem, bb.encf_stats, "encoder.layer_norm", 0, (0, 0), None, rot=bb.xdec0, T=T, q8="mem")
         return bb.mem
 
     def decode(self, bb, mem, T, xdec0=None):
@@ -771,7 +794,7 @@ class Seq2SeqEngine:
             K.rope(mem, self.D, bb.xdec0, self.D, bb.M, self.D, *self.rope(T, self.D), T, self.D, stream=self.st)
             xdec0 = bb.xdec0
         x = xdec0
-        self._mem_q = self._fp8_quant(mem, mem=True) if self.fp8 else None
+        self._mem_q = (self._xq.get(mem.data_ptr()) or self._fp8_quant(mem, mem=True)) if self.fp8 else None
         for l in range(self.L):
             x = self._dec_layer(bb, l, x, mem, T)
         self._ln(None, x, bb.xf, bb.decf_stats, "decoder.layer_norm", 0, (0, 0), None)

@@ -208,3 +208,30 @@ def test_fp8_model_forward_and_step():
         model(src.to(DEV))
     torch.cuda.synchronize()
     assert torch.equal(sc.cpu(), s_ref) and torch.equal(q.cpu().view(torch.uint8), q_ref.view(torch.uint8))
+
+
+def test_ln_fwd_fused_fp8_copy_matches_standalone():
+    """nstl_ln_fwd's optional q8 output is exactly nstl_fp8_quant_rows of its
+    bf16 output (LayerNorm -> fp8 projection hand-off of config C5)."""
+    rows, D = 300, 1024
+    x = rnd(rows, D, dtype=torch.bfloat16, seed=1).to(DEV)
+    y = rnd(rows, D, dtype=torch.bfloat16, seed=2).to(DEV)
+    gamma = (1 + 0.1 * rnd(D, seed=3)).to(DEV)
+    beta = (0.1 * rnd(D, seed=4)).to(DEV)
+    out = torch.empty(rows, D, dtype=torch.bfloat16, device=DEV)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    q8 = torch.zeros(rows, D + 64, dtype=torch.float8_e4m3fn, device=DEV)
+    s8 = torch.empty(rows, device=DEV)
+    a = K.LnArgs()
+    a.dtype, a.rows, a.D = K.BF16, rows, D
+    a.x, a.y = x.data_ptr(), y.data_ptr()
+    a.n_masks, a.p_drop, a.seed1, a.seed2 = 2, 0.3, 11, 12
+    a.gamma, a.beta, a.eps = gamma.data_ptr(), beta.data_ptr(), 1e-5
+    a.out, a.mean, a.rstd = out.data_ptr(), mean.data_ptr(), rstd.data_ptr()
+    a.q8, a.ldq8, a.q8_scale = q8.data_ptr(), q8.stride(0), s8.data_ptr()
+    K.ln_fwd(a)
+    torch.cuda.synchronize()
+    q_ref, s_ref = fp8_ref.quant_rows(out.cpu())
+    assert torch.equal(s8.cpu(), s_ref)
+    assert torch.equal(q8[:, :D].cpu().view(torch.uint8), q_ref.view(torch.uint8))
