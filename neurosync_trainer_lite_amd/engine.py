@@ -142,7 +142,8 @@ class _Buffers:
             self.e_mask = [e(nw, dtype=torch.int64) for _ in range(L)]
             self.d_mask = [e(nw, dtype=torch.int64) for _ in range(L)]
             self.d_maskc = [e(nw, dtype=torch.int64) for _ in range(L)]
-            self.n_part = max(1, min(256, M // 8))  # LN backward: >= 1 row per wave (8 waves)
+            # LN backward blocks (8 waves each, >= 1 row per wave); NSTL_LN_PARTS: A/B only
+            self.n_part = max(1, min(int(os.environ.get("NSTL_LN_PARTS", "256")), M // 8))
             # one per LayerNorm of a layer (3 in a decoder layer): batched reduction
             self.ln_parts = [e(3, self.n_part, D, dtype=f32) for _ in range(3)]
             self.ln_part = self.ln_parts[0]

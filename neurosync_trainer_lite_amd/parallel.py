@@ -44,6 +44,11 @@ def init_from_env(backend=None):
         return 0, 1, 0
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    # NSTL_DIST_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on
+    # the GPUs there are (rank -> GPU local % count); gloo carries the collectives
+    backend = backend or os.environ.get("NSTL_DIST_BACKEND") or None
+    if backend == "gloo" and torch.cuda.is_available():
+        local = local % torch.cuda.device_count()
     if not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
