@@ -1,7 +1,7 @@
 """Aggregate rocprofv3 FETCH_SIZE / WRITE_SIZE passes into the per-launch HBM
 traffic of the GEMM family (the bench's dominant kernel) -> JSON for bench.py.
 
-  python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> <tag>
+  python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> <tag> [kernel-name filter]
 
 Corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE is reported in KiB and counts
 a wide coalesced streaming read at exactly half its bytes on gfx950 -> x2;
@@ -14,14 +14,14 @@ import os
 import sys
 
 
-def per_dispatch(d, counter):
+def per_dispatch(d, counter, only=None):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"]
-            if "gemm" not in name or "splitk" in name:
+            if "gemm" not in name or "splitk" in name or (only and only not in name):
                 continue
             key = int(r["Dispatch_Id"])
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
@@ -30,14 +30,16 @@ def per_dispatch(d, counter):
 
 def main():
     fetch_dir, write_dir, out, tag = sys.argv[1:5]
-    fetch = per_dispatch(fetch_dir, "FETCH_SIZE")
-    write = per_dispatch(write_dir, "WRITE_SIZE")
+    only = sys.argv[5] if len(sys.argv) > 5 else None  # kernel-name filter (e.g. gemm256f8)
+    fetch = per_dispatch(fetch_dir, "FETCH_SIZE", only)
+    write = per_dispatch(write_dir, "WRITE_SIZE", only)
     n_f, n_w = len(fetch), len(write)
     f_kib = sum(fetch.values()) / max(1, n_f)
     w_kib = sum(write.values()) / max(1, n_w)
     res = {
         "tag": tag,
-        "kernel": "nstl GEMM family (gemm256r_kernel / gemm_kernel), every dispatch of the profiled bench run",
+        "kernel": (only + " dispatches" if only else "nstl GEMM family (gemm256r_kernel / gemm_kernel), every dispatch")
+                  + " of the profiled bench run",
         "dispatches_fetch": n_f, "dispatches_write": n_w,
         "fetch_size_kib_per_launch_raw": round(f_kib, 1),
         "write_size_kib_per_launch": round(w_kib, 1),
