@@ -296,11 +296,41 @@ __global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void at
   if (g == 0) p.lse[(int64_t)bh * T_ + q0 + c] = m * p.scale + logf(sum);
 }
 
-// rotate a (row t, col d) accumulator element back by -theta (RoPE^T)
-NSTL_DEV float rope_back(float v, int t, int d, const float* cs, const float* sn) {
-  const float partner = __shfl_xor(v, 1);
-  const float c = cs[t * (DH / 2) + (d >> 1)], s = sn[t * (DH / 2) + (d >> 1)];
-  return (d & 1) ? (v * c - partner * s) : (v * c + partner * s);
+// RoPE^T: rotate (row t, col d) accumulator elements back by -theta
+// partner element of a RoPE pair: lane c <-> c ^ 1 (DPP quad_perm [1,0,3,2], no LDS)
+NSTL_DEV float swap_pair(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+// RoPE^T over a lane's 16 x 64 tile elements v[dt][r] = (row0 + r, d = 16 dt + c):
+// the 32 table reads are issued together (rope_tab), the pair swaps are DPP
+// moves (the per-element form waited on one ds_bpermute and two table reads at
+// a time).  Tables [T][RS] with row stride RS floats (32 in global memory, 36
+// in the fused kernel's LDS copy: the rows 4g + r of a wave's four lane groups
+// then fall on distinct banks).  rope_apply needs every lane of the wave active.
+template <int RS>
+NSTL_DEV void rope_tab(float (&tc)[4][4], float (&ts)[4][4], int row0, int c, const float* cs, const float* sn) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int i = (row0 + r) * RS + dt * 8 + (c >> 1);
+      tc[dt][r] = cs[i];
+      ts[dt][r] = sn[i];
+    }
+}
+NSTL_DEV void rope_apply(float (&v)[4][4], const float (&tc)[4][4], const float (&ts)[4][4], int c) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const float x = v[dt][r], partner = swap_pair(x);
+      v[dt][r] = (c & 1) ? (x * tc[dt][r] - partner * ts[dt][r]) : (x * tc[dt][r] + partner * ts[dt][r]);
+    }
+}
+NSTL_DEV void rope_back_tile(float (&v)[4][4], int row0, int c, const float* cs, const float* sn) {
+  float tc[4][4], ts[4][4];
+  rope_tab<DH / 2>(tc, ts, row0, c, cs, sn);
+  rope_apply(v, tc, ts, c);
 }
 
 // Bias gradients fused into the backward stores: column sums of a wave's stored
@@ -456,16 +486,10 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
   }
   float vq[4][4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int q = q0 + 4 * g + r;
+  for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int d = dt * 16 + c;
-      float x = dq[dt][r] * p.scale;
-      if (p.rope_q) x = rope_back(x, q, d, p.rope_cos, p.rope_sin);
-      vq[dt][r] = x;
-    }
-  }
+    for (int dt = 0; dt < 4; ++dt) vq[dt][r] = dq[dt][r] * p.scale;
+  if (p.rope_q) rope_back_tile(vq, q0 + 4 * g, c, p.rope_cos, p.rope_sin);
   store_tile16x64<T>(vq, scratch + w * 16 * RBK, p.dq + ((tok0 + q0) * p.dq_ld + h * DH) * ESZ, p.dq_ld, lane);
   if (bias_row) {
     wave_colsum16x64<T>(vq, red, w, lane);
@@ -583,17 +607,13 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
   }
   float vk[4][4], vv[4][4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int key = k0 + 4 * g + r;
+  for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const int d = dt * 16 + c;
-      float x = dk[dt][r] * p.scale;
-      if (p.rope_k) x = rope_back(x, key, d, p.rope_cos, p.rope_sin);
-      vk[dt][r] = x;
+      vk[dt][r] = dk[dt][r] * p.scale;
       vv[dt][r] = dv[dt][r];
     }
-  }
+  if (p.rope_k) rope_back_tile(vk, k0 + 4 * g, c, p.rope_cos, p.rope_sin);
   char* scr = scratch + w * 16 * RBK;
   store_tile16x64<T>(vk, scr, p.dk + ((tok0 + k0) * p.dk_ld + h * DH) * ESZ, p.dk_ld, lane);
   store_tile16x64<T>(vv, scr, p.dv + ((tok0 + k0) * p.dv_ld + h * DH) * ESZ, p.dv_ld, lane);
@@ -625,8 +645,21 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
 //   phase 2 : barrier; dS^T -> image; barrier; dQ = dS K
 //   stores  : barrier; dQ, dK, dV rows (+ bias column sums, last wave out)
 constexpr int FUSED_MAX_T = 128;
+// LDS map after phase 2: staging [0, 16 KB), bias partials [16 KB, 22 KB), RoPE
+// tables [22 KB, 58 KB) over the dead K image / lse / D, then the counter
+constexpr int FUSED_ROPE_OFF = 8 * 16 * DH * 2 + 3 * 8 * 64 * 4;
+constexpr int FUSED_RS = DH / 2 + 4;  // padded table row (floats): 144 B, 16-byte aligned
+constexpr int FUSED_ARRIVED_OFF = FUSED_ROPE_OFF + 2 * FUSED_MAX_T * FUSED_RS * 4;
 constexpr int FUSED_DS_RB = FUSED_MAX_T * 2;  // dS^T image row: 128 queries (bf16)
 typedef ImgMN<FUSED_DS_RB> DsImg;
+
+// 16-byte chunk idx of the concatenated cos | sin tables (nchunk chunks each);
+// past the end it re-reads the last chunk (the caller does not store it)
+NSTL_DEV uint4 rope_chunk(const AttnParams& p, int idx, int nchunk) {
+  idx = min(idx, 2 * nchunk - 1);
+  const uint4* src = idx < nchunk ? (const uint4*)p.rope_cos + idx : (const uint4*)p.rope_sin + (idx - nchunk);
+  return *src;
+}
 
 __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p) {
   typedef bf16x8 Frag;
@@ -641,9 +674,11 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
   char* Kimg = smem + 2 * FUSED_MAX_T * RBK;                   // [128][128 B]
   float* lse_s = (float*)(Kimg + FUSED_MAX_T * RBK);
   float* d_s = lse_s + FUSED_MAX_T;
-  unsigned* arrived = (unsigned*)(d_s + FUSED_MAX_T);
   char* scratch = smem;                                        // after phase 2: [NW][16][RBK]
   float* red = (float*)(smem + NW * 16 * RBK);                 // after phase 2: [3][NW][64]
+  float* cos_s = (float*)(smem + FUSED_ROPE_OFF);              // after phase 2: RoPE tables [T][DH/2] x 2
+  float* sin_s = cos_s + T_ * FUSED_RS;
+  unsigned* arrived = (unsigned*)(smem + FUSED_ARRIVED_OFF);
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -744,6 +779,19 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
     }
   }
   __syncthreads();  // every wave is done with the Q / dO images
+  // RoPE tables for the epilogue's rope_back: 16-byte loads issued now, their
+  // latency hidden under the dS^T write and dQ; to LDS once the K image is
+  // dead.  (Read per element from global memory they cost ~16 dependent L2
+  // round trips per wave: 95 -> 79 us per call with RoPE^T off.)
+  const bool rope = p.rope_q || p.rope_k;
+  const int nchunk = T_ * (DH / 2) / 4;  // 16-byte chunks per table
+  uint4 rt0 = {}, rt1 = {}, rt2 = {}, rt3 = {};
+  if (rope) {
+    rt0 = rope_chunk(p, tid, nchunk);
+    rt1 = rope_chunk(p, tid + BWD_NT, nchunk);
+    rt2 = rope_chunk(p, tid + 2 * BWD_NT, nchunk);
+    rt3 = rope_chunk(p, tid + 3 * BWD_NT, nchunk);
+  }
   if (act) {
     // dS^T row = key k0 + c; fragment j holds queries 32j + 4g + 0..3 and 32j + 16 + 4g + 0..3
 #pragma unroll
@@ -775,23 +823,37 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
       }
     }
   }
-  __syncthreads();  // the dS^T / K images become output staging
+  __syncthreads();  // the dS^T / K images become output staging and RoPE tables
+  if (rope) {
+    // chunk idx (8 per 32-float table row) -> row-padded image, sin_s = cos_s + T * FUSED_RS
+    auto put = [&](int idx, const uint4& v) {
+      if (idx < 2 * nchunk) {
+        const int t = idx < nchunk ? idx : idx - nchunk;
+        *(uint4*)(cos_s + (idx < nchunk ? 0 : T_ * FUSED_RS) + (t >> 3) * FUSED_RS + (t & 7) * 4) = v;
+      }
+    };
+    put(tid, rt0);
+    put(tid + BWD_NT, rt1);
+    put(tid + 2 * BWD_NT, rt2);
+    put(tid + 3 * BWD_NT, rt3);
+    __syncthreads();
+  }
   float vq[4][4], vk[4][4], vv[4][4];
   float* bias_row = p.dbias ? p.dbias + (int64_t)b * 3 * p.H * DH : nullptr;
-  if (act) {  // wave-uniform: rope_back's lane shuffles see the whole wave
+  if (act) {  // wave-uniform: rope_back_tile's DPP swaps see the whole wave
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = k0 + 4 * g + r;
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const int d = dt * 16 + c;
-        float xq = dq[dt][r] * p.scale, xk = dk[dt][r] * p.scale;
-        if (p.rope_q) xq = rope_back(xq, row, d, p.rope_cos, p.rope_sin);
-        if (p.rope_k) xk = rope_back(xk, row, d, p.rope_cos, p.rope_sin);
-        vq[dt][r] = xq;
-        vk[dt][r] = xk;
+        vq[dt][r] = dq[dt][r] * p.scale;
+        vk[dt][r] = dk[dt][r] * p.scale;
         vv[dt][r] = dv[dt][r];
       }
+    if (rope) {  // dQ and dK rows are the same 16: one table read for both
+      float tc[4][4], ts[4][4];
+      rope_tab<FUSED_RS>(tc, ts, k0 + 4 * g, c, cos_s, sin_s);
+      if (p.rope_q) rope_apply(vq, tc, ts, c);
+      if (p.rope_k) rope_apply(vk, tc, ts, c);
     }
     char* scr = scratch + w * 16 * RBK;
     const int64_t r0 = tok0 + k0;
@@ -815,7 +877,9 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
     }
   }
 }
-constexpr size_t FUSED_LDS = 3 * FUSED_MAX_T * DH * 2 + 2 * FUSED_MAX_T * 4 + 16;
+constexpr size_t FUSED_LDS = FUSED_ARRIVED_OFF + 16;  // 58 KB: two workgroups per CU
+static_assert(FUSED_ARRIVED_OFF >= 3 * FUSED_MAX_T * DH * 2 + 2 * FUSED_MAX_T * 4, "counter past the images");
+static_assert(FUSED_ROPE_OFF % 16 == 0, "16-byte table chunks");
 static_assert(8 * 16 * DH * 2 + 3 * 8 * 64 * 4 <= 3 * FUSED_MAX_T * DH * 2, "staging must fit in the images");
 
 size_t fwd_lds_bytes(int T, int esz) {  // K, V images + per-wave output staging
@@ -1154,8 +1218,11 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
     if ((rc = launch(attn_bwd_dq_generic<float>, grid, lq, st, p, "nstl_attn_bwd generic dq"))) return rc;
     return launch(attn_bwd_dkv_generic<float>, grid, lkv, st, p, "nstl_attn_bwd generic dkv");
   }
-  if (use_fused_bwd(a))
+  if (use_fused_bwd(a)) {
+    NSTL_CHECK_ARG(!(a->rope_q || a->rope_k) || ((((uintptr_t)a->rope_cos) | ((uintptr_t)a->rope_sin)) & 15) == 0,
+                   "nstl_attn_bwd: RoPE tables must be 16-byte aligned");
     return launch(attn_bwd_fused_kernel, dim3(1, a->B * a->H), FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
+  }
   dim3 grid((a->T + BWD_ROWS - 1) / BWD_ROWS, a->B * a->H);
   const size_t lds = bwd_lds_bytes(a->T, esz);
   if (a->dtype == NSTL_BF16) {

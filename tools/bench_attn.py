@@ -47,7 +47,8 @@ for p in (0.3, 0.0):
         a.dout, a.dout_ld = do.data_ptr(), D
         a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dqkv.data_ptr(), 3 * D, dqkv[:, D:].data_ptr(), 3 * D,
                                                         dqkv[:, 2 * D:].data_ptr(), 3 * D)
-        a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
+        rope = 0 if os.environ.get("NSTL_BENCH_NOROPE") == "1" else 1   # RoPE^T off: its cost in the epilogue
+        a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), rope, rope
         a.dsum = dsum.data_ptr()
         if mask is not None:
             a.mask_bits = mask.data_ptr()
