@@ -42,6 +42,7 @@ struct AttnParams {
   char* dk; int64_t dk_ld;
   char* dv; int64_t dv_ld;
   const float* rope_cos; const float* rope_sin; int rope_q, rope_k;
+  int rope_fast;  // fused backward: RoPE^T angles recomputed with v_sin / v_cos instead of the tables
   int B, T, H, dh;
   float scale;
   uint32_t thresh; float inv_keep; uint64_t seed;
@@ -326,6 +327,23 @@ NSTL_DEV void rope_apply(float (&v)[4][4], const float (&tc)[4][4], const float 
       const float x = v[dt][r], partner = swap_pair(x);
       v[dt][r] = (c & 1) ? (x * tc[dt][r] - partner * ts[dt][r]) : (x * tc[dt][r] + partner * ts[dt][r]);
     }
+}
+// The same cos / sin values recomputed: angle = float(t) * inv_freq_i exactly as
+// rotation_tables() forms it (f32 product), then the hardware sin / cos
+// (v_sin_f32 / v_cos_f32 on angle / 2pi).  Against the f32 tables the error is
+// ~1e-6 absolute, far below the bf16 rounding of the dQ / dK it rotates.
+NSTL_DEV void rope_tab_fast(float (&tc)[4][4], float (&ts)[4][4], int row0, int c) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const float two_i = (float)(2 * (dt * 8 + (c >> 1)));
+    const float inv_freq = expf(-9.21034049987793f * two_i / (float)DH);  // f32(ln 10000)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a = (float)(row0 + r) * inv_freq;
+      ts[dt][r] = __sinf(a);
+      tc[dt][r] = __cosf(a);
+    }
+  }
 }
 NSTL_DEV void rope_back_tile(float (&v)[4][4], int row0, int c, const float* cs, const float* sn) {
   float tc[4][4], ts[4][4];
@@ -783,10 +801,10 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
   // latency hidden under the dS^T write and dQ; to LDS once the K image is
   // dead.  (Read per element from global memory they cost ~16 dependent L2
   // round trips per wave: 95 -> 79 us per call with RoPE^T off.)
-  const bool rope = p.rope_q || p.rope_k;
+  const bool rope = p.rope_q || p.rope_k, rope_tabs = rope && !p.rope_fast;
   const int nchunk = T_ * (DH / 2) / 4;  // 16-byte chunks per table
   uint4 rt0 = {}, rt1 = {}, rt2 = {}, rt3 = {};
-  if (rope) {
+  if (rope_tabs) {
     rt0 = rope_chunk(p, tid, nchunk);
     rt1 = rope_chunk(p, tid + BWD_NT, nchunk);
     rt2 = rope_chunk(p, tid + 2 * BWD_NT, nchunk);
@@ -824,7 +842,7 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
     }
   }
   __syncthreads();  // the dS^T / K images become output staging and RoPE tables
-  if (rope) {
+  if (rope_tabs) {
     // chunk idx (8 per 32-float table row) -> row-padded image, sin_s = cos_s + T * FUSED_RS
     auto put = [&](int idx, const uint4& v) {
       if (idx < 2 * nchunk) {
@@ -851,7 +869,8 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
       }
     if (rope) {  // dQ and dK rows are the same 16: one table read for both
       float tc[4][4], ts[4][4];
-      rope_tab<FUSED_RS>(tc, ts, k0 + 4 * g, c, cos_s, sin_s);
+      if (rope_tabs) rope_tab<FUSED_RS>(tc, ts, k0 + 4 * g, c, cos_s, sin_s);
+      else rope_tab_fast(tc, ts, k0 + 4 * g, c);
       if (p.rope_q) rope_apply(vq, tc, ts, c);
       if (p.rope_k) rope_apply(vk, tc, ts, c);
     }
@@ -1156,6 +1175,10 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   p.dv = (char*)a->dv; p.dv_ld = a->dv_ld;
   p.rope_cos = a->rope_cos; p.rope_sin = a->rope_sin;
   p.rope_q = a->rope_q; p.rope_k = a->rope_k;
+  {  // NSTL_ROPE_BWD=table: the fused backward reads the tables (A/B; read per call)
+    const char* e = getenv("NSTL_ROPE_BWD");
+    p.rope_fast = !(e && e[0] == 't');
+  }
   p.B = a->B; p.T = a->T; p.H = a->H; p.dh = a->dh;
   p.scale = 1.0f / sqrtf((float)a->dh);
   p.thresh = nstl_drop_thresh(a->p_drop);

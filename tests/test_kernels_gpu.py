@@ -438,8 +438,11 @@ def test_attention_bwd_fused_matches_split(T, monkeypatch):
     a.dsum = dsum.data_ptr()
     rows = K.attn_bias_rows(a)
     res = []
-    for mode in ("split", "fused"):
+    # fused: RoPE^T angles recomputed in the kernel (default); fused_table: from the tables
+    modes = ("split", "fused", "fused_table")
+    for mode in modes:
         monkeypatch.setenv("NSTL_ATTN_BWD", mode)
+        monkeypatch.setenv("NSTL_ROPE_BWD", "table" if mode == "fused_table" else "fast")
         dqkv = torch.full((M, 3 * D), float("nan"), dtype=dt, device=DEV)
         part = torch.full((rows, 3 * D), float("nan"), device=DEV)
         a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dqkv.data_ptr(), 3 * D, dqkv[:, D:].data_ptr(), 3 * D,
@@ -448,12 +451,16 @@ def test_attention_bwd_fused_matches_split(T, monkeypatch):
         K.attn_bwd(a)
         torch.cuda.synchronize()
         res.append((dqkv, part))
-    (ds, ps), (df, pf) = res
-    assert torch.isfinite(f64(df)).all() and torch.isfinite(f64(pf)).all()
-    for i, nm in enumerate(("dq", "dk", "dv")):
-        check(df[:, i * D:(i + 1) * D], ds[:, i * D:(i + 1) * D], 1e-2, "fused " + nm)
-    check(pf, f64(df).view(B, T, 3 * D).sum(1), 1e-5, "fused bias partials = column sums of the stored grads")
-    check(pf, ps, 1e-2, "fused vs split bias partials")
+    ds, ps = res[0]
+    for (df, pf), mode in zip(res[1:], modes[1:]):
+        assert torch.isfinite(f64(df)).all() and torch.isfinite(f64(pf)).all(), mode
+        for i, nm in enumerate(("dq", "dk", "dv")):
+            check(df[:, i * D:(i + 1) * D], ds[:, i * D:(i + 1) * D], 1e-2, mode + " " + nm)
+        check(pf, f64(df).view(B, T, 3 * D).sum(1), 1e-5, mode + " bias partials = column sums of the stored grads")
+        check(pf, ps, 1e-2, mode + " vs split bias partials")
+    # recomputed angles vs the tables: the same rotation to well inside bf16 rounding
+    for i in range(2):
+        check(res[1][0][:, i * D:(i + 1) * D], res[2][0][:, i * D:(i + 1) * D], 8e-3, "fast vs table RoPE^T")
 
 
 def test_attention_rejects_bad_shapes():
