@@ -48,6 +48,11 @@ struct AttnParams {
   uint32_t thresh; float inv_keep; uint64_t seed;
 };
 
+// 2^x as one v_exp_f32 (exp2f adds a denormal-range fix-up: 4 more vector
+// instructions per call; every argument here is <= 0 and a probability below
+// 2^-126 is 0 either way)
+NSTL_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // LDS-DMA rows [0, nrows) of a (b, h) slice (64 elements per row) into an
 // ImgK<RB> image.  One wave instruction moves 1 KB = 1024/RB rows; the image
 // swizzle is applied to the per-lane source chunk.
@@ -235,7 +240,7 @@ __global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void at
     if (kt < nkt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = exp2f((s[kt][r] - m) * c2);
+        const float e = fast_exp2((s[kt][r] - m) * c2);
         s[kt][r] = e;
         sum += e;
       }
@@ -254,10 +259,10 @@ __global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void at
         nstl_keep2(p.seed, idx, p.thresh, k[0], k[1]);
         nstl_keep2(p.seed, idx + 2, p.thresh, k[2], k[3]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[kt][r] = k[r] ? s[kt][r] * p.inv_keep : 0.f;
+        for (int r = 0; r < 4; ++r) s[kt][r] = k[r] ? s[kt][r] : 0.f;  // 1/(1-p): in the normalisation
         if (p.mask) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
+          for (int r = 0; r < 4; ++r) {  // lane kt*4 + r takes the wave's ballot of (kt, r)
             const uint64_t bal = __ballot(k[r]);
             if (lane == kt * 4 + r) {
               mlo = (uint32_t)bal;
@@ -287,9 +292,10 @@ __global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void at
   }
   // normalise (query 4g + r's sum is in lane 4g + r) and store 16-byte rows
   float ov[4][4];
+  const float keep_scale = p.thresh ? p.inv_keep : 1.f;  // dropout's 1/(1-p), applied to O instead of P
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const float inv = 1.f / __shfl(sum, 4 * g + r);
+    const float inv = keep_scale / __shfl(sum, 4 * g + r);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) ov[dt][r] = o[dt][r] * inv;
   }
@@ -488,7 +494,7 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(sc[r] * c2 - lq);
+        const float pv = fast_exp2(sc[r] * c2 - lq);
         float dpd = dp[r];
         if (p.thresh) dpd = keep[r] ? dpd * p.inv_keep : 0.f;
         dsv[u][r] = pv * (dpd - dqv);
@@ -601,7 +607,7 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = qt * 16 + 4 * g + r;
-        const float pv = exp2f(st[r] * c2 - lse_s[q]);
+        const float pv = fast_exp2(st[r] * c2 - lse_s[q]);
         float pdr = pv, dpd = dpt[r];
         if (p.thresh) {
           const bool keep = use_mask ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
@@ -772,7 +778,7 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int q = qt * 16 + 4 * g + r;
-            const float pv = exp2f(st[r] * c2 - lse_s[q]);
+            const float pv = fast_exp2(st[r] * c2 - lse_s[q]);
             float pdr = pv, dpd = dpt[r];
             if (p.thresh) {
               const bool keep = use_mask ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
