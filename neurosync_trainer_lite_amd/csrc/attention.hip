@@ -685,6 +685,9 @@ NSTL_DEV uint4 rope_chunk(const AttnParams& p, int idx, int nchunk) {
   return *src;
 }
 
+// DM: dropout mode, fixed per launch so the per-element loop carries no branch:
+// 0 none, 1 the forward's stored keep bits, 2 re-hashed (seed, element)
+template <int DM>
 __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p) {
   typedef bf16x8 Frag;
   constexpr int RBK = DH * 2;
@@ -729,9 +732,8 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
     }
   }
   // stored keep bits for this wave's 16 keys: lane 4*qt + r holds word (qt, k0/16, r)
-  const bool use_mask = p.thresh && p.mask;
   uint64_t mword = 0;
-  if (act && use_mask && (lane >> 2) < nkt) mword = p.mask[mask_word(bh, nkt, lane >> 2, k0 >> 4, lane & 3)];
+  if (DM == 1 && act && (lane >> 2) < nkt) mword = p.mask[mask_word(bh, nkt, lane >> 2, k0 >> 4, lane & 3)];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (act) {  // D of queries k0 + c (dO from its image, O from registers)
@@ -774,15 +776,15 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
           mma16(dpt, fb, fv[1]);
           // st[r] / dpt[r]: S / dP at (query 16qt + 4g + r, key k0 + c)
           uint32_t nib = 0;
-          if (use_mask) nib = (uint32_t)(shfl64(mword, 4 * qt + (lane & 3)) >> (16 * (c >> 2) + 4 * g));
+          if (DM == 1) nib = (uint32_t)(shfl64(mword, 4 * qt + (lane & 3)) >> (16 * (c >> 2) + 4 * g));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int q = qt * 16 + 4 * g + r;
             const float pv = fast_exp2(st[r] * c2 - lse_s[q]);
             float pdr = pv, dpd = dpt[r];
-            if (p.thresh) {
-              const bool keep = use_mask ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
-              pdr = keep ? pv * p.inv_keep : 0.f;
+            if constexpr (DM != 0) {  // P_drop's 1/(1-p) goes onto dV at the end
+              const bool keep = DM == 1 ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
+              pdr = keep ? pv : 0.f;
               dpd = keep ? dpd * p.inv_keep : 0.f;
             }
             pdv[u][r] = pdr;
@@ -871,7 +873,7 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
       for (int dt = 0; dt < 4; ++dt) {
         vq[dt][r] = dq[dt][r] * p.scale;
         vk[dt][r] = dk[dt][r] * p.scale;
-        vv[dt][r] = dv[dt][r];
+        vv[dt][r] = DM != 0 ? dv[dt][r] * p.inv_keep : dv[dt][r];
       }
     if (rope) {  // dQ and dK rows are the same 16: one table read for both
       float tc[4][4], ts[4][4];
@@ -1250,7 +1252,10 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
   if (use_fused_bwd(a)) {
     NSTL_CHECK_ARG(!(a->rope_q || a->rope_k) || ((((uintptr_t)a->rope_cos) | ((uintptr_t)a->rope_sin)) & 15) == 0,
                    "nstl_attn_bwd: RoPE tables must be 16-byte aligned");
-    return launch(attn_bwd_fused_kernel, dim3(1, a->B * a->H), FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
+    const dim3 grid(1, a->B * a->H);
+    if (!p.thresh) return launch(attn_bwd_fused_kernel<0>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
+    if (p.mask) return launch(attn_bwd_fused_kernel<1>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
+    return launch(attn_bwd_fused_kernel<2>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
   }
   dim3 grid((a->T + BWD_ROWS - 1) / BWD_ROWS, a->B * a->H);
   const size_t lds = bwd_lds_bytes(a->T, esz);
