@@ -414,6 +414,42 @@ def test_attention_bias_partials(dt, T):
     assert K.attn_bias_rows(a) == 0
 
 
+def test_dropout_hash_statistics():
+    """The counter hash behind every dropout mask (common.h nstl_pair_hash), read
+    back through the attention forward's stored keep bits (1M elements, p=0.3):
+    keep rate 1-p, and independent decisions for the two halves of one hash
+    (keys k, k+1), neighbouring hashes (k, k+2), neighbouring queries and
+    different heads."""
+    B, H, T, dh, p = 4, 16, 128, 64, 0.3
+    M, D = B * T, H * dh
+    qkv = rnd(M, 3 * D, dtype=torch.bfloat16, scale=0.5, seed=90)
+    o = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B * H * T, dtype=torch.float32, device=DEV)
+    mask = torch.zeros(B * H * T * T // 64, dtype=torch.int64, device=DEV)
+    a = K.attn_args(K.BF16, B, T, H, qkv.data_ptr(), 3 * D, qkv[:, D:].data_ptr(), 3 * D,
+                    qkv[:, 2 * D:].data_ptr(), 3 * D, o.data_ptr(), D, lse.data_ptr(), p, 20240917, dh=dh)
+    a.mask_bits = mask.data_ptr()
+    K.attn_fwd(a)
+    torch.cuda.synchronize()
+    nt = T // 16
+    w = mask.cpu().numpy().view(np.uint64).reshape(B * H, nt, nt, 4)  # [bh][qt][kt][key % 4]
+    bits = ((w[..., None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(np.uint8)
+    # bit 16 * ((key % 16) / 4) + query % 16  ->  keep[bh][query][key]
+    keep = bits.reshape(B * H, nt, nt, 4, 4, 16).transpose(0, 1, 5, 2, 4, 3).reshape(B * H, T, T).astype(np.float64)
+    q = 1.0 - p
+    assert abs(keep.mean() - q) < 0.003, keep.mean()
+    pairs = {
+        "halves of one hash (k, k+1)": (keep[:, :, 0::2], keep[:, :, 1::2]),
+        "neighbouring hashes (k, k+2)": (keep[:, :, 0:-2:2], keep[:, :, 2::2]),
+        "neighbouring queries": (keep[:, :-1, :], keep[:, 1:, :]),
+    }
+    for what, (x, y) in pairs.items():
+        joint = (x * y).mean()
+        assert abs(joint - q * q) < 0.004, (what, joint)
+    agree = (keep[0::2] == keep[1::2]).mean()  # head 2i vs head 2i+1
+    assert abs(agree - (q * q + p * p)) < 0.006, agree
+
+
 @pytest.mark.parametrize("T", [32, 96, 128])
 def test_attention_bwd_fused_matches_split(T, monkeypatch):
     """The fused one-workgroup-per-(b, h) backward (bf16, T <= 128) against the split
