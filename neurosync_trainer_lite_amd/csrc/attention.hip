@@ -399,7 +399,8 @@ NSTL_DEV void wave_sum_out(const float* red, int nw, float* out, int lane) {
 constexpr int BWD_NT = 512, BWD_ROWS = 16 * BWD_NT / 64;  // 8 waves, 128 rows
 
 // (BWD_NT, 6): 6 waves per SIMD = 3 workgroups per CU (bf16: 78 VGPRs, no spill)
-template <typename T>
+// DM: dropout mode as in attn_bwd_fused_kernel (0 none, 1 stored bits, 2 re-hash)
+template <typename T, int DM>
 __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
   constexpr int ESZ = (int)sizeof(T);
@@ -461,9 +462,8 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
 
   const float c2 = p.scale * LOG2E;
   // stored keep bits of this wave's 16 queries: lane kt*4 + r holds word (kt, r)
-  const bool use_mask = p.thresh && p.mask;
   uint64_t mword = 0;
-  if (use_mask && lane < nkt * 4) mword = p.mask[mask_word(bh, nkt, q0 >> 4, 0, 0) + lane];
+  if (DM == 1 && lane < nkt * 4) mword = p.mask[mask_word(bh, nkt, q0 >> 4, 0, 0) + lane];
   f32x4 dq[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -484,10 +484,10 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
       mma16(dp, fb, fo[1]);
       // sc[r] / dp[r]: S^T / dP^T at (key 16kt + 4g + r, query q0 + c)
       bool keep[4] = {true, true, true, true};
-      if (use_mask) {
+      if constexpr (DM == 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) keep[r] = (readlane64(mword, kt * 4 + r) >> lane) & 1;
-      } else if (p.thresh) {
+      } else if constexpr (DM == 2) {
         const uint64_t idx = drop_idx(bh, T_, q0 + c, kt * 16 + 4 * g);
         nstl_keep2(p.seed, idx, p.thresh, keep[0], keep[1]);
         nstl_keep2(p.seed, idx + 2, p.thresh, keep[2], keep[3]);
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
       for (int r = 0; r < 4; ++r) {
         const float pv = fast_exp2(sc[r] * c2 - lq);
         float dpd = dp[r];
-        if (p.thresh) dpd = keep[r] ? dpd * p.inv_keep : 0.f;
+        if constexpr (DM != 0) dpd = keep[r] ? dpd * p.inv_keep : 0.f;
         dsv[u][r] = pv * (dpd - dqv);
       }
     }
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
   }
 }
 
-template <typename T>
+template <typename T, int DM>
 __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
   constexpr int ESZ = (int)sizeof(T);
@@ -579,9 +579,8 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
 
   const float c2 = p.scale * LOG2E;
   // stored keep bits for this wave's 16 keys: lane 4*qt + r holds word (qt, k0/16, r)
-  const bool use_mask = p.thresh && p.mask;
   uint64_t mword = 0;
-  if (use_mask && (lane >> 2) < nkt) mword = p.mask[mask_word(bh, nkt, lane >> 2, k0 >> 4, lane & 3)];
+  if (DM == 1 && (lane >> 2) < nkt) mword = p.mask[mask_word(bh, nkt, lane >> 2, k0 >> 4, lane & 3)];
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -603,15 +602,15 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
       // st[r] / dpt[r]: S / dP at (query 16qt + 4g + r, key k0 + c)
       // its keep bits: 4 consecutive bits of word (qt, k0/16, key % 4)
       uint32_t nib = 0;
-      if (use_mask) nib = (uint32_t)(shfl64(mword, 4 * qt + (lane & 3)) >> (16 * (c >> 2) + 4 * g));
+      if (DM == 1) nib = (uint32_t)(shfl64(mword, 4 * qt + (lane & 3)) >> (16 * (c >> 2) + 4 * g));
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = qt * 16 + 4 * g + r;
         const float pv = fast_exp2(st[r] * c2 - lse_s[q]);
         float pdr = pv, dpd = dpt[r];
-        if (p.thresh) {
-          const bool keep = use_mask ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
-          pdr = keep ? pv * p.inv_keep : 0.f;
+        if constexpr (DM != 0) {  // P_drop's 1/(1-p) goes onto dV at the end
+          const bool keep = DM == 1 ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
+          pdr = keep ? pv : 0.f;
           dpd = keep ? dpd * p.inv_keep : 0.f;
         }
         pdv[u][r] = pdr;
@@ -635,7 +634,7 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       vk[dt][r] = dk[dt][r] * p.scale;
-      vv[dt][r] = dv[dt][r];
+      vv[dt][r] = DM != 0 ? dv[dt][r] * p.inv_keep : dv[dt][r];
     }
   if (p.rope_k) rope_back_tile(vk, k0 + 4 * g, c, p.rope_cos, p.rope_sin);
   char* scr = scratch + w * 16 * RBK;
@@ -1204,6 +1203,14 @@ int launch(K kern, dim3 grid, size_t lds, hipStream_t st, const AttnParams& p, c
   return 0;
 }
 
+// the split backward: dQ (also writes D = rowsum(dO * O)), then dK / dV
+template <typename T, int DM>
+int launch_split(dim3 grid, size_t lds, hipStream_t st, const AttnParams& p) {
+  int rc = launch(attn_bwd_dq_kernel<T, DM>, grid, lds, st, p, "nstl_attn_bwd dq", BWD_NT);
+  if (rc) return rc;
+  return launch(attn_bwd_dkv_kernel<T, DM>, grid, lds, st, p, "nstl_attn_bwd dkv", BWD_NT);
+}
+
 }  // namespace
 
 extern "C" int nstl_attn_fwd(const nstl_attn_args* a, void* stream) {
@@ -1259,12 +1266,15 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
   }
   dim3 grid((a->T + BWD_ROWS - 1) / BWD_ROWS, a->B * a->H);
   const size_t lds = bwd_lds_bytes(a->T, esz);
+  const int dm = !p.thresh ? 0 : (p.mask ? 1 : 2);
   if (a->dtype == NSTL_BF16) {
-    if ((rc = launch(attn_bwd_dq_kernel<bf16>, grid, lds, st, p, "nstl_attn_bwd dq", BWD_NT))) return rc;
-    return launch(attn_bwd_dkv_kernel<bf16>, grid, lds, st, p, "nstl_attn_bwd dkv", BWD_NT);
+    if (dm == 0) return launch_split<bf16, 0>(grid, lds, st, p);
+    if (dm == 1) return launch_split<bf16, 1>(grid, lds, st, p);
+    return launch_split<bf16, 2>(grid, lds, st, p);
   }
-  if ((rc = launch(attn_bwd_dq_kernel<float>, grid, lds, st, p, "nstl_attn_bwd dq", BWD_NT))) return rc;
-  return launch(attn_bwd_dkv_kernel<float>, grid, lds, st, p, "nstl_attn_bwd dkv", BWD_NT);
+  if (dm == 0) return launch_split<float, 0>(grid, lds, st, p);
+  if (dm == 1) return launch_split<float, 1>(grid, lds, st, p);
+  return launch_split<float, 2>(grid, lds, st, p);
 }
 
 extern "C" int nstl_attn_bias_rows(const nstl_attn_args* a) {

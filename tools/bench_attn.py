@@ -10,7 +10,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from neurosync_trainer_lite_amd import _hip as K  # noqa: E402
 from neurosync_trainer_lite_amd.engine import rotation_tables  # noqa: E402
 
-B, T, H, DH = 128, 128, 16, 64
+T = int(os.environ.get("NSTL_BENCH_T", "128"))     # 256: BASELINE C5's long clips (B halved)
+B, H, DH = 128 * 128 // T, 16, 64
 D, M = H * DH, B * T
 dev = "cuda:0"
 bf = torch.bfloat16
