@@ -121,6 +121,9 @@ class _Buffers:
             self.dqkv = e(M, 3 * D)
             self.dq = e(M, D)
             self.dkv = e(M, 2 * D)
+            # cross-attention k|v gradients of every decoder layer side by side: the
+            # memory gradient is then ONE GEMM over K = L * 2D (Engine.dmem_concat)
+            self.dkv_all = e(M, nl * 2 * D)
             self.dh = e(M, Fd)
             self.demb = e(M, D)
             self.dpred = torch.zeros(M, 64, dtype=dt, device=dev)
@@ -198,6 +201,10 @@ class Seq2SeqEngine:
         # instead of being written in the compute dtype and added by the next LN backward
         self.res_handoff_on = os.environ.get("NSTL_RES_HANDOFF", "1") != "0"
         self._dadd_pending = False
+        # NSTL_DMEM_CONCAT=0: the memory gradient accumulated into the f32 dmem by one
+        # K = 2D GEMM per decoder layer instead of one K = L * 2D GEMM after the decoder
+        self.dmem_concat = os.environ.get("NSTL_DMEM_CONCAT", "1") != "0"
+        self._wkv = None           # [W_kv_0; ...; W_kv_{L-1}] slab (_kv_weights)
         # NSTL_RELU_MASK=0: the FFN2 dX epilogue reads the saved hidden h for its
         # dReLU instead of the 1-bit keep&positive mask the FFN1 epilogue writes
         self.relu_mask_on = os.environ.get("NSTL_RELU_MASK", "1") != "0"
@@ -349,6 +356,19 @@ class Seq2SeqEngine:
     def b(self, name, rows=1):
         o, k, _ = self.offsets[name]
         return self.p32[o:o + k * rows]
+
+    def _kv_weights(self):
+        """The decoder cross-attention k|v weights (compute dtype) stacked in one
+        contiguous [L * 2D, D] slab, the B operand of the concatenated memory-gradient
+        GEMM; refreshed every backward (the optimizer has moved the weights).  Runs
+        on the current stream, which backward() makes the engine's stream."""
+        D, L = self.D, self.L
+        if self._wkv is None:
+            self._wkv = torch.empty(L * 2 * D, D, dtype=self.dt, device=self.device)
+        for l in range(L):
+            self._wkv[2 * D * l:2 * D * (l + 1)].copy_(
+                self.w("decoder.transformer_decoder.%d.multihead_attn.k_linear.weight" % l, 2))
+        return self._wkv
 
     def gw(self, name, rows=1):
         o, k, shp = self.offsets[name]
@@ -859,6 +879,13 @@ class Seq2SeqEngine:
             self._dec_layer_bwd(bb, l, T, bf, first=(l == L - 1))
             self._red_flush()
             ready("decoder.transformer_decoder.%d.self_attn.v_linear.bias" % l)
+        if self.dmem_concat:
+            # dmem = sum_l dkv_l W_kv_l = [dkv_0 | ... | dkv_{L-1}] [W_kv_0; ...; W_kv_{L-1}]:
+            # one single-round GEMM with K = L * 2D (L accumulating K = 2D GEMMs each
+            # read and wrote the f32 dmem, 128 MB per launch at the 228M shape)
+            W = self._kv_weights()
+            K.gemm(bb.dkv_all, W, bb.dmem, M, D, W.shape[0], a_kmajor=True, b_kmajor=False, beta=0.0,
+                   stream=self.st)
         # decoder input x = GPE(mem): dmem += GPE^T(dres)
         cs, sn = self.rope(T, D)
         K.rope(dres, D, bb.dmem, D, M, D, cs, sn, T, D, inverse=True, accumulate=True, stream=self.st)
@@ -958,14 +985,16 @@ class Seq2SeqEngine:
         self._dw(dyx, bb.d_oc[l], m + "out_linear.weight", 1, bf, ws, bias=False)
         self._dx(dyx, m + "out_linear.weight", 1, bb.dattn, 0.0)
         kvc = bb.d_kvc[l]
+        dkv = bb.dkv_all[:, 2 * D * l:2 * D * (l + 1)] if self.dmem_concat else bb.dkv
         fused = self._attn_bwd(bb.d_qc[l], kvc[:, :D], kvc[:, D:], bb.d_oc[l], bb.d_lsec[l], bb.dattn,
-                               bb.dq, bb.dkv[:, :D], bb.dkv[:, D:], sd("xattn"), T, bb.B, mask=bb.d_maskc[l],
+                               bb.dq, dkv[:, :D], dkv[:, D:], sd("xattn"), T, bb.B, mask=bb.d_maskc[l],
                                bias=[(0, D, self.gb(m + "q_linear.bias")), (D, 2 * D, self.gb(m + "k_linear.bias", 2))],
                                bf=bf)
         self._dw(bb.dq, bb.d_x1[l], m + "q_linear.weight", 1, bf, ws, bias=not fused)
         self._dx_res(bb.dq, m + "q_linear.weight", 1)
-        self._dw(bb.dkv, bb.mem, m + "k_linear.weight", 2, bf, ws, bias=not fused)
-        self._dx(bb.dkv, m + "k_linear.weight", 2, bb.dmem, 0.0 if first else 1.0)
+        self._dw(dkv, bb.mem, m + "k_linear.weight", 2, bf, ws, bias=not fused)
+        if not self.dmem_concat:
+            self._dx(dkv, m + "k_linear.weight", 2, bb.dmem, 0.0 if first else 1.0)
         self._attn_block_bwd(bb, pre, x_in, bb.d_qkv[l], bb.d_o[l], bb.d_lse[l], st[0:2], bb.d_s1[l], "norm1",
                              (sd("resid"), sd("drop1"), sd("attn")), T, bf, bb.d_mask[l], last=(l == 0))
         if grouped:

@@ -225,6 +225,29 @@ def test_bf16_grouped_weight_gradients_match_split_k(monkeypatch):
     assert len(dec) > 0 and all(grads[0][k].abs().sum() > 0 for k in dec)
 
 
+def test_bf16_concatenated_memory_gradient_matches_per_layer(monkeypatch):
+    """The memory gradient as one GEMM over all decoder layers' k|v gradients
+    (NSTL_DMEM_CONCAT=1) equals the per-layer accumulation up to f32 summation order
+    (carried through the bf16 encoder backward)."""
+    grads = []
+    for cat in ("1", "0"):
+        monkeypatch.setenv("NSTL_DMEM_CONCAT", cat)
+        cfg, model, crit, opt, params = make(256, 4, 3, 11, amp=True, dropout=0.1)
+        torch.manual_seed(5)
+        g = torch.Generator().manual_seed(6)
+        src = torch.randn(4, 128, 256, generator=g).to(DEV)
+        trg = (torch.randn(4, 128, 61, generator=g) * 20).to(DEV)
+        model.train()
+        opt.zero_grad()
+        crit(model(src), trg).backward()
+        torch.cuda.synchronize()
+        grads.append({k: p.grad.detach().double().cpu().clone() for k, p in model.named_parameters()})
+    worst = max(rel(grads[0][k], grads[1][k]) for k in grads[0])
+    assert worst < 2e-3, worst
+    enc = [k for k in grads[0] if k.startswith("encoder.") and k.endswith("weight")]
+    assert len(enc) > 0 and all(grads[0][k].abs().sum() > 0 for k in enc)
+
+
 def test_bf16_batched_reductions_match_per_call(monkeypatch):
     """LayerNorm and bias-gradient partials reduced in one batched launch per backward
     layer (default) equal the per-call reductions: LayerNorm gamma/beta bit-exact
