@@ -271,6 +271,29 @@ int nstl_features_frames(int64_t n_samples, int sr);
 const char* nstl_last_error_string(void);
 int nstl_version(void);
 
+/* Launch counters by kernel family, process-wide (host side, counted at each
+ * launch): lets a test assert which kernels a call path took, e.g. that a
+ * production-shape step ran the 256x256 ring GEMM and the fused attention
+ * backward.  No reference counterpart (verification aid). */
+enum {
+  NSTL_K_GEMM128 = 0,        /* 128x128 GEMM launches (small / f32 problems) */
+  NSTL_K_GEMM_RING,          /* 256x256 LDS-DMA ring GEMM launches */
+  NSTL_K_GEMM_RING_TILES,    /*   ... their 256x256 output tiles */
+  NSTL_K_GEMM_GROUP,         /* grouped ring GEMM launches (weight gradients) */
+  NSTL_K_GEMM_GROUP_TILES,   /*   ... their tiles */
+  NSTL_K_GEMM_SPLITK_REDUCE, /* split-K combine launches */
+  NSTL_K_GEMM_FP8,           /* fp8 ring GEMM launches */
+  NSTL_K_ATTN_FWD,           /* MFMA attention forward */
+  NSTL_K_ATTN_FWD_GENERIC,
+  NSTL_K_ATTN_BWD_FUSED,     /* one-kernel attention backward */
+  NSTL_K_ATTN_BWD_SPLIT,     /* dQ + dK/dV kernel pairs */
+  NSTL_K_ATTN_BWD_GENERIC,
+  NSTL_K_COUNT
+};
+/* Copies min(n, NSTL_K_COUNT) counters to out; returns NSTL_K_COUNT. */
+int nstl_kernel_counts(int64_t* out, int n);
+void nstl_kernel_counts_reset(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -109,8 +109,13 @@ EXPORTS = [
     "nstl_colsum", "nstl_rope",
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
     "nstl_features", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
-    "nstl_version", "nstl_fp8_quant_rows",
+    "nstl_version", "nstl_fp8_quant_rows", "nstl_kernel_counts", "nstl_kernel_counts_reset",
 ]
+
+# nstl_kernel_counts order (NSTL_K_* in include/nstl.h)
+KERNEL_COUNT_NAMES = ["gemm128", "gemm_ring", "gemm_ring_tiles", "gemm_group", "gemm_group_tiles",
+                      "gemm_splitk_reduce", "gemm_fp8", "attn_fwd", "attn_fwd_generic", "attn_bwd_fused",
+                      "attn_bwd_split", "attn_bwd_generic"]
 
 _lib = None
 
@@ -159,6 +164,9 @@ def lib():
         L.nstl_features_frames.restype = _i32
         L.nstl_last_error_string.restype = ctypes.c_char_p
         L.nstl_version.restype = _i32
+        L.nstl_kernel_counts.argtypes = [_vp, _i32]
+        L.nstl_kernel_counts.restype = _i32
+        L.nstl_kernel_counts_reset.restype = None
         _lib = L
     return _lib
 
@@ -167,6 +175,20 @@ def check(rc, what):
     if rc != 0:
         msg = lib().nstl_last_error_string().decode(errors="replace")
         raise RuntimeError("%s failed (code %d): %s" % (what, rc, msg))
+
+
+def kernel_counts():
+    """{family: launches} since the last kernel_counts_reset() (nstl_kernel_counts)."""
+    n = len(KERNEL_COUNT_NAMES)
+    buf = (ctypes.c_int64 * n)()
+    total = lib().nstl_kernel_counts(ctypes.cast(buf, _vp), n)
+    if total != n:
+        raise RuntimeError("nstl_kernel_counts: library has %d counters, bindings %d" % (total, n))
+    return dict(zip(KERNEL_COUNT_NAMES, buf))
+
+
+def kernel_counts_reset():
+    lib().nstl_kernel_counts_reset()
 
 
 def ptr(t):

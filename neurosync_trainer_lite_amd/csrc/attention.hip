@@ -1206,6 +1206,7 @@ int launch(K kern, dim3 grid, size_t lds, hipStream_t st, const AttnParams& p, c
 // the split backward: dQ (also writes D = rowsum(dO * O)), then dK / dV
 template <typename T, int DM>
 int launch_split(dim3 grid, size_t lds, hipStream_t st, const AttnParams& p) {
+  nstl::count(NSTL_K_ATTN_BWD_SPLIT);
   int rc = launch(attn_bwd_dq_kernel<T, DM>, grid, lds, st, p, "nstl_attn_bwd dq", BWD_NT);
   if (rc) return rc;
   return launch(attn_bwd_dkv_kernel<T, DM>, grid, lds, st, p, "nstl_attn_bwd dkv", BWD_NT);
@@ -1220,11 +1221,13 @@ extern "C" int nstl_attn_fwd(const nstl_attn_args* a, void* stream) {
   const int esz = a->dtype == NSTL_F32 ? 4 : 2;
   hipStream_t st = (hipStream_t)stream;
   if (!use_fast(a)) {
+    nstl::count(NSTL_K_ATTN_FWD_GENERIC);
     dim3 grid((a->T + 3) / 4, a->B * a->H);
     const size_t lds = 4 * (size_t)(a->dh + a->T) * 4;
     if (a->dtype == NSTL_BF16) return launch(attn_fwd_generic<bf16>, grid, lds, st, p, "nstl_attn_fwd generic");
     return launch(attn_fwd_generic<float>, grid, lds, st, p, "nstl_attn_fwd generic");
   }
+  nstl::count(NSTL_K_ATTN_FWD);
   dim3 grid((a->T + FWD_QB - 1) / FWD_QB, a->B * a->H);
   const size_t lds = fwd_lds_bytes(a->T, esz);
   // T % 32 == 0 and T <= 256 on this path: NKT in {2, 4, ..., 16}
@@ -1247,6 +1250,7 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
   const int esz = a->dtype == NSTL_F32 ? 4 : 2;
   hipStream_t st = (hipStream_t)stream;
   if (!use_fast(a)) {
+    nstl::count(NSTL_K_ATTN_BWD_GENERIC);
     dim3 grid((a->T + 3) / 4, a->B * a->H);
     const size_t lq = 4 * (size_t)(2 * a->dh + a->T) * 4, lkv = 4 * (size_t)(2 * a->dh + 2 * a->T) * 4;
     if (a->dtype == NSTL_BF16) {
@@ -1260,6 +1264,7 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
     NSTL_CHECK_ARG(!(a->rope_q || a->rope_k) || ((((uintptr_t)a->rope_cos) | ((uintptr_t)a->rope_sin)) & 15) == 0,
                    "nstl_attn_bwd: RoPE tables must be 16-byte aligned");
     const dim3 grid(1, a->B * a->H);
+    nstl::count(NSTL_K_ATTN_BWD_FUSED);
     if (!p.thresh) return launch(attn_bwd_fused_kernel<0>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
     if (p.mask) return launch(attn_bwd_fused_kernel<1>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
     return launch(attn_bwd_fused_kernel<2>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);

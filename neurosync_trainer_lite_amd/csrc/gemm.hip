@@ -1167,6 +1167,8 @@ int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t s
     else if (!a->a_kmajor && !a->b_kmajor) launch_ring_em<false, false>(em, grid, block, st, p);
     else launch_ring_em<false, true>(em, grid, block, st, p);
     NSTL_LAUNCH_CHECK("nstl_gemm (256 ring)");
+    nstl::count(NSTL_K_GEMM_RING);
+    nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt * splits);
     return 0;
   }
   if (a->a_kmajor && a->b_kmajor)
@@ -1194,6 +1196,7 @@ int launch_typed(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t
   else
     hipLaunchKernelGGL((gemm_kernel<T, false, true>), grid, block, 0, st, p);
   NSTL_LAUNCH_CHECK("nstl_gemm");
+  nstl::count(NSTL_K_GEMM128);
   return 0;
 }
 
@@ -1295,6 +1298,7 @@ int gemm_f8(const nstl_gemm_args* a, GemmParams& p, hipStream_t st) {
     default: hipLaunchKernelGGL((gemm256f8_kernel<EM_F32>), grid, block, 0, st, p); break;
   }
   NSTL_LAUNCH_CHECK("nstl_gemm (FP8)");
+  nstl::count(NSTL_K_GEMM_FP8);
   return 0;
 }
 
@@ -1347,6 +1351,7 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
     hipLaunchKernelGGL(splitk_reduce, dim3(blocks), dim3(256), 0, st, p.ws, splits, a->M, a->N, p.C, a->ldc,
                        p.c_f32, a->beta, a->epilogue == NSTL_EPI_BIAS ? a->bias : nullptr);
     NSTL_LAUNCH_CHECK("nstl_gemm splitk_reduce");
+    nstl::count(NSTL_K_GEMM_SPLITK_REDUCE);
   }
   return 0;
 }
@@ -1384,6 +1389,8 @@ extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream
   else { NSTL_GROUP_LAUNCH(false, true) }
 #undef NSTL_GROUP_LAUNCH
   NSTL_LAUNCH_CHECK("nstl_gemm_grouped");
+  nstl::count(NSTL_K_GEMM_GROUP);
+  nstl::count(NSTL_K_GEMM_GROUP_TILES, tiles);
   return 0;
 }
 

@@ -8,6 +8,7 @@
 namespace nstl {
 void set_error(const std::string& msg);
 int fail(int code, const char* fmt, ...);
+void count(int which, long long n = 1);  // nstl_kernel_counts (NSTL_K_*)
 }  // namespace nstl
 
 #define NSTL_CHECK_ARG(cond, ...)                                         \

@@ -13,7 +13,6 @@ import numpy as np
 import pandas as pd
 
 from ..utils.audio.extraction.extract_features import extract_audio_features
-from ..utils.video.mov_extraction import find_files, get_audio
 
 COLUMNS_TO_DROP = ['Timecode', 'BlendshapeCount']
 _NOISE_COLUMNS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60]
@@ -37,21 +36,39 @@ def scale_facial_data(facial_data, scale_factor=1.1):
     return np.clip(np.asarray(facial_data, dtype=np.float64) * scale_factor, -1, 1)
 
 
+_CLIP_SUFFIXES = {'.mov': 'mov', '.mp4': 'mp4', '.wav': 'wav'}
+
+
+def clip_files(folder_path):
+    """What process_folder reads from one clip folder: {'mov', 'mp4', 'wav',
+    'facial'} -> path, plus the feature-cache path.  The facial CSV is a *.csv
+    whose name contains 'iPhone_cal' (the naming rule of the reference's
+    find_files, utils/video/mov_extraction.py:23); where several files of one
+    kind exist, the last in os.listdir order is taken, as there."""
+    found = {}
+    for name in os.listdir(folder_path):
+        ext = os.path.splitext(name)[1]
+        kind = 'facial' if (ext == '.csv' and 'iPhone_cal' in name) else _CLIP_SUFFIXES.get(ext)
+        if kind is not None:
+            found[kind] = os.path.join(folder_path, name)
+    return found, os.path.join(folder_path, 'audio_features.csv')
+
+
 def process_folder(folder_path, sr, apply_smoothing=False, apply_over_scale=False):
-    """data_processing.py:44-78."""
-    mov_path, mp4_path, wav_path, facial_csv_path, audio_features_csv_path, _ = find_files(folder_path)
-    video_path = mov_path or mp4_path
-    if facial_csv_path and (video_path or wav_path or os.path.exists(audio_features_csv_path)):
-        audio_path = get_audio(video_path, wav_path, folder_path) if (video_path or wav_path) else None
-        if audio_path or os.path.exists(audio_features_csv_path):
-            audio_features, facial_data = collect_features(audio_path if audio_path else _, audio_features_csv_path,
-                                                           facial_csv_path, sr)
-            if apply_over_scale:
-                facial_data = scale_facial_data(facial_data)
-            facial_data[:, :61] *= 100
-            if apply_smoothing:
-                facial_data = smooth_facial_data(facial_data)
-            return audio_features, facial_data
+    """data_processing.py:44-78.  A video clip (mov preferred over mp4, as the
+    reference's ``mov_path or mp4_path``) is decoded by ffmpeg inside
+    load_audio rather than first written to an audio.wav beside it."""
+    found, audio_features_csv_path = clip_files(folder_path)
+    facial_csv_path = found.get('facial')
+    audio_path = found.get('mov') or found.get('mp4') or found.get('wav')
+    if facial_csv_path and (audio_path or os.path.exists(audio_features_csv_path)):
+        audio_features, facial_data = collect_features(audio_path, audio_features_csv_path, facial_csv_path, sr)
+        if apply_over_scale:
+            facial_data = scale_facial_data(facial_data)
+        facial_data[:, :61] *= 100
+        if apply_smoothing:
+            facial_data = smooth_facial_data(facial_data)
+        return audio_features, facial_data
     return None, None
 
 

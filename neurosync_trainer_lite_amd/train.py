@@ -10,10 +10,12 @@ GPU, RCCL over xGMI) instead of the reference's single-process replicas
 same batch order from one broadcast seed, trains on batches r, r+n, ...;
 rank 0 alone writes checkpoints, plots and the validation clip.
 """
+import json
 import os
 import socket
 import subprocess
 import sys
+import tempfile
 import threading
 
 import torch
@@ -94,10 +96,30 @@ def _free_port():
     return port
 
 
-def _relaunch(n):
+CONFIG_ENV = "NSTL_TRAIN_CONFIG"
+
+
+def _relaunch(n, config):
+    """torchrun this module on n GPUs with ``config`` handed over as a JSON file
+    (its path in $NSTL_TRAIN_CONFIG), so the children train the caller's config
+    rather than the module default."""
+    with tempfile.NamedTemporaryFile("w", suffix=".json", prefix="nstl_config_", delete=False) as f:
+        json.dump(config, f)
+        path = f.name
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "neurosync_trainer_lite_amd.train"]
-    return subprocess.call(cmd)
+    try:
+        return subprocess.call(cmd, env=dict(os.environ, **{CONFIG_ENV: path}))
+    finally:
+        os.unlink(path)
+
+
+def _config_from_env():
+    path = os.environ.get(CONFIG_ENV)
+    if not path:
+        return None
+    with open(path) as f:
+        return json.load(f)
 
 
 def _common_seed(rank, world, device):
@@ -113,7 +135,7 @@ def main(config=None):
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     n_dev = torch.cuda.device_count()
     if world_env == 1 and config.get('use_multi_gpu', False) and n_dev > 1 and config.get('num_gpus', 1) > 1:
-        return _relaunch(min(n_dev, config['num_gpus']))
+        return _relaunch(min(n_dev, config['num_gpus']), config)
     if n_dev == 0:
         raise RuntimeError("the MI355X training path needs a GPU (there is no CPU path)")
     rank, world, local = parallel.init_from_env()
@@ -143,4 +165,4 @@ def main(config=None):
 
 
 if __name__ == "__main__":
-    main()
+    main(_config_from_env())

@@ -8,11 +8,14 @@ rates are resampled with a windowed-sinc polyphase filter
 (``scipy.signal.resample_poly``).  That resampler is not soxr: for 88.2 kHz input
 (the reference's own capture rate, and every benchmark input) there is no
 resampling and the samples are identical; for other rates parity is unpinned
-(DESIGN.md).  Other containers (mov/mp4) go through ffmpeg, as in the reference
-(utils/video/mov_extraction.py).
+(DESIGN.md).  Other containers (mov/mp4) are decoded by ffmpeg straight to
+mono f32 PCM at 88.2 kHz on a pipe (the reference first writes an audio.wav
+with ffmpeg, utils/video/mov_extraction.py:39-62).
 """
 import io
+import os
 import struct
+import subprocess
 from math import gcd
 
 import numpy as np
@@ -76,10 +79,23 @@ def peak_normalise(y):
     return y / m if m > 0 else y
 
 
+def _decode_container(path, sr):
+    """Any container ffmpeg reads -> mono f32 at ``sr`` (ffmpeg resamples)."""
+    from ...config import training_config
+    sr = sr or TARGET_SR
+    cmd = [training_config['ffmpeg_path'], '-v', 'error', '-i', path, '-vn', '-ac', '1', '-ar', str(sr),
+           '-f', 'f32le', '-']
+    pcm = subprocess.run(cmd, check=True, stdout=subprocess.PIPE).stdout
+    return np.frombuffer(pcm, '<f4').astype(np.float32), sr
+
+
 def load_audio(audio_path, sr=TARGET_SR):
     """load_audio.py:18-21: decode, mono, resample to ``sr``."""
-    with open(audio_path, "rb") as f:
-        y, file_sr = _parse_wav(f.read())
+    if os.path.splitext(audio_path)[1].lower() in ('.mov', '.mp4'):
+        y, file_sr = _decode_container(audio_path, sr)
+    else:
+        with open(audio_path, "rb") as f:
+            y, file_sr = _parse_wav(f.read())
     if sr is not None:
         y, file_sr = resample(y, file_sr, sr), sr
     print(f"Loaded audio file '{audio_path}' with sample rate {file_sr}")

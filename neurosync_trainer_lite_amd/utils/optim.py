@@ -114,7 +114,6 @@ class FusedAdam(torch.optim.Optimizer):
         if max_norm is not None:
             a.sumsq_partial, a.n_partial, a.max_norm = self.partial.data_ptr(), N_PARTIAL, float(max_norm)
             a.norm_out = self.norm.data_ptr()
-            self.last_norm = self.norm
 
         def adam_fn(lo, n, grads, partial):
             a.p, a.g, a.m, a.v = (eng.p32[lo:].data_ptr(), grads.data_ptr(), self.m[lo:].data_ptr(),
@@ -131,6 +130,7 @@ class FusedAdam(torch.optim.Optimizer):
         if self._comm is None:
             sumsq_fn(eng.g32, self.partial)
             adam_fn(0, eng.numel, eng.g32, self.partial)
+            self._snapshot_norm(max_norm)
             return loss
         from .. import parallel
         if max_norm is None:
@@ -139,7 +139,15 @@ class FusedAdam(torch.optim.Optimizer):
                             [eng.p16] if eng.p16 is not eng.p32 else [eng.p32], tail=(eng.n_shardable, eng.numel))
         eng.master_stale = eng.p16 is not eng.p32
         self._moments_stale = True
+        self._snapshot_norm(max_norm)
         return loss
+
+    def _snapshot_norm(self, max_norm):
+        # self.norm is one device word every step overwrites; callers that read a
+        # step's norm later (training_utils._Pending reads step n after step n+1
+        # is queued) need their own copy, queued on the same stream.
+        if max_norm is not None:
+            self.last_norm = self.norm.clone()
 
     def zero_grad(self, set_to_none=True):
         """The next backward overwrites the gradient arena (no memset; p.grad stays

@@ -4,7 +4,9 @@ on the GPU, batched chunk inference, CSV + plot + comparison statistics).
 The reference writes the CSV and the plot from child processes
 (multiprocessing.Process under ``lock``); here they are written in-process,
 under the same lock, because forking a process that holds a GPU context is
-not safe on ROCm."""
+not safe on ROCm.  The JawOpen comparison plot (utils/csv/plot_comparison.py)
+is cosmetic and out of scope; the statistics it sits
+beside are written."""
 import os
 
 import numpy as np
@@ -13,7 +15,6 @@ import pandas as pd
 from ..config import training_config
 from .audio.extraction.extract_features import extract_audio_features
 from .audio.processing.audio_processing import process_audio_features
-from .csv.plot_comparison import plot_comparison
 from .csv.save_csv import BLENDSHAPE_COLUMNS, save_generated_data_as_csv
 
 DIMENSION_LABELS = BLENDSHAPE_COLUMNS
@@ -29,9 +30,6 @@ def generate_and_save_facial_data(epoch, audio_path, model, ground_truth_path, l
     output_csv_path = os.path.join(base_dir, f"generated_facial_data_epoch_{epoch + 1}.csv")
     with lock:
         save_generated_data_as_csv(generated_facial_data, output_csv_path)
-    output_image_path = os.path.join(base_dir, f"comparison_plot_epoch_{epoch + 1}.jpg")
-    with lock:
-        plot_comparison(ground_truth_path, output_csv_path, output_image_path)
     output_stats_path = os.path.join(stats_dir, f"comparison_stats_epoch_{epoch + 1}.txt")
     return save_comparison_stats(output_csv_path, ground_truth_path, output_stats_path)
 

@@ -23,7 +23,8 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 
 from oracle import model_ref  # noqa: E402  (seeded parameter sets, shared with tests)
-from tests.golden.make_goldens_helpers import summary, synth_audio, full_layer_params  # noqa: E402
+from tests.golden.make_goldens_helpers import (summary, synth_audio, full_layer_params, FakeSeq2Seq,  # noqa: E402
+                                              INFER_FRAMES, INFER_MODEL)
 
 
 def _install_librosa_stub():
@@ -258,6 +259,64 @@ def gen_lr():
     save("lr.npz", **vals)
 
 
+def gen_inference():
+    """audio_processing.process_audio_features (the per-epoch validation
+    inference) run by the reference: chunking/blend cases on an
+    elementwise stand-in model, and one seeded small Seq2Seq of the reference
+    (weights regenerated from the seed in the tests)."""
+    from utils.audio.processing import audio_processing as ap
+    out = {}
+    cfg = {"frame_size": 128, "overlap": 16}
+    for n in INFER_FRAMES:
+        feats = np.random.default_rng(n).standard_normal((n, 256))
+        out["feats_sum_%d" % n] = feats.sum()   # inputs are regenerated from the seed
+        out["fake_%d" % n] = ap.process_audio_features(feats, FakeSeq2Seq(), "cpu", cfg)
+    mc = INFER_MODEL
+    _, m, _ = _ref_model(mc["D"], mc["H"], mc["L"], mc["seed"])
+    feats = np.random.default_rng(mc["seed"]).standard_normal((mc["frames"], 256)).astype(np.float32)
+    out["model_feats_sum"] = feats.astype(np.float64).sum()
+    out["model_out"] = ap.process_audio_features(feats, m, "cpu", dict(cfg, overlap=16))
+    save("inference.npz", **out)
+
+
+def gen_formats():
+    """Byte images of the files the reference writes on this path (SURVEY
+    8(f)2): the LiveLink CSV (utils/csv/save_csv.py:4-62) and the
+    audio_features.csv feature cache (dataset/data_processing.py:112-120)."""
+    from utils.csv.save_csv import save_generated_data_as_csv
+    out = {}
+    rng = np.random.default_rng(41)
+    cases = {"f32_61": (rng.random((130, 61)).astype(np.float32), False),
+             "f64_68_emotions": (rng.standard_normal((70, 68)), True),
+             "f64_68_base": (rng.standard_normal((20, 68)), False),
+             "zeros_long": (np.zeros((3700, 61)), False)}   # timecodes past one minute
+    with tempfile.TemporaryDirectory() as td:
+        for tag, (arr, emo) in cases.items():
+            path = os.path.join(td, tag + ".csv")
+            save_generated_data_as_csv(arr, path, include_emotion_dimensions=emo)
+            out["csv_in_" + tag] = arr
+            out["csv_emo_" + tag] = np.array(emo)
+            out["csv_bytes_" + tag] = np.frombuffer(open(path, "rb").read(), np.uint8)
+        feats = rng.standard_normal((90, 256))
+        facial = rng.standard_normal((90, 61))
+        cols = ["Timecode", "BlendshapeCount"] + ["c%d" % i for i in range(61)]
+        import pandas as pd
+        fpath = os.path.join(td, "x_iPhone_cal.csv")
+        pd.DataFrame(np.hstack([np.zeros((90, 1)), np.full((90, 1), 61), facial]), columns=cols).to_csv(
+            fpath, index=False)
+        cache = os.path.join(td, "audio_features.csv")
+        saved = dp.extract_audio_features
+        dp.extract_audio_features = lambda path, sr: (feats, None)
+        try:
+            dp.collect_features("clip.wav", cache, fpath, 88200, include_fast=False)
+        finally:
+            dp.extract_audio_features = saved
+        out["cache_feats"] = feats
+        out["cache_facial"] = facial
+        out["cache_bytes"] = np.frombuffer(open(cache, "rb").read(), np.uint8)
+    save("formats.npz", **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     gen_loss()
@@ -269,3 +328,5 @@ if __name__ == "__main__":
     gen_windows()
     gen_augment()
     gen_lr()
+    gen_inference()
+    gen_formats()

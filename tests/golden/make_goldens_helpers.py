@@ -34,3 +34,26 @@ def full_layer_params():
     d = {"d." + k[len("decoder.transformer_decoder.0."):]: v for k, v in shapes.items()
          if k.startswith("decoder.transformer_decoder.0.")}
     return model_ref.seeded_params(e, 8), model_ref.seeded_params(d, 9)
+
+
+class FakeSeq2Seq:
+    """A deterministic per-frame stand-in with the reference model's
+    ``encoder``/``decoder`` split (what audio_processing.decode_audio_chunk calls),
+    elementwise only so batching chunks cannot change a bit.  The position term
+    makes every chunk boundary visible in the output."""
+
+    def eval(self):
+        return self
+
+    def encoder(self, x):
+        import torch
+        return torch.tanh(x)
+
+    def decoder(self, m):
+        import torch
+        pos = torch.arange(m.shape[1], dtype=m.dtype)[None, :, None]
+        return m[..., :61] * 30.0 + m[..., 61:122] * 7.0 + pos * 0.25
+
+
+INFER_FRAMES = (37, 128, 129, 250, 1000)   # chunking cases (short, exact, +1, ragged, long)
+INFER_MODEL = dict(D=128, H=2, L=1, seed=31, frames=300)

@@ -42,3 +42,11 @@ def test_features_sizes_without_device():
     # 1 s at 88.2 kHz: F120 = 1 + 88200 // 735 = 121 -> F60 = 61
     assert _hip.features_frames(88200, 88200) == 61
     assert _hip.features_workspace_bytes(88200, 88200) > 121 * 1472 * 4 * 2
+
+
+def test_kernel_counters_without_device():
+    """The launch counters exist, reset, and match the bindings' family list."""
+    from neurosync_trainer_lite_amd import _hip
+    _hip.kernel_counts_reset()
+    c = _hip.kernel_counts()
+    assert set(c) == set(_hip.KERNEL_COUNT_NAMES) and not any(c.values())

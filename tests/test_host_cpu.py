@@ -13,6 +13,7 @@ from neurosync_trainer_lite_amd.utils.audio import load_audio as la
 from neurosync_trainer_lite_amd.utils.audio.processing import audio_processing as ap
 from neurosync_trainer_lite_amd.utils.csv.save_csv import save_generated_data_as_csv, timecode
 from oracle import data_ref
+from tests.golden.make_goldens_helpers import FakeSeq2Seq, INFER_FRAMES
 
 
 def _dataset(window=128):
@@ -99,64 +100,56 @@ def test_wav_roundtrip(tmp_path):
     assert np.abs(zb).max() == pytest.approx(1.0)
 
 
-def _reference_process(audio_features, decode, frame_length, overlap):
-    """audio_processing.py:50-112 as written (sequential per-chunk decode)."""
-    num_features, num_frames = audio_features.shape[1], audio_features.shape[0]
-    outs, start = [], 0
-    while start < num_frames:
-        end = min(start + frame_length, num_frames)
-        chunk = ap.pad_audio_chunk(audio_features[start:end], frame_length, num_features)
-        dec = decode(chunk)[:end - start]
-        if outs:
-            last = outs.pop()
-            ov = min(overlap, len(last), len(dec))
-            if ov == 0:
-                outs.append(np.vstack((last, dec)))
-            else:
-                b = np.copy(last)
-                for i in range(ov):
-                    alpha = i / ov
-                    b[-ov + i] = (1 - alpha) * last[-ov + i] + alpha * dec[i]
-                outs.append(np.vstack((b, dec[ov:])))
-        else:
-            outs.append(dec)
-        start += frame_length - overlap
-    cur = sum(len(c) for c in outs)
-    if cur < num_frames:
-        rem = num_frames - cur
-        outs.append(decode(ap.pad_audio_chunk(audio_features[num_frames - rem:], frame_length, num_features))[:rem])
-    final = np.concatenate(outs, axis=0)[:num_frames]
-    final[:, :61] /= 100
-    return final
-
-
-class _FakeSeq2Seq(torch.nn.Module):
-    """Deterministic per-frame stand-in with the reference's encoder/decoder split."""
-
-    def __init__(self):
-        super().__init__()
-        g = torch.Generator().manual_seed(0)
-        self.w = torch.randn(256, 61, generator=g)
-        self.encoder = lambda x: torch.tanh(x)
-        self.decoder = lambda m: (m @ self.w) * 30.0 + torch.arange(m.shape[1], dtype=torch.float32)[None, :, None]
-
-
-@pytest.mark.parametrize("n", [37, 128, 129, 250, 1000])
-def test_process_audio_features_matches_reference_loop(n):
-    rng = np.random.default_rng(n)
-    feats = rng.standard_normal((n, 256))
-    model = _FakeSeq2Seq()
-    cfg = {"frame_size": 128, "overlap": 16}
-
-    def decode(chunk):
-        with torch.no_grad():
-            src = torch.tensor(chunk, dtype=torch.float32).unsqueeze(0)
-            return model.decoder(model.encoder(src)).squeeze(0).numpy()
-
-    want = _reference_process(feats, decode, 128, 16)
-    got = ap.process_audio_features(feats, model, "cpu", cfg)
+@pytest.mark.parametrize("n", INFER_FRAMES)
+def test_process_audio_features_matches_reference(golden, n):
+    """Chunking, reflect padding, cross-fade, tail chunk and /100 against the
+    reference's own process_audio_features (tests/golden/inference.npz,
+    audio_processing.py:50-112), bit for bit."""
+    g = golden("inference.npz")
+    feats = np.random.default_rng(n).standard_normal((n, 256))
+    assert feats.sum() == g["feats_sum_%d" % n]
+    got = ap.process_audio_features(feats, FakeSeq2Seq(), "cpu", {"frame_size": 128, "overlap": 16})
     assert got.shape == (n, 61)
-    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got, g["fake_%d" % n])
+
+
+@pytest.mark.parametrize("tag", ["f32_61", "f64_68_emotions", "f64_68_base", "zeros_long"])
+def test_csv_writer_bytes_match_reference(golden, tmp_path, tag):
+    """The LiveLink CSV is byte-identical to the reference writer's
+    (utils/csv/save_csv.py:4-62; tests/golden/formats.npz)."""
+    g = golden("formats.npz")
+    out = tmp_path / "g.csv"
+    save_generated_data_as_csv(g["csv_in_" + tag], str(out), include_emotion_dimensions=bool(g["csv_emo_" + tag]))
+    assert out.read_bytes() == g["csv_bytes_" + tag].tobytes()
+
+
+def test_feature_cache_bytes_match_reference(golden, tmp_path, monkeypatch):
+    """collect_features writes the audio_features.csv cache byte-identically to
+    the reference (data_processing.py:112-120) and reads it back exactly."""
+    g = golden("formats.npz")
+    cols = ["Timecode", "BlendshapeCount"] + ["c%d" % i for i in range(61)]
+    facial = g["cache_facial"]
+    fpath = tmp_path / "x_iPhone_cal.csv"
+    pd.DataFrame(np.hstack([np.zeros((90, 1)), np.full((90, 1), 61), facial]), columns=cols).to_csv(fpath, index=False)
+    cache = tmp_path / "audio_features.csv"
+    monkeypatch.setattr(dp, "extract_audio_features", lambda path, sr: (g["cache_feats"], None))
+    a1, _ = dp.collect_features("clip.wav", str(cache), str(fpath), 88200, include_fast=False)
+    assert cache.read_bytes() == g["cache_bytes"].tobytes()
+    monkeypatch.setattr(dp, "extract_audio_features", None)  # second read must come from the cache
+    a2, _ = dp.collect_features("clip.wav", str(cache), str(fpath), 88200, include_fast=False)
+    # pandas' default float parser is not round-trip exact (the reference shares this)
+    np.testing.assert_allclose(a1, a2, rtol=1e-15, atol=1e-15)
+
+
+def test_clip_files_naming_rule(tmp_path):
+    """Folder discovery keeps the reference's rule: the facial CSV is the one
+    whose name contains 'iPhone_cal' (mov_extraction.py:23); mov before mp4."""
+    for name in ("a.mp4", "b.mov", "take_iPhone_cal.csv", "other.csv", "notes.txt"):
+        (tmp_path / name).write_bytes(b"")
+    found, cache = dp.clip_files(str(tmp_path))
+    assert os.path.basename(found["facial"]) == "take_iPhone_cal.csv"
+    assert {k: os.path.basename(v) for k, v in found.items() if k != "facial"} == {"mov": "b.mov", "mp4": "a.mp4"}
+    assert os.path.basename(cache) == "audio_features.csv"
 
 
 def test_csv_writer(tmp_path):

@@ -301,3 +301,21 @@ def test_long_clip_t256_parity():
     named = dict(model.named_parameters())
     for k, og in oracle_grads(oracle, list(params)).items():
         assert rel(named[k].grad, og) < 0.1, k
+
+
+def test_logged_norms_are_per_step(golden):
+    """Each step's gradient norm stays readable after later steps are queued
+    (training_utils._Pending reads step n after step n+1)."""
+    g = golden("model_tiny.npz")
+    D, H, L, seed = int(g["D"]), int(g["H"]), int(g["L"]), int(g["seed"])
+    cfg, model, crit, opt, params = make(D, H, L, seed, amp=False)
+    model.train()
+    norms = []
+    for s in range(int(g["steps"])):
+        opt.zero_grad()
+        loss = crit(model(torch.tensor(g["src%d" % s], device=DEV)), torch.tensor(g["trg%d" % s], device=DEV))
+        loss.backward()
+        opt.step(max_norm=2.0)
+        norms.append(opt.last_norm)
+    for s, n in enumerate(norms):
+        assert abs(n.item() - float(g["gnorm%d" % s])) < 1e-4 * float(g["gnorm%d" % s]), s

@@ -1,0 +1,106 @@
+"""Production-shape parity: the training step at B*T = 16,384 frames (B=128
+windows x T=128, D=1024, H=16) against the CPU oracle, through the kernels the
+228M bench runs (reference step: utils/training_utils.py:56-80).
+
+At this shape the bf16 step takes the 256x256 LDS-DMA ring GEMM for every
+projection, the grouped weight-gradient launches (one 256-tile launch per
+decoder layer, one 768-tile launch per 4 encoder layers), the fused attention
+backward over B*H = 2,048 (b, h) blocks and the batched row reductions; the
+launch counters of the C ABI (nstl_kernel_counts) assert that choice.  L=4 is
+the smallest depth with a full 4-layer encoder group.
+
+Bounds are those of tests/test_model_gpu.py (fp32: forward 1e-4, gradients 1e-4
+relative per tensor; bf16: forward 3e-2, loss 2e-2, gradients 0.1), plus the
+metric's forward MSE gate (1e-3).
+"""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from neurosync_trainer_lite_amd import _hip as K
+from oracle import model_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+D, H, L, B, T = 1024, 16, 4, 128, 128
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def problem():
+    params = model_ref.seeded_params(model_ref.param_shapes(256, D, L, 61), 61)
+    rng = np.random.default_rng(62)
+    src = torch.tensor(rng.standard_normal((B, T, 256)).astype(np.float32))
+    trg = torch.tensor((rng.standard_normal((B, T, 61)) * 20).astype(np.float32))
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    t0 = time.time()
+    oracle = model_ref.OracleTrainer(params, H)
+    o_loss, o_norm, o_pred = oracle.step(src, trg)
+    print("oracle step %.1f s" % (time.time() - t0))
+    return params, src, trg, o_loss, o_norm, o_pred, oracle.last_grads
+
+
+def run_step(params, src, trg, amp):
+    from neurosync_trainer_lite_amd.config import training_config
+    from neurosync_trainer_lite_amd.utils.model_utils import build_model, prepare_training_components
+    cfg = dict(training_config)
+    cfg.update(hidden_dim=D, num_heads=H, n_layers=L, dropout=0.0, use_amp=amp)
+    model = build_model(cfg, DEV)
+    model.load_state_dict(params, strict=True)
+    crit, opt, _ = prepare_training_components(cfg, model)
+    model.train()
+    opt.zero_grad()
+    pred = model(src.to(DEV))  # builds the workspace; the counted step follows
+    torch.cuda.synchronize()
+    K.kernel_counts_reset()
+    opt.zero_grad()
+    pred = model(src.to(DEV))
+    loss = crit(pred, trg.to(DEV))
+    loss.backward()
+    opt.step(max_norm=2.0)
+    torch.cuda.synchronize()
+    counts = K.kernel_counts()
+    grads = {k: p.grad.detach().cpu().clone() for k, p in model.named_parameters()}
+    return pred.detach().cpu(), loss.item(), opt.last_norm.item(), grads, counts
+
+
+def check_grads(grads, o_grads, bound):
+    worst = max(((rel(grads[k], og), k) for k, og in o_grads.items()), key=lambda x: x[0])
+    assert worst[0] < bound, worst
+    return worst
+
+
+def test_bf16_production_step_matches_oracle(problem):
+    params, src, trg, o_loss, o_norm, o_pred, o_grads = problem
+    pred, loss, norm, grads, c = run_step(params, src, trg, amp=True)
+    # the kernels the 228M bench runs
+    assert c["gemm_ring"] >= 16 * L, c
+    assert c["gemm_group"] == L + L // 4 and c["gemm_group_tiles"] == L * 256 + (L // 4) * 768, c
+    assert c["attn_fwd"] == 3 * L and c["attn_bwd_fused"] == 3 * L, c
+    assert c["attn_bwd_split"] == 0 and c["attn_fwd_generic"] == 0 and c["attn_bwd_generic"] == 0, c
+    assert c["gemm_splitk_reduce"] <= 2, c  # only the 61-column head's weight gradient may split
+    assert rel(pred, o_pred) < 3e-2
+    mse = ((pred.double() - o_pred.double()) ** 2).mean().item()
+    assert mse < 1e-3, mse
+    assert abs(loss - o_loss.item()) < 2e-2 * abs(o_loss.item())
+    assert abs(norm - o_norm.item()) < 2e-2 * o_norm.item()
+    worst = check_grads(grads, o_grads, 0.1)
+    print("bf16 production step: rel(pred) %.2e mse %.2e, worst grad %s" % (rel(pred, o_pred), mse, worst))
+
+
+def test_fp32_production_step_matches_oracle(problem):
+    params, src, trg, o_loss, o_norm, o_pred, o_grads = problem
+    pred, loss, norm, grads, c = run_step(params, src, trg, amp=False)
+    assert c["gemm_ring"] == 0 and c["gemm128"] > 0, c          # fp32 parity mode: the 128 kernel
+    assert c["attn_fwd"] == 3 * L and c["attn_bwd_split"] == 3 * L, c
+    assert rel(pred, o_pred) < 1e-4
+    assert ((pred.double() - o_pred.double()) ** 2).mean().item() < 1e-3
+    assert abs(loss - o_loss.item()) < 1e-5 * abs(o_loss.item())
+    assert abs(norm - o_norm.item()) < 1e-4 * o_norm.item()
+    check_grads(grads, o_grads, 1e-4)
