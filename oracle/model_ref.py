@@ -35,8 +35,8 @@ def rotate_pairs(x, cos, sin):
     """Rotate interleaved pairs (2i, 2i+1) of the last dim (model.py:44-48, :75-79)."""
     xe = x[..., 0::2]
     xo = x[..., 1::2]
-    cos = cos.to(x.dtype)
-    sin = sin.to(x.dtype)
+    cos = cos.to(x.device, x.dtype)
+    sin = sin.to(x.device, x.dtype)
     out = torch.empty_like(x)
     out[..., 0::2] = xe * cos - xo * sin
     out[..., 1::2] = xe * sin + xo * cos

@@ -64,26 +64,29 @@ def test_extract_audio_features_from_wav(tmp_path):
     np.testing.assert_allclose(feats[:, :69], want[:, :69], atol=2e-3)
 
 
-def test_batched_inference_matches_per_chunk_loop():
+def test_inference_matches_reference_fixture(golden):
+    """The per-epoch validation inference (process_audio_features,
+    audio_processing.py:50-112) of a seeded small Seq2Seq on the GPU (fp32 mode,
+    chunks batched) against the reference's own run of it on the CPU
+    (tests/golden/inference.npz, 300 frames: 3 chunks, overlap 16, tail)."""
     from neurosync_trainer_lite_amd.config import training_config
     from neurosync_trainer_lite_amd.utils.audio.processing import audio_processing as ap
     from neurosync_trainer_lite_amd.utils.model_utils import build_model
     from oracle import model_ref
-    from tests.test_host_cpu import _reference_process
+    from tests.golden.make_goldens_helpers import INFER_MODEL as mc
+    g = golden("inference.npz")
     cfg = dict(training_config)
-    cfg.update(hidden_dim=128, num_heads=2, n_layers=2, use_amp=False)
+    cfg.update(hidden_dim=mc["D"], num_heads=mc["H"], n_layers=mc["L"], use_amp=False)
     dev = torch.device("cuda:0")
     model = build_model(cfg, dev)
-    model.load_state_dict(model_ref.seeded_params(model_ref.param_shapes(256, 128, 2, 61), 3), strict=True)
-    model.eval()
-    feats = np.random.default_rng(0).standard_normal((700, 256))
-
-    def decode(chunk):
-        return ap.decode_audio_chunk(chunk, model, dev)
-
-    want = _reference_process(feats, decode, 128, 16)
-    got = ap.process_audio_features(feats, model, dev, cfg)
-    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6)
+    model.load_state_dict(model_ref.seeded_params(model_ref.param_shapes(256, mc["D"], mc["L"], 61), mc["seed"]),
+                          strict=True)
+    feats = np.random.default_rng(mc["seed"]).standard_normal((mc["frames"], 256)).astype(np.float32)
+    assert feats.astype(np.float64).sum() == g["model_feats_sum"]
+    got = ap.process_audio_features(feats, model, dev, dict(cfg, frame_size=128, overlap=16))
+    want = g["model_out"]
+    assert got.shape == want.shape
+    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
 
 
 def test_c1_train_main_full_width(tmp_path, monkeypatch):
