@@ -16,7 +16,11 @@ depth: the reference's own mixed precision (the oracle model under torch bf16
 autocast on the GPU) already misses the fp32 gradients by up to 0.11 relative
 on some tensors (tiny-norm, cancellation-dominated ones such as the q biases,
 and the deepest encoder weights: tools/diag_bf16_grads.py), so a tensor passes
-at max(0.1, 1.25 x that autocast error).
+at max(0.1, 1.25 x that autocast error).  fp32 likewise: at B*T = 16,384 the
+oracle's own fp32 forward/backward run by torch on the GPU already differs from
+the CPU run by ~1.4e-3 relative on every gradient (summation order amplified by
+the loss's first-difference terms), and ours by the same ~1.5e-3: a tensor
+passes at max(1e-4, 1.25 x the torch-GPU fp32 error).
 """
 import time
 
@@ -84,12 +88,13 @@ def check_grads(grads, o_grads, bound, floor=None):
     return max((e, k) for k, e in errs.items())
 
 
-def autocast_reference_grads(params, src, trg):
-    """The reference model's gradients under torch bf16 autocast (the oracle's
+def autocast_reference_grads(params, src, trg, dtype=torch.bfloat16):
+    """The reference model's gradients under torch autocast (the oracle's
     functional model, on the GPU): the error the reference's own mixed precision
-    carries (reference step: training_utils.py:64-70 with autocast)."""
+    carries (reference step: training_utils.py:64-70 with autocast); with
+    dtype=float32, plain torch fp32 on the GPU."""
     p = {k: v.detach().clone().to(DEV).requires_grad_(True) for k, v in params.items()}
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype != torch.float32):
         pred = model_ref.seq2seq_forward(p, src.to(DEV), H)
     model_ref.loss_fn(pred.float(), trg.to(DEV)).backward()
     return {k: v.grad.detach().cpu() for k, v in p.items()}
@@ -124,4 +129,7 @@ def test_fp32_production_step_matches_oracle(problem):
     assert ((pred.double() - o_pred.double()) ** 2).mean().item() < 1e-3
     assert abs(loss - o_loss.item()) < 1e-5 * abs(o_loss.item())
     assert abs(norm - o_norm.item()) < 1e-4 * o_norm.item()
-    check_grads(grads, o_grads, 1e-4)
+    gg = autocast_reference_grads(params, src, trg, dtype=torch.float32)
+    floor = {k: rel(gg[k], og) for k, og in o_grads.items()}
+    worst = check_grads(grads, o_grads, 1e-4, floor)
+    print("fp32 production step: rel(pred) %.2e, worst grad %s" % (rel(pred, o_pred), worst))

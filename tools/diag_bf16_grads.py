@@ -40,3 +40,15 @@ for r in rows[:25]:
     print("%-62s %9.3e %9.3e %10.3e" % (r[3], r[0], r[1], r[2]))
 print("max ours %.3e  max autocast %.3e  max ratio %.2f" % (
     max(r[0] for r in rows), max(r[1] for r in rows), max(r[0] / max(r[1], 1e-12) for r in rows)))
+
+# fp32: ours (parity mode) and the oracle's own fp32 on the GPU, against the CPU oracle
+pred32, loss32, norm32, grads32, c32 = run_step(params, src, trg, amp=False)
+p = {k: v.detach().clone().cuda().requires_grad_(True) for k, v in params.items()}
+gp = model_ref.seq2seq_forward(p, src.cuda(), H)
+model_ref.loss_fn(gp, trg.cuda()).backward()
+gg = {k: v.grad.detach().cpu() for k, v in p.items()}
+print("fp32: ours rel(pred) %.3e, torch-gpu rel(pred) %.3e" % (rel(pred32, o_pred), rel(gp.detach(), o_pred)))
+rows = sorted(((rel(grads32[k], og[k]), rel(gg[k], og[k]), og[k].norm().item(), k) for k in og), reverse=True)
+print("%-62s %9s %9s %10s" % ("tensor", "ours32", "torchgpu", "|g|"))
+for r in rows[:25]:
+    print("%-62s %9.3e %9.3e %10.3e" % (r[3], r[0], r[1], r[2]))
