@@ -445,34 +445,59 @@ constexpr int R_BK = 32, R_SLOT = 32768, R_STAGES = 5;
 // chunk with 2 ((r >> 2) & 1) gives all 16 lanes of a group distinct slots.
 NSTL_DEV int kswz(int row) { return ((row >> 2) & 1) << 1; }
 
+// Per-lane LDS-DMA sources of one operand's 16 KB stage (2 wave-instructions
+// per wave), computed once per tile: a K-step then only adds a wave-uniform
+// byte offset (k0 * 2 for K-major rows, k0 * ld * 2 for MN-major rows), so the
+// staging issue in the R phase is one 64-bit add per instruction instead of the
+// index arithmetic (and, in the grouped kernel, the reload of the problem's
+// parameters from the kernel-argument memory) it used to redo every K-step.
 template <bool KMAJ>
-NSTL_DEV void glds_stage32(char* img, const char* base, int64_t ld, int row0, int rows_total, int k0, int wave,
-                           int lane) {
-  // 16 KB operand tile = 16 wave-instructions of 1 KB, 2 per wave
+NSTL_DEV void glds_src32(const char* (&src)[2], const char* base, int64_t ld, int row0, int rows_total, int wave,
+                         int lane) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int q = wave * 2 + s;
-    const char* src;
     if (KMAJ) {  // 64-byte rows (32 k), 16 rows per KB, chunk c of row r at c ^ kswz(r)
       const int row = 16 * q + (lane >> 2), ch = (lane & 3) ^ kswz(row);
       const int gi = min(row0 + row, rows_total - 1);
-      src = base + ((int64_t)gi * ld + k0 + ch * 8) * 2;
+      src[s] = base + ((int64_t)gi * ld + ch * 8) * 2;
     } else {     // 512-byte rows (256 m/n), 2 rows per KB, ImgMN<512>
       const int row = 2 * q + (lane >> 5), pc = lane & 31;
       const int x = (row & 3) | (((row >> 3) & 1) << 2);
       const int lc = pc ^ (x << 1);
       const int gi = min(row0 + lc * 8, ((rows_total - 1) / 8) * 8);
-      src = base + ((int64_t)(k0 + row) * ld + gi) * 2;
+      src[s] = base + ((int64_t)row * ld + gi) * 2;
     }
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                     (void __attribute__((address_space(3)))*)(img + q * 1024), 16, 0, 0);
   }
 }
 
+NSTL_DEV void glds_issue32(char* img, const char* const (&src)[2], int64_t off, int wave) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src[s] + off),
+                                     (void __attribute__((address_space(3)))*)(img + (wave * 2 + s) * 1024), 16, 0, 0);
+}
+
+// one tile's staging state: the sources of A and B and their per-k byte strides
+struct RingSrc {
+  const char* a[2];
+  const char* b[2];
+  int64_t a_kb, b_kb;  // bytes per unit of k
+};
+
 template <bool AK, bool BKM>
-NSTL_DEV void ring_stage(char* slot, const GemmParams& p, int m0, int n0, int k0, int wave, int lane) {
-  glds_stage32<AK>(slot, p.A, p.lda, m0, p.M, k0, wave, lane);
-  glds_stage32<BKM>(slot + R_SLOT / 2, p.B, p.ldb, n0, p.N, k0, wave, lane);
+NSTL_DEV RingSrc ring_src(const GemmParams& p, int m0, int n0, int wave, int lane) {
+  RingSrc r;
+  glds_src32<AK>(r.a, p.A, p.lda, m0, p.M, wave, lane);
+  glds_src32<BKM>(r.b, p.B, p.ldb, n0, p.N, wave, lane);
+  r.a_kb = AK ? 2 : 2 * p.lda;
+  r.b_kb = BKM ? 2 : 2 * p.ldb;
+  return r;
+}
+
+NSTL_DEV void ring_stage(char* slot, const RingSrc& r, int k0, int wave) {
+  glds_issue32(slot, r.a, (int64_t)k0 * r.a_kb, wave);
+  glds_issue32(slot + R_SLOT / 2, r.b, (int64_t)k0 * r.b_kb, wave);
 }
 
 #define NSTL_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
@@ -841,6 +866,7 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
   const int kz1 = min(p.K, kz0 + p.k_chunk);
   const int nk = (kz1 - kz0) / R_BK;
   const uint32_t smem_u32 = lds_u32(smem);
+  const RingSrc rs = ring_src<AK, BKM>(p, m0, n0, wave, lane);
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -851,7 +877,7 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
   // prologue: tiles 0..2 in flight, tile 0 landed everywhere
 #pragma unroll
   for (int s = 0; s < 3; ++s)
-    if (s < nk) ring_stage<AK, BKM>(smem + s * R_SLOT, p, m0, n0, kz0 + s * R_BK, wave, lane);
+    if (s < nk) ring_stage(smem + s * R_SLOT, rs, kz0 + s * R_BK, wave);
   if (nk >= 3) NSTL_VMCNT(8);
   else if (nk == 2) NSTL_VMCNT(4);
   else NSTL_VMCNT(0);
@@ -877,7 +903,7 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
     if (kt + 3 < nk) {
       int s3 = slot + 3;
       if (s3 >= R_STAGES) s3 -= R_STAGES;
-      ring_stage<AK, BKM>(smem + s3 * R_SLOT, p, m0, n0, kz0 + (kt + 3) * R_BK, wave, lane);
+      ring_stage(smem + s3 * R_SLOT, rs, kz0 + (kt + 3) * R_BK, wave);
     }
     if (wm == 1) retire_next(kt, nk);
     __builtin_amdgcn_s_barrier();

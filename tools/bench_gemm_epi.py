@@ -97,5 +97,24 @@ s = t(lambda: K.gemm(At, Bt, G, 4096, 4096, M, a_kmajor=True, b_kmajor=True))
 rows.append(("TT  4096^2 K=16384", 2 * M * 4096 * 4096, s))
 s = t(lambda: K.gemm(At, X, G, 4096, 4096, M, a_kmajor=True, b_kmajor=False))
 rows.append(("TN  4096^2 K=16384", 2 * M * 4096 * 4096, s))
+# the step's grouped weight-gradient launches: one decoder layer (7 GEMMs, 256
+# tiles) and four encoder layers (16 GEMMs, 768 tiles), K = 16384 tokens
+def group(shapes):
+    probs, fl = [], 0
+    for n, k in shapes:
+        dY, X = r(M, n), r(M, k)
+        G = torch.empty(n, k, dtype=torch.float32, device=dev)
+        probs.append((dY, X, G, n, k, M, dict(a_kmajor=False, b_kmajor=False)))
+        fl += 2 * M * n * k
+    return probs, fl
+
+
+dec = [(D, F), (F, D), (D, D), (D, D), (2 * D, D), (D, D), (3 * D, D)]
+enc = [(D, F), (F, D), (D, D), (3 * D, D)] * 4
+for name, shapes in (("dW  group dec layer", dec), ("dW  group enc x4", enc)):
+    probs, fl = group(shapes)
+    s = t(lambda: K.gemm_grouped(probs))
+    rows.append((name, fl, s))
+    del probs
 for nm, fl, s in rows:
     print("%-22s %8.1f TF/s %9.1f us" % (nm, fl / s / 1e12, s * 1e6))
