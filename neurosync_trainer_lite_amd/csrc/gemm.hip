@@ -884,8 +884,14 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
   __builtin_amdgcn_s_barrier();
   if (wm == 1) __builtin_amdgcn_s_barrier();  // the stagger
 
+  // Branch-free steps (as the fp8 kernel): in the main loop both groups wait
+  // vmcnt(8) at both of their wait points (the earlier retires stage kt+1 for
+  // group 1, the later for group 0; the other is then already satisfied or
+  // nearly so), with the count a constant of each call (8 while a stage is
+  // issued three ahead, then 4, 0, 0), instead of the per-step branch chain of
+  // retire_next.
   int slot = 0;
-  for (int kt = 0; kt < nk; ++kt) {
+  auto step = [&](int kt, bool stage3, int wait) {
     // ---- R(kt)
     const uint32_t Ai = smem_u32 + slot * R_SLOT;
     const uint32_t Bi = Ai + R_SLOT / 2;
@@ -900,12 +906,15 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
       if (AK) asm_frag_k64(fa[a], Ai, wm * 128 + a * 16 + (lane & 15), 8 * (lane >> 4));
       else asm_frag_mn512(fa[a], Ai, wm * 128 + a * 16, lane);
     }
-    if (kt + 3 < nk) {
+    if (stage3) {
       int s3 = slot + 3;
       if (s3 >= R_STAGES) s3 -= R_STAGES;
       ring_stage(smem + s3 * R_SLOT, rs, kz0 + (kt + 3) * R_BK, wave);
     }
-    if (wm == 1) retire_next(kt, nk);
+    if (wait == 8) NSTL_VMCNT(8);
+    else if (wait == 4) NSTL_VMCNT(4);
+    else if (wait == 0) NSTL_VMCNT(0);
+    else if (wm == 1) retire_next(kt, nk);
     __builtin_amdgcn_s_barrier();
     // ---- M(kt)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -917,10 +926,22 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
     for (int a = 0; a < 8; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) mma16(acc[a][b], fb[b], fa[a]);
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(0);
-    if (wm == 0) retire_next(kt, nk);
+    if (wait == 8) NSTL_VMCNT(8);
+    else if (wait == 4) NSTL_VMCNT(4);
+    else if (wait == 0) NSTL_VMCNT(0);
+    else if (wm == 0) retire_next(kt, nk);
     __builtin_amdgcn_s_barrier();
     slot = slot + 1 == R_STAGES ? 0 : slot + 1;
+  };
+  if (nk >= 3) {
+    for (int kt = 0; kt + 3 < nk; ++kt) step(kt, true, 8);
+    step(nk - 3, false, 4);
+    step(nk - 2, false, 0);
+    step(nk - 1, false, 0);
+  } else {
+    for (int kt = 0; kt < nk; ++kt) step(kt, false, -1);
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger
   if (p.debug_skip_epilogue == 1) {  // timing experiments only (NSTL_GEMM_DEBUG=skip_epi)
@@ -984,24 +1005,24 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm256r_group_kernel(GroupParams g
 constexpr int F8_BK = 64;        // K bytes (= elements) per fp8 stage
 constexpr int F8_UNIT = 0x7f7f7f7f;  // E8M0 127 = 2^0 in every byte
 
-NSTL_DEV void glds_stage_f8(char* img, const char* base, int64_t ld, int row0, int rows_total, int k0, int wave,
-                            int lane) {
-  // 16 KB operand image = 16 wave-instructions of 1 KB (16 rows of 64 B), 2 per wave
+
+// per-lane sources of one fp8 stage, once per tile (K-major rows: a K-step adds k0 bytes)
+NSTL_DEV void glds_src_f8(const char* (&src)[2], const char* base, int64_t ld, int row0, int rows_total, int wave,
+                          int lane) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const int q = wave * 2 + s;
-    const int row = 16 * q + (lane >> 2);
+    const int row = 16 * (wave * 2 + s) + (lane >> 2);
     const int c = (lane & 3) ^ ((row >> 2) & 3);
-    const int gi = min(row0 + row, rows_total - 1);
-    const char* src = base + (int64_t)gi * ld + k0 + c * 16;
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                     (void __attribute__((address_space(3)))*)(img + q * 1024), 16, 0, 0);
+    src[s] = base + (int64_t)min(row0 + row, rows_total - 1) * ld + c * 16;
   }
 }
 
-NSTL_DEV void ring_stage_f8(char* slot, const GemmParams& p, int m0, int n0, int k0, int wave, int lane) {
-  glds_stage_f8(slot, p.A, p.lda, m0, p.M, k0, wave, lane);
-  glds_stage_f8(slot + R_SLOT / 2, p.B, p.ldb, n0, p.N, k0, wave, lane);
+NSTL_DEV RingSrc ring_src_f8(const GemmParams& p, int m0, int n0, int wave, int lane) {
+  RingSrc r;
+  glds_src_f8(r.a, p.A, p.lda, m0, p.M, wave, lane);
+  glds_src_f8(r.b, p.B, p.ldb, n0, p.N, wave, lane);
+  r.a_kb = r.b_kb = 1;
+  return r;
 }
 
 // one 32 x 64 fp8 fragment: lane l holds row (l & 31), K bytes 32 (l >> 5) .. +31
@@ -1033,6 +1054,7 @@ NSTL_DEV void ring_tile_f8(const GemmParams& p, int id, char* smem) {
   const int m0 = tm * BIG, n0 = tn * BIG;
   const int nk = p.K / F8_BK;
   const uint32_t smem_u32 = lds_u32(smem);
+  const RingSrc rs = ring_src_f8(p, m0, n0, wave, lane);
 
   f32x16 acc[4][2];
 #pragma unroll
@@ -1044,7 +1066,7 @@ NSTL_DEV void ring_tile_f8(const GemmParams& p, int id, char* smem) {
 
 #pragma unroll
   for (int s = 0; s < 3; ++s)
-    if (s < nk) ring_stage_f8(smem + s * R_SLOT, p, m0, n0, s * F8_BK, wave, lane);
+    if (s < nk) ring_stage(smem + s * R_SLOT, rs, s * F8_BK, wave);
   if (nk >= 3) NSTL_VMCNT(8);
   else if (nk == 2) NSTL_VMCNT(4);
   else NSTL_VMCNT(0);
@@ -1071,7 +1093,7 @@ NSTL_DEV void ring_tile_f8(const GemmParams& p, int id, char* smem) {
     if (stage3) {
       int s3 = slot + 3;
       if (s3 >= R_STAGES) s3 -= R_STAGES;
-      ring_stage_f8(smem + s3 * R_SLOT, p, m0, n0, (kt + 3) * F8_BK, wave, lane);
+      ring_stage(smem + s3 * R_SLOT, rs, (kt + 3) * F8_BK, wave);
     }
     if (wait == 8) NSTL_VMCNT(8);
     else if (wait == 4) NSTL_VMCNT(4);
