@@ -122,6 +122,9 @@ def fwd_parity(cfg, dev, T, windows=2):
         del m
         torch.cuda.empty_cache()
     out["pass"] = out["mse_fp32"] <= out["gate"]
+    if "mse_fp8" in out:  # C5: the fp8 forward is held to the same gate
+        out["pass_fp8"] = out["mse_fp8"] <= out["gate"]
+        out["pass"] = out["pass"] and out["pass_fp8"]
     return out
 
 
