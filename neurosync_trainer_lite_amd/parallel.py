@@ -68,13 +68,19 @@ def shard_batch_indices(num_batches, rank, world):
 
 
 class GradAllReducer:
-    """Bucketed asynchronous SUM all-reduce over a flat gradient arena."""
+    """Bucketed asynchronous SUM all-reduce over a flat gradient arena.
 
-    def __init__(self, grads, group=None, bucket_bytes=DEFAULT_BUCKET_BYTES):
+    ``min_world``: below this many ranks nothing is launched (an all-reduce
+    over one rank is the identity); 1 makes a single-rank group run the real
+    collectives (tests and tools/rccl_probe.py: RCCL kernels resident beside a
+    backward on one GPU)."""
+
+    def __init__(self, grads, group=None, bucket_bytes=DEFAULT_BUCKET_BYTES, min_world=2):
         self.g = grads
         self.group = group
         self.bucket = max(1, bucket_bytes // grads.element_size())
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.active = dist.is_initialized() and self.world >= min_world
         self.reset()
 
     def reset(self):
@@ -83,7 +89,7 @@ class GradAllReducer:
 
     def ready(self, upto):
         """Arena prefix [0, upto) is final: launch buckets of the unsent part."""
-        if self.world == 1:
+        if not self.active:
             return
         while upto - self.sent >= self.bucket:
             self._launch(self.sent, self.sent + self.bucket)
@@ -94,7 +100,7 @@ class GradAllReducer:
 
     def finish(self):
         """Reduce the tail and make the current stream wait for every bucket."""
-        if self.world == 1:
+        if not self.active:
             return
         if self.sent < self.g.numel():
             self._launch(self.sent, self.g.numel())
@@ -105,9 +111,8 @@ class GradAllReducer:
 
 class ShardComm:
     """Equal contiguous shards of a flat arena over the ranks of `group`:
-    reduce-scatter / all-gather helpers (RCCL collectives on nccl; gloo, used by
-    the CPU tests, has neither, so there they are built from all_reduce /
-    all_gather)."""
+    reduce-scatter / all-gather of the arena (torch's tensor collectives, the
+    same calls on RCCL and on the gloo backend of the CPU tests)."""
 
     def __init__(self, numel, group=None):
         self.group = group
@@ -119,26 +124,14 @@ class ShardComm:
         self.shard = numel // self.world
         self.lo = self.rank * self.shard
         self.hi = self.lo + self.shard
-        self._nccl = dist.get_backend(group) == "nccl"
 
     def reduce_scatter(self, full, out):
         """out (this rank's shard) = sum over ranks of full[lo:hi]."""
-        if self._nccl:
-            dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.group)
-        else:
-            t = full.clone()
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-            out.copy_(t[self.lo:self.hi])
+        dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.group)
 
     def all_gather(self, full):
         """full[every shard] = the owning rank's full[lo:hi] (in place)."""
-        mine = full[self.lo:self.hi]
-        if self._nccl:
-            dist.all_gather_into_tensor(full, mine.clone(), group=self.group)
-        else:
-            parts = [torch.empty_like(mine) for _ in range(self.world)]
-            dist.all_gather(parts, mine.contiguous(), group=self.group)
-            full.copy_(torch.cat(parts))
+        dist.all_gather_into_tensor(full, full[self.lo:self.hi].clone(), group=self.group)
 
 
 def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=None):
