@@ -215,6 +215,7 @@ class Seq2SeqEngine:
         # operands with row-wise scales (oracle/fp8_ref.py; Seq2Seq.set_fp8 or the
         # config key 'use_fp8').  Backward keeps the bf16 weights and activations.
         self.fp8 = False
+        self.fp8_scope = "attn+enc_ffn1"
         self._fp8_w = None         # (weight name, rows) -> (e4m3 [rows*N, K], f32 scales [rows*N])
         self._fp8_act = {}         # M -> (e4m3 scratch [M, max(D, Fd)], scales [M], e4m3 mem, mem scales)
         self._xq = {}              # data_ptr of an activation -> its live e4m3 copy (q, scales)
@@ -416,26 +417,45 @@ class Seq2SeqEngine:
         return s
 
     # ------------------------------------------------------------------ fp8
+    FP8_SCOPES = ("attn+enc_ffn1", "all")
+
     def fp8_groups(self):
         """(weight name, rows) of the projections whose forward runs in fp8 (C5:
-        q/k/v and FFN): self-attention q|k|v (3 matrices, one GEMM), the decoder's
-        cross-attention q and k|v, FFN linear1 and linear2."""
+        q/k/v and FFN).  Scope "attn+enc_ffn1" (default): every attention input
+        projection -- self-attention q|k|v (3 matrices, one GEMM), the decoder's
+        cross-attention q and k|v -- and the encoder's FFN linear1.  Scope "all"
+        adds the encoder FFN linear2 and the decoder FFN: its forward misses the
+        metric's 1e-3 MSE gate (1.8-2.5e-3 at the 228M config, e4m3's 3 mantissa
+        bits; per-32 E8M0 block scales do not change it), while this scope
+        measures 6.4-7.8e-4 over four seeded models (tests/test_fp8_cpu.py)."""
         out = []
         for l in range(self.L):
             pre = "encoder.transformer_encoder.%d." % l
-            out += [(pre + "self_attn.q_linear.weight", 3), (pre + "ffn.linear1.weight", 1),
-                    (pre + "ffn.linear2.weight", 1)]
+            out += [(pre + "self_attn.q_linear.weight", 3), (pre + "ffn.linear1.weight", 1)]
+            if self.fp8_scope == "all":
+                out += [(pre + "ffn.linear2.weight", 1)]
         for l in range(self.L):
             pre = "decoder.transformer_decoder.%d." % l
             out += [(pre + "self_attn.q_linear.weight", 3), (pre + "multihead_attn.q_linear.weight", 1),
-                    (pre + "multihead_attn.k_linear.weight", 2), (pre + "ffn.linear1.weight", 1),
-                    (pre + "ffn.linear2.weight", 1)]
+                    (pre + "multihead_attn.k_linear.weight", 2)]
+            if self.fp8_scope == "all":
+                out += [(pre + "ffn.linear1.weight", 1), (pre + "ffn.linear2.weight", 1)]
         return out
 
-    def set_fp8(self, on):
+    def set_fp8(self, on, scope=None):
         if on and self.dt != torch.bfloat16:
             raise ValueError("fp8 projections need the bf16 compute dtype (use_amp=True)")
+        if scope is not None:
+            if scope not in self.FP8_SCOPES:
+                raise ValueError("fp8 scope must be one of %s" % (self.FP8_SCOPES,))
+            if scope != self.fp8_scope:
+                self._fp8_w = None  # re-quantize the new set
+            self.fp8_scope = scope
         self.fp8 = bool(on)
+
+    def _fp8_on(self, name, rows=1):
+        """Does the projection `name` run in fp8 in this forward?"""
+        return self.fp8 and self._fp8_w is not None and (name, rows) in self._fp8_w
 
     def _fp8_weights(self):
         """Quantize the fp8 projections' weights from the bf16 shadow (one batched
@@ -771,7 +791,8 @@ class Seq2SeqEngine:
                    mask=bb.d_maskc[l] if bb.save else None)
         self._gemm_fwd(L_(bb.d_oc), pre + "multihead_attn.out_linear.weight", bb.y, K.EPI_BIAS)
         x2 = L_(bb.d_x2)
-        self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 2, (sd("xresid"), sd("drop2x")), L_(bb.d_s2), q8="scratch")
+        self._ln(x1, bb.y, x2, st[2:4], pre + "norm2", 2, (sd("xresid"), sd("drop2x")), L_(bb.d_s2),
+                 q8="scratch" if self._fp8_on(pre + "ffn.linear1.weight") else None)
         h = L_(bb.d_h)
         ok = self._gemm_fwd(x2, pre + "ffn.linear1.weight", h, K.EPI_BIAS_RELU_DROP, p_drop=self.p, seed=sd("ffn"),
                             relu_mask=bb.d_rmask[l] if bb.save else None)

@@ -32,8 +32,8 @@ def build_model(config, device):
     decoder = Decoder(config['output_dim'], config['hidden_dim'], config['n_layers'], config['num_heads'], config['dropout'])
     model = Seq2Seq(encoder, decoder, device).to(device)
     model.set_compute_dtype(torch.bfloat16 if config.get('use_amp', True) else torch.float32)
-    if config.get('use_fp8', False):  # BASELINE config C5 (not a reference key): fp8 q/k/v + FFN forward
-        model.set_fp8(True)
+    if config.get('use_fp8', False):  # BASELINE config C5 (not a reference key): fp8 forward projections
+        model.set_fp8(True, config.get('fp8_scope', 'attn+enc_ffn1'))
     if torch.device(device).type == 'cuda':
         model.engine(device)
     return model

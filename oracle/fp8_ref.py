@@ -39,3 +39,49 @@ def gemm(qa, sa, qb, sb):
     """s_a[i] s_b[j] sum_r qa[i][r] qb[j][r] in float64 (the products are exact)."""
     acc = qa.double() @ qb.double().T
     return acc * sa.double()[:, None] * sb.double()[None, :]
+
+
+# ----------------------------------------------------------------------------
+# C5 scope: which Linears run on fp8 operands (engine.Seq2SeqEngine.fp8_groups)
+# ----------------------------------------------------------------------------
+def scope_linears(scope, n_layers):
+    """Module names (reference state_dict prefixes) of the Linears whose forward
+    is fp8 under `scope` ("attn+enc_ffn1" or "all")."""
+    out = []
+    for l in range(n_layers):
+        e = "encoder.transformer_encoder.%d." % l
+        out += [e + "self_attn.q_linear", e + "self_attn.k_linear", e + "self_attn.v_linear", e + "ffn.linear1"]
+        if scope == "all":
+            out += [e + "ffn.linear2"]
+        d = "decoder.transformer_decoder.%d." % l
+        out += [d + "self_attn.q_linear", d + "self_attn.k_linear", d + "self_attn.v_linear",
+                d + "multihead_attn.q_linear", d + "multihead_attn.k_linear", d + "multihead_attn.v_linear"]
+        if scope == "all":
+            out += [d + "ffn.linear1", d + "ffn.linear2"]
+    return out
+
+
+def simulated_forward(params, src, num_heads, scope):
+    """The oracle forward (model_ref.seq2seq_forward, fp32) with the scope's
+    Linears taking row-quantized e4m3 operands (quant_rows of the input rows and
+    of the weight rows, products in f32): the fp8 model's error budget without
+    its bf16 rounding elsewhere."""
+    import torch.nn.functional as F
+    from oracle import model_ref
+    names = set(scope_linears(scope, model_ref.n_layers_of(params)))
+    orig = model_ref.linear
+
+    def q(x):
+        qx, sx = quant_rows(x.reshape(-1, x.shape[-1]))
+        return dequant(qx, sx).reshape(x.shape)
+
+    def lin(p, name, x):
+        if name in names:
+            return F.linear(q(x), q(p[name + ".weight"]), p[name + ".bias"])
+        return orig(p, name, x)
+
+    model_ref.linear = lin
+    try:
+        return model_ref.seq2seq_forward(params, src, num_heads)
+    finally:
+        model_ref.linear = orig
