@@ -18,7 +18,7 @@ GEMM FLOPs / GEMM time.  `cpu_baseline` times the fp32 CPU oracle step (the refe
 restated in torch-CPU) on a bounded sample on rank 0.  `parity` is the metric's
 "MSE vs ref": forward output of the full 228M config vs the fp32 CPU oracle on
 the same 2-window batch and seeded weights (fp32 mode gated at 1e-3; bf16 reported).
---fp8 is BASELINE config C5 (e4m3 q/k/v + FFN forward GEMMs; add --seq 256
+--fp8 is BASELINE config C5 (e4m3 attention q/k/v + encoder FFN1 forward GEMMs; add --seq 256
 --batch 64 for its doubled clip length): its fp8 GEMM launches are reported as
 `roofline_fp8` against the fp8 dense peak, and `parity` adds the fp8 forward MSE.
 """
@@ -93,6 +93,89 @@ def cpu_baseline(cfg, T, budget_s=20.0):
                       % (B, T, n)}
 
 
+def synth_corpus(root, clips, seconds, seed=0, sr=88200, fps=60):
+    """BASELINE C4's corpus, synthetic and seeded: per clip a
+    folder with an 88.2 kHz 16-bit mono WAV (3 harmonics of f0 ~ U[80, 300] Hz,
+    4 Hz AM, N(0, 0.01^2) noise, peak-normalised) and a 60 fps
+    *_iPhone_cal.csv of 61 blendshape/pose curves (low-pass noise: cols 0-51
+    clipped to [0, 1], cols 52-60 0.3 tanh) -- the files process_folder reads."""
+    import numpy as np
+    import pandas as pd
+    from neurosync_trainer_lite_amd.utils.audio.load_audio import write_wav
+    from neurosync_trainer_lite_amd.utils.csv.save_csv import BLENDSHAPE_COLUMNS
+    rng = np.random.default_rng(seed)
+    n, nf = int(seconds * sr), int(seconds * fps)
+    t = np.arange(n) / sr
+    k = np.exp(-np.arange(-30, 31) ** 2 / (2 * 8.0 ** 2))
+    k /= k.sum()
+    for c in range(clips):
+        d = os.path.join(root, "clip%03d" % c)
+        os.makedirs(d, exist_ok=True)
+        f0 = rng.uniform(80, 300)
+        y = sum((0.6 / h) * np.sin(2 * np.pi * h * f0 * t + rng.uniform(0, 6.28)) for h in (1, 2, 3))
+        y = y * (0.55 + 0.45 * np.sin(2 * np.pi * 4 * t)) + 0.01 * rng.standard_normal(n)
+        write_wav(os.path.join(d, "audio.wav"), (y / np.abs(y).max()).astype(np.float32), sr)
+        z = np.stack([np.convolve(rng.standard_normal(nf), k, mode="same") for _ in range(61)], 1) * 4
+        z[:, :52] = np.clip(z[:, :52], 0, 1)
+        z[:, 52:] = 0.3 * np.tanh(z[:, 52:])
+        df = pd.DataFrame(z, columns=BLENDSHAPE_COLUMNS)
+        df.insert(0, "BlendshapeCount", 61)
+        df.insert(0, "Timecode", ["%02d:%02d:%02d:%02d.000" % (i // 216000, i // 3600 % 60, i // 60 % 60, i % 60)
+                                  for i in range(nf)])
+        df.to_csv(os.path.join(d, "take_iPhone_cal.csv"), index=False)
+
+
+def data_feed(cfg, args, step_fn, dev, rank, world):
+    """BASELINE C4's feed: the synthetic corpus through the drop-in data path
+    (prepare_dataloader_with_split -> load_data -> collect_features with
+    include_fast + include_slow -> GPU feature extraction -> windows), batches
+    fetched whole into pinned host memory and copied with non_blocking H2D into
+    the same train step; rank r of n takes batches r, r+n, ... (rank_batches)."""
+    import tempfile
+    from neurosync_trainer_lite_amd.dataset.dataset import prepare_dataloader_with_split
+    from neurosync_trainer_lite_amd.utils.training_utils import rank_batches
+    t0 = time.perf_counter()
+    with tempfile.TemporaryDirectory(prefix="nstl_c4_%d_" % rank) as root:
+        synth_corpus(root, args.feed_clips, args.feed_seconds, seed=0)
+        c = dict(cfg, root_dir=root, include_fast=True, include_slow=True)
+        torch.manual_seed(4321)  # the same split and order on every rank
+        ds_tr, ds_val, dl, _ = prepare_dataloader_with_split(c, val_split=0.1)
+    build_s = time.perf_counter() - t0
+    n_frames = sum(len(a) for a, _ in ds_tr.dataset.clips)
+    log("C4 corpus: %d clips x %.0f s -> %d frames (fast+slow), %d train windows, built in %.1fs"
+        % (args.feed_clips, args.feed_seconds, n_frames, len(ds_tr), build_s))
+    it = rank_batches(dl, rank, world) if world > 1 else enumerate(dl)
+
+    def fed_step():
+        _, (src, trg) = next(it)
+        return step_fn(src.to(dev, non_blocking=True), trg.to(dev, non_blocking=True))
+
+    for _ in range(3):
+        fed_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.feed_steps):
+        fed_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t1
+    if world > 1:
+        tt = torch.tensor([el], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        el = tt.item()
+    B, T = args.batch, args.seq
+    return {"value": round(B * T * world * args.feed_steps / el, 1), "unit": "frames/s",
+            "ms_per_step": round(el / args.feed_steps * 1e3, 3), "steps": args.feed_steps,
+            "corpus": "%d synthetic clips x %.0f s, include_fast + include_slow: %d frames, %d train windows"
+                      % (args.feed_clips, args.feed_seconds, n_frames, len(ds_tr)),
+            "corpus_build_s": round(build_s, 1),
+            "path": "prepare_dataloader_with_split -> DataLoader(batched fetch into pinned host memory, shuffle) "
+                    "-> non_blocking H2D -> train step"}
+
+
 def fwd_parity(cfg, dev, T, windows=2):
     """BASELINE metric's "MSE vs ref" (SURVEY.md 8(d)(i)): forward output of the
     full 228M config (all 8+8 layers) vs the fp32 CPU oracle on the same batch
@@ -141,6 +224,11 @@ def main():
                     help="timed steps (the last ones) whose GEMM launches carry HIP timing events")
     ap.add_argument("--feature-steps", type=int, default=10,
                     help="steps of the feature-inclusive variant (raw audio -> GPU features -> step); 0 = skip")
+    ap.add_argument("--feed-steps", type=int, default=20,
+                    help="steps of the C4 data-feed variant (synthetic corpus with fast+slow augmentation through "
+                         "the DataLoader with pinned non_blocking H2D); 0 = skip")
+    ap.add_argument("--feed-clips", type=int, default=16)
+    ap.add_argument("--feed-seconds", type=float, default=60.0)
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE config C5: q/k/v + FFN forward GEMMs on e4m3 operands (row-wise scales); "
                          "C5 also doubles the clip length: --seq 256 --batch 64")
@@ -172,9 +260,9 @@ def main():
     src = torch.randn(B, T, cfg["input_dim"], device=dev, generator=g)
     trg = torch.randn(B, T, cfg["output_dim"], device=dev, generator=g) * 20
 
-    def step():
+    def step(x=src, y=trg):
         opt.zero_grad()
-        loss = crit(model(src), trg)
+        loss = crit(model(x), y)
         loss.backward()
         opt.step(max_norm=2.0)
         return loss
@@ -258,7 +346,7 @@ def main():
     if ev8:
         ms8 = sum(a.elapsed_time(b) for a, b, _, _, _ in ev8)
         tf8 = sum(f for _, _, f, _, _ in ev8) / (ms8 * 1e-3) / 1e12
-        fp8_roof = {"bound": "mfma", "kernel": "gemm256f8_kernel (e4m3 q/k/v + FFN forward, row scales)",
+        fp8_roof = {"bound": "mfma", "kernel": "gemm256f8_kernel (e4m3 attention q/k/v + encoder FFN1 forward, row scales)",
                     "achieved": round(tf8, 1), "peak": FP8_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(tf8 / FP8_DENSE_PEAK_TFLOPS, 4), "launches": len(ev8),
                     "avg_launch_us": round(ms8 * 1e3 / len(ev8), 2),
@@ -319,6 +407,11 @@ def main():
                 "workload": "per step: %.1f s of synthetic 88.2 kHz audio per GPU -> GPU MFCC(+d,dd)+autocorr "
                             "features [%d frames x 256] -> the same train step" % (n_samp / sr, B * T)}
 
+    feed = None
+    if args.feed_steps > 0:
+        feed = data_feed(cfg, args, step, dev, rank, world)
+        feed["vs_resident"] = round(feed["value"] / value, 4)
+
     if rank == 0:
         out = {
             "metric": "train frames/sec (audio->blendshape) 228M cfg",
@@ -351,11 +444,13 @@ def main():
         }
         if fp8_roof is not None:
             out["roofline_fp8"] = fp8_roof
-            out["dtype"] = "bf16 + e4m3 (q/k/v + FFN forward GEMMs, row-wise scales)"
+            out["dtype"] = "bf16 + e4m3 (attention q/k/v + encoder FFN1 forward GEMMs, row-wise scales)"
             out["config"]["workload"] = ("C5: 228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam), "
-                                         "fp8 q/k/v + FFN forward, T=%d" % T)
+                                         "fp8 attention q/k/v + encoder FFN1 forward, T=%d" % T)
         if feat is not None:
             out["feature_inclusive"] = feat
+        if feed is not None:
+            out["data_feed"] = feed
         if world == 1 and not args.no_parity:
             out["parity"] = fwd_parity(cfg, dev, T)
             log("parity: %s" % out["parity"])

@@ -18,13 +18,16 @@ COLUMNS_TO_DROP = ['Timecode', 'BlendshapeCount']
 _NOISE_COLUMNS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60]
 
 
-def load_data(root_dir, sr, processed_folders):
-    """data_processing.py:10-26: one (audio_features, facial_data) per clip folder."""
+def load_data(root_dir, sr, processed_folders, include_fast=True, include_slow=False):
+    """data_processing.py:10-26: one (audio_features, facial_data) per clip folder.
+    include_fast / include_slow reach collect_features (the reference fixes them
+    at its defaults, fast on and slow off; BASELINE config C4 turns slow on)."""
     examples = []
     for folder in os.listdir(root_dir):
         folder_path = os.path.join(root_dir, folder)
         if os.path.isdir(folder_path) and folder not in processed_folders:
-            audio_features, facial_data = process_folder(folder_path, sr)
+            audio_features, facial_data = process_folder(folder_path, sr, include_fast=include_fast,
+                                                         include_slow=include_slow)
             if audio_features is not None and facial_data is not None:
                 examples.append((audio_features, facial_data))
                 processed_folders.add(folder)
@@ -54,7 +57,8 @@ def clip_files(folder_path):
     return found, os.path.join(folder_path, 'audio_features.csv')
 
 
-def process_folder(folder_path, sr, apply_smoothing=False, apply_over_scale=False):
+def process_folder(folder_path, sr, apply_smoothing=False, apply_over_scale=False, include_fast=True,
+                   include_slow=False):
     """data_processing.py:44-78.  A video clip (mov preferred over mp4, as the
     reference's ``mov_path or mp4_path``) is decoded by ffmpeg inside
     load_audio rather than first written to an audio.wav beside it."""
@@ -62,7 +66,8 @@ def process_folder(folder_path, sr, apply_smoothing=False, apply_over_scale=Fals
     facial_csv_path = found.get('facial')
     audio_path = found.get('mov') or found.get('mp4') or found.get('wav')
     if facial_csv_path and (audio_path or os.path.exists(audio_features_csv_path)):
-        audio_features, facial_data = collect_features(audio_path, audio_features_csv_path, facial_csv_path, sr)
+        audio_features, facial_data = collect_features(audio_path, audio_features_csv_path, facial_csv_path, sr,
+                                                       include_fast=include_fast, include_slow=include_slow)
         if apply_over_scale:
             facial_data = scale_facial_data(facial_data)
         facial_data[:, :61] *= 100

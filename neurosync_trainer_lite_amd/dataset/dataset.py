@@ -8,6 +8,13 @@ front (the reference keeps ~162 KB per window in host RAM, README.md:34):
 each clip is stored once as float32 and a window is sliced when requested.
 Values are identical: the reference casts each window float64 -> float32
 elementwise, here the clip is cast once.
+
+Batches are fetched whole (``__getitems__``, which torch's DataLoader and
+random_split's Subset call with a batch's indices): the windows are copied
+straight into one page-locked (pinned) host batch from the caching host
+allocator, so ``src.to(device, non_blocking=True)`` in the training loop is an
+asynchronous DMA, and the allocator keeps a pinned block out of reuse until the
+copies that read it have finished.
 """
 import numpy as np
 import torch
@@ -81,7 +88,10 @@ class AudioFacialDataset(Dataset):
         self.processed_folders = set()
         self.clips = []   # [(audio f32 [N, 256], facial f32 [N, 61])]
         self.index = []   # [(clip, start, is_tail)]
-        for audio_features, facial_data in load_data(self.root_dir, self.sr, self.processed_folders):
+        self.pin = torch.cuda.is_available()
+        for audio_features, facial_data in load_data(self.root_dir, self.sr, self.processed_folders,
+                                                     include_fast=config.get('include_fast', True),
+                                                     include_slow=config.get('include_slow', False)):
             self.add_clip(audio_features, facial_data)
 
     def add_clip(self, audio_features, facial_data):
@@ -106,9 +116,31 @@ class AudioFacialDataset(Dataset):
         return (torch.from_numpy(_window(audio, start, w, tail, end)),
                 torch.from_numpy(_window(facial, start, w, tail, end)))
 
+    def __getitems__(self, indices):
+        """A whole batch (torch DataLoader batched fetch): windows copied into one
+        pinned (src, trg) pair, in index order."""
+        w = self.micro_batch_size
+        a0, f0 = self.clips[self.index[indices[0]][0]] if len(indices) else (np.zeros((0, 256)), np.zeros((0, 61)))
+        src = torch.empty((len(indices), w, a0.shape[1]), dtype=torch.float32, pin_memory=self.pin)
+        trg = torch.empty((len(indices), w, f0.shape[1]), dtype=torch.float32, pin_memory=self.pin)
+        s_np, t_np = src.numpy(), trg.numpy()
+        for i, idx in enumerate(indices):
+            c, start, tail = self.index[idx]
+            audio, facial = self.clips[c]
+            end = max(len(audio), len(facial))
+            for x, out in ((audio, s_np[i]), (facial, t_np[i])):
+                if not tail and start + w <= len(x):
+                    out[:] = x[start:start + w]  # the common case: one contiguous copy
+                else:
+                    out[:] = _window(x, start, w, tail, end)
+        return _Batch(src, trg)
+
     @staticmethod
     def collate_fn(batch):
-        """dataset.py:51-56 (every window has the same length: a stack)."""
+        """dataset.py:51-56 (every window has the same length: a stack); a batch
+        fetched whole by __getitems__ passes through."""
+        if isinstance(batch, _Batch):
+            return batch.src, batch.trg
         src_batch, trg_batch = zip(*batch)
         return torch.stack(src_batch), torch.stack(trg_batch)
 
@@ -119,6 +151,13 @@ class AudioFacialDataset(Dataset):
         return [(torch.from_numpy(_window(np.asarray(audio_features, dtype=np.float32), s, w, t, end)),
                  torch.from_numpy(_window(np.asarray(facial_data, dtype=np.float32), s, w, t, end)))
                 for s, t in window_plan(len(audio_features), len(facial_data), w)]
+
+
+class _Batch:
+    """(src [B, T, 256], trg [B, T, 61]) as fetched by __getitems__."""
+
+    def __init__(self, src, trg):
+        self.src, self.trg = src, trg
 
 
 class _LazyExamples:

@@ -160,8 +160,10 @@ def rank_batches(dataloader, rank, world):
         return
     order = list(bs)
     ds, collate = dataloader.dataset, dataloader.collate_fn
+    fetch = getattr(ds, "__getitems__", None)  # batched pinned fetch (dataset.AudioFacialDataset)
     for s in range(steps):
-        yield s, collate([ds[i] for i in order[s * world + rank]])
+        idx = order[s * world + rank]
+        yield s, collate(fetch(idx) if callable(fetch) else [ds[i] for i in idx])
 
 
 def attach_data_parallel(model, optimizer, world):

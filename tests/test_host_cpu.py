@@ -20,6 +20,7 @@ def _dataset(window=128):
     ds = AudioFacialDataset.__new__(AudioFacialDataset)
     ds.micro_batch_size = window
     ds.clips, ds.index = [], []
+    ds.pin = False
     return ds
 
 
@@ -204,3 +205,24 @@ def test_comparison_stats():
     overall, per_dim = comparison_stats(gen, gt)
     assert overall['Mean Squared Error (MSE)'] == pytest.approx(np.mean((gt[:48] - gen) ** 2))
     assert len(per_dim) == 61 and per_dim['JawOpen']['MAE'] > 0
+
+
+def test_batched_fetch_equals_per_window(golden):
+    """__getitems__ (the DataLoader's batched fetch into one host batch) returns
+    exactly the windows __getitem__ does, tails and short streams included, and
+    the DataLoader path collates it unchanged."""
+    from torch.utils.data import DataLoader, random_split
+    ds = _dataset()
+    rng = np.random.default_rng(4)
+    for na, nf in ((300, 300), (256, 260), (1000, 997), (128, 128)):
+        ds.add_clip(rng.standard_normal((na, 256)), rng.standard_normal((nf, 61)))
+    idx = list(rng.permutation(len(ds))[:77]) + [len(ds) - 1, 0]
+    src, trg = AudioFacialDataset.collate_fn(ds.__getitems__(idx))
+    for i, j in enumerate(idx):
+        a, f = ds[j]
+        assert torch.equal(src[i], a) and torch.equal(trg[i], f)
+    train, _ = random_split(ds, [len(ds) - 10, 10], generator=torch.Generator().manual_seed(0))
+    dl = DataLoader(train, batch_size=32, shuffle=False, collate_fn=AudioFacialDataset.collate_fn)
+    s0, t0 = next(iter(dl))
+    want = [ds[train.indices[i]] for i in range(32)]
+    assert torch.equal(s0, torch.stack([w[0] for w in want])) and torch.equal(t0, torch.stack([w[1] for w in want]))
