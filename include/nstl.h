@@ -268,6 +268,18 @@ int nstl_features(const float* y, int64_t n_samples, int sr, float* out, int64_t
 int64_t nstl_features_workspace_bytes(int64_t n_samples, int sr);
 int nstl_features_frames(int64_t n_samples, int sr);
 
+/* The frame-axis stages of nstl_features on their own.
+ * nstl_cmvn_delta_reduce: x f32 [ncoef][F] (coefficient-major, F >= 9) ->
+ *   out f32 [(F+1)/2][ld_out], columns [0, ncoef) = reduce(cmvn(x)),
+ *   [ncoef, 2 ncoef) = reduce(delta1(cmvn(x))), [2 ncoef, 3 ncoef) = reduce(delta2(...)).
+ *   Replaces cepstral_mean_variance_normalization + librosa.feature.delta +
+ *   reduce_features (extract_features_utils.py:5-8, :25-27, :33-44).
+ * nstl_reduce_frame_pairs: x f64 [F][cols] -> out f32 [(F+1)/2] rows, columns
+ *   [col0, col0 + cols) = means of frame pairs (2k, 2k+1), an odd last frame kept
+ *   (reduce_features, extract_features_utils.py:33-44, on the autocorrelation lags). */
+int nstl_cmvn_delta_reduce(const float* x, int ncoef, int F, float* out, int64_t ld_out, void* stream);
+int nstl_reduce_frame_pairs(const double* x, int F, int cols, float* out, int64_t ld_out, int col0, void* stream);
+
 const char* nstl_last_error_string(void);
 int nstl_version(void);
 

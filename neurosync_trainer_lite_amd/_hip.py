@@ -110,6 +110,7 @@ EXPORTS = [
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
     "nstl_features", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
     "nstl_version", "nstl_fp8_quant_rows", "nstl_kernel_counts", "nstl_kernel_counts_reset",
+    "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs",
 ]
 
 # nstl_kernel_counts order (NSTL_K_* in include/nstl.h)
@@ -164,6 +165,8 @@ def lib():
         L.nstl_features_frames.restype = _i32
         L.nstl_last_error_string.restype = ctypes.c_char_p
         L.nstl_version.restype = _i32
+        L.nstl_cmvn_delta_reduce.argtypes = [_vp, _i32, _i32, _vp, _i64, _vp]
+        L.nstl_reduce_frame_pairs.argtypes = [_vp, _i32, _i32, _vp, _i64, _i32, _vp]
         L.nstl_kernel_counts.argtypes = [_vp, _i32]
         L.nstl_kernel_counts.restype = _i32
         L.nstl_kernel_counts_reset.restype = None
@@ -175,6 +178,20 @@ def check(rc, what):
     if rc != 0:
         msg = lib().nstl_last_error_string().decode(errors="replace")
         raise RuntimeError("%s failed (code %d): %s" % (what, rc, msg))
+
+
+def cmvn_delta_reduce(x, out, stream=None):
+    """x f32 [ncoef, F] (device) -> out f32 [(F+1)/2, >= 3 ncoef] (nstl_cmvn_delta_reduce)."""
+    ncoef, F = x.shape
+    check(lib().nstl_cmvn_delta_reduce(x.data_ptr(), ncoef, F, out.data_ptr(), out.stride(0),
+                                       stream if stream is not None else stream_of()), "nstl_cmvn_delta_reduce")
+
+
+def reduce_frame_pairs(x, out, col0=0, stream=None):
+    """x f64 [F, cols] (device) -> out f32 [(F+1)/2, >= col0 + cols] (nstl_reduce_frame_pairs)."""
+    F, cols = x.shape
+    check(lib().nstl_reduce_frame_pairs(x.data_ptr(), F, cols, out.data_ptr(), out.stride(0), col0,
+                                        stream if stream is not None else stream_of()), "nstl_reduce_frame_pairs")
 
 
 def kernel_counts():

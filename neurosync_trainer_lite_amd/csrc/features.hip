@@ -380,8 +380,9 @@ __device__ __forceinline__ float block_sum_f64(double v, double* red) {
   return (float)s;
 }
 
-// One workgroup per MFCC coefficient: CMVN, deltas, pair reduction -> out.
-__global__ __launch_bounds__(1024) void cmvn_delta_reduce_kernel(const float* __restrict__ mfcc, int F,
+// One workgroup per MFCC coefficient: CMVN, deltas, pair reduction -> out
+// columns [c | ncoef + c | 2 ncoef + c] (ncoef = 23 in the feature pipeline).
+__global__ __launch_bounds__(1024) void cmvn_delta_reduce_kernel(const float* __restrict__ mfcc, int F, int ncoef,
                                                                  const float* __restrict__ sg, float* __restrict__ out,
                                                                  int64_t ldo, int F60) {
   __shared__ double red[16];
@@ -416,8 +417,8 @@ __global__ __launch_bounds__(1024) void cmvn_delta_reduce_kernel(const float* __
     const float scale = j_end - 2 * r == 2 ? 0.5f : 1.f;
     float* o = out + (int64_t)r * ldo;
     o[c] = v[0] * scale;
-    o[N_MFCC + c] = v[1] * scale;
-    o[2 * N_MFCC + c] = v[2] * scale;
+    o[ncoef + c] = v[1] * scale;
+    o[2 * ncoef + c] = v[2] * scale;
   }
 }
 
@@ -518,12 +519,41 @@ extern "C" int nstl_features(const float* y, int64_t n_samples, int sr, float* o
   NSTL_LAUNCH_CHECK("nstl_features mel");
   hipLaunchKernelGGL(dct_kernel, dim3((L.F + 63) / 64), dim3(256), 0, st, db, L.F, T->dct, key, mf);
   NSTL_LAUNCH_CHECK("nstl_features dct");
-  hipLaunchKernelGGL(cmvn_delta_reduce_kernel, dim3(N_MFCC), dim3(1024), 0, st, mf, L.F, T->sg, out, ld_out, L.F60);
+  hipLaunchKernelGGL(cmvn_delta_reduce_kernel, dim3(N_MFCC), dim3(1024), 0, st, mf, L.F, N_MFCC, T->sg, out, ld_out,
+                     L.F60);
   NSTL_LAUNCH_CHECK("nstl_features cmvn");
   if (int rc = nstl_autocorr(y, n_samples, L.n_fft, L.hop, N_AC, ac, L.F, stream)) return rc;
   const int64_t n_red = (int64_t)L.F60 * N_AC;
   hipLaunchKernelGGL(reduce_ac_kernel, dim3((unsigned)((n_red + 255) / 256)), dim3(256), 0, st, ac, L.F, N_AC, out,
                      ld_out, 3 * N_MFCC, L.F60);
   NSTL_LAUNCH_CHECK("nstl_features reduce");
+  return 0;
+}
+
+// The two frame-axis stages of the feature pipeline on their own (their
+// reference counterparts are pinned by tests/golden/features_autocorr.npz):
+// cepstral_mean_variance_normalization + librosa.feature.delta (width 9, orders
+// 1 and 2) + reduce_features of [ncoef][F] coefficient rows, and reduce_features
+// of [F][cols] f64 rows (the autocorrelation lags).
+extern "C" int nstl_cmvn_delta_reduce(const float* x, int ncoef, int F, float* out, int64_t ld_out, void* stream) {
+  NSTL_CHECK_ARG(x && out && ncoef > 0 && F >= SG_W, "nstl_cmvn_delta_reduce: bad sizes (F >= %d)", SG_W);
+  NSTL_CHECK_ARG(ld_out >= 3 * ncoef, "nstl_cmvn_delta_reduce: ld_out < 3 ncoef");
+  const FeatTables* T = nullptr;
+  if (int rc = get_tables(88200, &T)) return rc;  // the Savitzky-Golay table does not depend on sr
+  hipLaunchKernelGGL(cmvn_delta_reduce_kernel, dim3(ncoef), dim3(1024), 0, (hipStream_t)stream, x, F, ncoef, T->sg, out,
+                     ld_out, (F + 1) / 2);
+  NSTL_LAUNCH_CHECK("nstl_cmvn_delta_reduce");
+  return 0;
+}
+
+extern "C" int nstl_reduce_frame_pairs(const double* x, int F, int cols, float* out, int64_t ld_out, int col0,
+                                       void* stream) {
+  NSTL_CHECK_ARG(x && out && F > 0 && cols > 0 && col0 >= 0 && ld_out >= col0 + cols,
+                 "nstl_reduce_frame_pairs: bad sizes");
+  const int F60 = (F + 1) / 2;
+  const int64_t n = (int64_t)F60 * cols;
+  hipLaunchKernelGGL(reduce_ac_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, F, cols,
+                     out, ld_out, col0, F60);
+  NSTL_LAUNCH_CHECK("nstl_reduce_frame_pairs");
   return 0;
 }

@@ -33,6 +33,57 @@ def _rope_apply(x, dim):
     return out
 
 
+# ------------------------------------------------------------ module-level forwards
+# A layer or block of the module tree can also run on its own, as the reference
+# allows (e.g. CustomTransformerEncoderLayer(...)(x)): f32 on the HIP kernels
+# (nstl_gemm, nstl_rope, nstl_attn_fwd, nstl_ln_fwd), forward only.  Training
+# runs the whole Seq2Seq on the fused engine instead, so a module-level call in
+# training mode with dropout > 0, or one that would need autograd, raises.
+def _check_module_call(module, *xs, mask=None):
+    if mask is not None:
+        raise NotImplementedError("attention masks are not used by the reference model (mask=None only)")
+    for x in xs:
+        _require_gpu(x, type(module).__name__)
+    p = max([m.p for m in module.modules() if isinstance(m, nn.Dropout)] + [0.0])
+    if module.training and p > 0:
+        raise RuntimeError("%s: a module-level forward is inference-only (eval() or dropout 0); training runs "
+                           "fused inside Seq2Seq" % type(module).__name__)
+    if torch.is_grad_enabled() and (any(x.requires_grad for x in xs) or
+                                    any(q.requires_grad for q in module.parameters())):
+        raise RuntimeError("%s: a module-level forward has no backward; run it under torch.no_grad() (training "
+                           "runs fused inside Seq2Seq)" % type(module).__name__)
+
+
+def _linear_f32(x2, lin, epilogue=K.EPI_BIAS):
+    """x2 f32 [M, in] -> f32 [M, out] = x2 W^T + b (nstl_gemm, f32 MFMA)."""
+    W = lin.weight.detach().float().contiguous()
+    out = torch.empty(x2.shape[0], W.shape[0], dtype=torch.float32, device=x2.device)
+    K.gemm(x2, W, out, x2.shape[0], W.shape[0], W.shape[1], epilogue=epilogue,
+           bias=lin.bias.detach().float().contiguous())
+    return out
+
+
+def _rows_f32(x):
+    return x.detach().reshape(-1, x.shape[-1]).float().contiguous()
+
+
+def _layer_norm_f32(ln, x2, y2):
+    """LayerNorm(x2 + y2) (post-LN residual), f32 rows (nstl_ln_fwd)."""
+    M, D = x2.shape
+    out = torch.empty_like(x2)
+    mean = torch.empty(M, dtype=torch.float32, device=x2.device)
+    rstd = torch.empty_like(mean)
+    a = K.LnArgs()
+    a.dtype, a.rows, a.D = K.F32, M, D
+    a.x, a.y = x2.data_ptr(), y2.data_ptr()
+    a.n_masks, a.p_drop = 0, 0.0
+    a.gamma, a.beta, a.eps = (ln.weight.detach().float().contiguous().data_ptr(),
+                              ln.bias.detach().float().contiguous().data_ptr(), ln.eps)
+    a.out, a.mean, a.rstd = out.data_ptr(), mean.data_ptr(), rstd.data_ptr()
+    K.ln_fwd(a)
+    return out
+
+
 def _owner_engine(module, device):
     ref = getattr(module, "_owner_ref", None)
     owner = ref() if ref is not None else None
@@ -88,8 +139,26 @@ class MultiHeadAttention(nn.Module):
         self.dropout = dropout
         self.flash = True
 
-    def forward(self, *a, **k):
-        raise RuntimeError("MultiHeadAttention runs fused inside Seq2Seq/Encoder/Decoder on MI355X")
+    def forward(self, query, key, value, mask=None):
+        """model.py:110-141 -> (output [B, Tq, D], attn_weights = None: the
+        reference's SDPA branch returns no weights)."""
+        _check_module_call(self, query, key, value, mask=mask)
+        B, Tq, D = query.shape
+        Tk = key.shape[1]
+        if Tk != Tq or value.shape[1] != Tk:
+            raise NotImplementedError("nstl_attn takes equal query and key lengths (the model's case)")
+        H, dh = self.num_heads, self.head_dim
+        q = _linear_f32(_rows_f32(query), self.q_linear)
+        k = _linear_f32(_rows_f32(key), self.k_linear)
+        v = _linear_f32(_rows_f32(value), self.v_linear)
+        cs, sn = rotation_tables(Tq, dh, query.device)
+        for t in (q, k):  # apply_rope_qk: per-head pairs, position = row % T
+            K.rope(t, D, t, D, B * Tq, D, cs, sn, Tq, dh)
+        o = torch.empty_like(q)
+        lse = torch.empty(B * H * Tq, dtype=torch.float32, device=query.device)
+        K.attn_fwd(K.attn_args(K.F32, B, Tq, H, q.data_ptr(), D, k.data_ptr(), D, v.data_ptr(), D, o.data_ptr(), D,
+                               lse.data_ptr(), 0.0, 0, dh=dh))
+        return _linear_f32(o, self.out_linear).view(B, Tq, D), None
 
 
 class FeedForwardNetwork(nn.Module):
@@ -102,7 +171,10 @@ class FeedForwardNetwork(nn.Module):
         self.linear2 = nn.Linear(dim_feedforward, hidden_dim)
 
     def forward(self, x):
-        raise RuntimeError("FeedForwardNetwork runs fused inside Seq2Seq/Encoder/Decoder on MI355X")
+        """model.py:153-158: linear2(dropout(relu(linear1(x)))) (ReLU in the GEMM epilogue)."""
+        _check_module_call(self, x)
+        h = _linear_f32(_rows_f32(x), self.linear1, epilogue=K.EPI_BIAS_RELU_DROP)
+        return _linear_f32(h, self.linear2).view(*x.shape[:-1], self.linear2.out_features)
 
 
 class CustomTransformerEncoderLayer(nn.Module):
@@ -118,7 +190,13 @@ class CustomTransformerEncoderLayer(nn.Module):
         self.dropout2 = nn.Dropout(dropout)
 
     def forward(self, src, mask=None):
-        raise RuntimeError("encoder layers run fused inside Encoder on MI355X")
+        """model.py:173-181 (post-LN)."""
+        _check_module_call(self, src, mask=mask)
+        x = _rows_f32(src)
+        a, _ = self.self_attn(src, src, src)
+        x = _layer_norm_f32(self.norm1, x, _rows_f32(a))
+        f = self.ffn(x.view(src.shape))
+        return _layer_norm_f32(self.norm2, x, _rows_f32(f)).view(src.shape)
 
 
 class CustomTransformerDecoderLayer(nn.Module):
@@ -137,7 +215,15 @@ class CustomTransformerDecoderLayer(nn.Module):
         self.dropout3 = nn.Dropout(dropout)
 
     def forward(self, tgt, memory, tgt_mask=None, memory_mask=None):
-        raise RuntimeError("decoder layers run fused inside Decoder on MI355X")
+        """model.py:196-208 (post-LN: self-attention, cross-attention, FFN)."""
+        _check_module_call(self, tgt, memory, mask=tgt_mask if tgt_mask is not None else memory_mask)
+        x = _rows_f32(tgt)
+        a, _ = self.self_attn(tgt, tgt, tgt)
+        x = _layer_norm_f32(self.norm1, x, _rows_f32(a))
+        c, _ = self.multihead_attn(x.view(tgt.shape), memory, memory)
+        x = _layer_norm_f32(self.norm2, x, _rows_f32(c))
+        f = self.ffn(x.view(tgt.shape))
+        return _layer_norm_f32(self.norm3, x, _rows_f32(f)).view(tgt.shape)
 
 
 class Encoder(nn.Module):

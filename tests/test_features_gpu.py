@@ -107,3 +107,35 @@ def test_c1_train_main_full_width(tmp_path, monkeypatch):
     assert os.path.exists("out/model.pth") and os.path.exists(cfg["checkpoint_path"])
     stats = open("dataset/validation_plots/stats/comparison_stats_epoch_1.txt").read()
     assert "Mean Squared Error (MSE)" in stats
+
+
+@pytest.mark.parametrize("key", ["reduce_in", "reduce_in_even"])
+def test_cmvn_and_pair_reduce_match_reference_fixtures(golden, key):
+    """The HIP frame-axis stages fed the reference-pinned fixtures directly
+    (tests/golden/features_autocorr.npz, generated by the reference's own
+    reduce_features / cepstral_mean_variance_normalization): the pair reduction
+    of f64 rows bit for bit (f64 pair means cast to f32), CMVN then reduction
+    within f32 rounding; the delta columns against the oracle's Savitzky-Golay
+    restatement (librosa.feature.delta: parity unpinned)."""
+    from neurosync_trainer_lite_amd import _hip as K
+    g = golden("features_autocorr.npz")
+    x = g[key]                                   # [C, F] f64
+    out_key = "reduce_out" if key == "reduce_in" else "reduce_out_even"
+    C, F = x.shape
+    F60 = (F + 1) // 2
+    dev = "cuda:0"
+    # reduce_features on [F][cols] f64 rows (the autocorrelation-lag layout)
+    red = torch.zeros(F60, C + 3, dtype=torch.float32, device=dev)
+    K.reduce_frame_pairs(torch.tensor(x.T.copy(), device=dev), red, col0=3)
+    torch.cuda.synchronize()
+    assert np.array_equal(red[:, 3:].cpu().numpy(), g[out_key].T.astype(np.float32))
+    # CMVN + deltas + reduction of coefficient rows (the MFCC layout)
+    out = torch.zeros(F60, 3 * C, dtype=torch.float32, device=dev)
+    K.cmvn_delta_reduce(torch.tensor(x, dtype=torch.float32, device=dev), out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().astype(np.float64)
+    cm = g["cmvn_out"] if key == "reduce_in" else data_ref.cmvn(x)
+    np.testing.assert_allclose(got[:, :C], data_ref.reduce_features(cm).T, rtol=1e-5, atol=1e-6)
+    for o in (1, 2):
+        want = data_ref.reduce_features(data_ref.savgol_delta(cm, o)).T
+        np.testing.assert_allclose(got[:, o * C:(o + 1) * C], want, rtol=1e-4, atol=1e-5)

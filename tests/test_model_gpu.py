@@ -319,3 +319,41 @@ def test_logged_norms_are_per_step(golden):
         norms.append(opt.last_norm)
     for s, n in enumerate(norms):
         assert abs(n.item() - float(g["gnorm%d" % s])) < 1e-4 * float(g["gnorm%d" % s]), s
+
+
+def test_module_level_forwards_match_reference_layers(golden):
+    """The reference's layer classes run on their own (model.py:110-208): the
+    full-width encoder and decoder layers on the layers_full fixture (generated
+    by the reference's CustomTransformer*Layer, D=1024, H=16, T=128), plus
+    MultiHeadAttention's (output, None) return and the FFN, against the oracle."""
+    from neurosync_trainer_lite_amd.utils import model as M
+    from tests.golden.make_goldens_helpers import full_layer_params
+    g = golden("layers_full.npz")
+    rng = np.random.default_rng(7)
+    x = torch.tensor(rng.standard_normal((1, 128, 1024)).astype(np.float32), device=DEV)
+    mem = torch.tensor(rng.standard_normal((1, 128, 1024)).astype(np.float32), device=DEV)
+    pe, pd_ = full_layer_params()
+    enc = M.CustomTransformerEncoderLayer(1024, 16, 0.0).to(DEV)
+    dec = M.CustomTransformerDecoderLayer(1024, 16, 0.0).to(DEV)
+    enc.load_state_dict({k[2:]: v for k, v in pe.items()})
+    dec.load_state_dict({k[2:]: v for k, v in pd_.items()})
+    enc.eval()
+    dec.eval()
+    with torch.no_grad():
+        ye = enc(x).cpu().numpy()[0]
+        yd = dec(x, mem).cpu().numpy()[0]
+        np.testing.assert_allclose(ye[::17], g["enc_rows"], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(yd[::17], g["dec_rows"], rtol=1e-4, atol=1e-4)
+        out, w = enc.self_attn(x, x, x)
+        ref = model_ref.attention({"a." + k[len("self_attn."):]: v for k, v in
+                                   {kk[2:]: vv for kk, vv in pe.items()}.items() if k.startswith("self_attn.")},
+                                  "a", x.cpu(), x.cpu(), 16)
+        assert w is None and rel(out, ref) < 1e-5
+        f = enc.ffn(x)
+        fref = model_ref.ffn({"f." + k[len("ffn."):]: v for k, v in
+                              {kk[2:]: vv for kk, vv in pe.items()}.items() if k.startswith("ffn.")}, "f", x.cpu())
+        assert rel(f, fref) < 1e-5
+    enc.train()
+    enc.ffn.dropout.p = 0.3
+    with pytest.raises(RuntimeError, match="inference-only"), torch.no_grad():
+        enc(x)
