@@ -147,6 +147,13 @@ NSTL_DEV void gload_frag<float>(f32x8& f, const float* row, int k0) {
   f = (f32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// four consecutive elements of a row: one 8-byte (bf16) / 16-byte (f32) store
+template <typename T> NSTL_DEV void store4(T* dst, const f32x4& v);
+template <> NSTL_DEV void store4<bf16>(bf16* dst, const f32x4& v) {
+  *(bf16x4*)dst = (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+}
+template <> NSTL_DEV void store4<float>(float* dst, const f32x4& v) { *(f32x4*)dst = v; }
+
 // A wave's 16 x 64 result tile (lane: rows 4g+r, column dt*16 + (lane&15)) to
 // global memory through the wave's LDS scratch: element writes into a dense
 // [16][64] image, then 16-byte row chunks (2-byte scattered stores write
@@ -191,7 +198,6 @@ __global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void at
   constexpr int nkt = NKT;
   char* Kimg = smem;
   char* Vimg = Kimg + T_ * RBK;
-  char* Ostage = Vimg + T_ * RBK;  // [NW][16][RBK]
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -248,58 +254,54 @@ __global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void at
   sum += __shfl_xor(sum, 16);
   sum += __shfl_xor(sum, 32);
   if (p.thresh) {
-    // dropout on P: keys (r, r+1) of this lane's query share one hash
+    // dropout on P: keys (r, r+1) of this lane's query share one hash.  The keep
+    // compare is an SGPR lane mask already -- the ballot of (kt, r) -- and lane
+    // kt*4 + r takes it by v_writelane (the select-by-lane-index form cost ~7
+    // vector instructions per ballot).
     const int q = q0 + c;
+    const uint64_t row = drop_idx(bh, T_, q, 4 * g);
     uint32_t mlo = 0, mhi = 0;  // lane kt*4 + r: keep bits of (kt, r)
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       if (kt < nkt) {
-        bool k[4];
-        const uint64_t idx = drop_idx(bh, T_, q, kt * 16 + 4 * g);
-        nstl_keep2(p.seed, idx, p.thresh, k[0], k[1]);
-        nstl_keep2(p.seed, idx + 2, p.thresh, k[2], k[3]);
+        const uint32_t h0 = nstl_pair_hash(p.seed, row + kt * 16), h1 = nstl_pair_hash(p.seed, row + kt * 16 + 2);
+        const bool k[4] = {(h0 & 0xFFFFu) >= p.thresh, (h0 >> 16) >= p.thresh, (h1 & 0xFFFFu) >= p.thresh,
+                           (h1 >> 16) >= p.thresh};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[kt][r] = k[r] ? s[kt][r] : 0.f;  // 1/(1-p): in the normalisation
-        if (p.mask) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {  // lane kt*4 + r takes the wave's ballot of (kt, r)
-            const uint64_t bal = __ballot(k[r]);
-            if (lane == kt * 4 + r) {
-              mlo = (uint32_t)bal;
-              mhi = (uint32_t)(bal >> 32);
-            }
-          }
+        for (int r = 0; r < 4; ++r) {
+          s[kt][r] = k[r] ? s[kt][r] : 0.f;  // 1/(1-p): in the normalisation
+          // in the compare's own block: the ballot IS its SGPR mask (under a branch
+          // the compiler rebuilds the mask from a materialised bool)
+          const uint64_t bal = __builtin_amdgcn_ballot_w64(k[r]);
+          mlo = nstl_writelane_i32((int)(uint32_t)bal, kt * 4 + r, (int)mlo);
+          mhi = nstl_writelane_i32((int)(uint32_t)(bal >> 32), kt * 4 + r, (int)mhi);
         }
       }
     }
     if (p.mask && lane < nkt * 4) p.mask[mask_word(bh, nkt, q0 >> 4, 0, 0) + lane] = ((uint64_t)mhi << 32) | mlo;
   }
-  // O = P V over 32-key chunks: o[dt][r] = O(query q0 + 4g + r, d = 16dt + c)
+  // O^T = V^T P^T over 32-key chunks (V^T the A operand, the score registers
+  // the B operand): o[dt][r] = O(query q0 + c, d = 16dt + 4g + r), so a lane
+  // holds 4 consecutive dims of ITS query, whose softmax sum it already has, and
+  // stores them straight from registers (no LDS round trip).
   f32x4 o[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < NKT / 2; ++j) {
-    {
-      const Frag fp = acc_frag<T>(s[2 * j], s[2 * j + 1]);
+    const Frag fp = acc_frag<T>(s[2 * j], s[2 * j + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        Frag fv;
-        frag_col2<Img>(fv, Vimg, dt * 16, 32 * j, lane);
-        mma16(o[dt], fp, fv);
-      }
+    for (int dt = 0; dt < 4; ++dt) {
+      Frag fv;
+      frag_col2<Img>(fv, Vimg, dt * 16, 32 * j, lane);
+      mma16(o[dt], fv, fp);
     }
   }
-  // normalise (query 4g + r's sum is in lane 4g + r) and store 16-byte rows
-  float ov[4][4];
-  const float keep_scale = p.thresh ? p.inv_keep : 1.f;  // dropout's 1/(1-p), applied to O instead of P
+  // normalise (dropout's 1/(1-p) applied to O instead of P) and store
+  const float inv = (p.thresh ? p.inv_keep : 1.f) * __builtin_amdgcn_rcpf(sum);
+  T* orow = (T*)p.o + (tok0 + q0 + c) * p.o_ld + h * DH + 4 * g;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float inv = keep_scale / __shfl(sum, 4 * g + r);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) ov[dt][r] = o[dt][r] * inv;
-  }
-  store_tile16x64<T>(ov, Ostage + w * 16 * RBK, p.o + ((tok0 + q0) * p.o_ld + h * DH) * ESZ, p.o_ld, lane);
+  for (int dt = 0; dt < 4; ++dt) store4<T>(orow + 16 * dt, o[dt] * inv);
   if (g == 0) p.lse[(int64_t)bh * T_ + q0 + c] = m * p.scale + logf(sum);
 }
 
@@ -908,8 +910,8 @@ static_assert(FUSED_ARRIVED_OFF >= 3 * FUSED_MAX_T * DH * 2 + 2 * FUSED_MAX_T * 
 static_assert(FUSED_ROPE_OFF % 16 == 0, "16-byte table chunks");
 static_assert(8 * 16 * DH * 2 + 3 * 8 * 64 * 4 <= 3 * FUSED_MAX_T * DH * 2, "staging must fit in the images");
 
-size_t fwd_lds_bytes(int T, int esz) {  // K, V images + per-wave output staging
-  return (size_t)2 * T * DH * esz + (FWD_NT / 64) * 16 * DH * (size_t)esz;
+size_t fwd_lds_bytes(int T, int esz) {  // K, V images (the output leaves from registers)
+  return (size_t)2 * T * DH * esz;
 }
 size_t bwd_lds_bytes(int T, int esz) {  // either backward kernel (+ 2 x [8][64] f32 bias partials + counter)
   return (size_t)2 * T * DH * esz + 2 * T * 4 + (BWD_NT / 64) * 16 * DH * (size_t)esz + 2 * (BWD_NT / 64) * 64 * 4 +

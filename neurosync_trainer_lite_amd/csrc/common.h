@@ -160,6 +160,11 @@ static inline uint32_t nstl_drop_thresh(float p) {
   return (uint32_t)t;
 }
 
+// v_writelane_b32 through the LLVM intrinsic (hipcc exposes no clang builtin for
+// it): lane `lane` of `old` takes the wave-uniform `val`; the backend inserts the
+// VALU-writes-SGPR -> v_writelane wait states (inline asm would not)
+__device__ int nstl_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 // wave-level reductions (64 lanes)
 NSTL_DEV float wave_sum(float v) {
 #pragma unroll
