@@ -131,11 +131,13 @@ def data_feed(cfg, args, step_fn, dev, rank, world):
     include_fast + include_slow -> GPU feature extraction -> windows), batches
     fetched whole into pinned host memory and copied with non_blocking H2D into
     the same train step; rank r of n takes batches r, r+n, ... (rank_batches)."""
+    import contextlib
     import tempfile
     from neurosync_trainer_lite_amd.dataset.dataset import prepare_dataloader_with_split
     from neurosync_trainer_lite_amd.utils.training_utils import rank_batches
     t0 = time.perf_counter()
-    with tempfile.TemporaryDirectory(prefix="nstl_c4_%d_" % rank) as root:
+    # the data path prints its progress as the reference does: keep stdout for the JSON line
+    with tempfile.TemporaryDirectory(prefix="nstl_c4_%d_" % rank) as root, contextlib.redirect_stdout(sys.stderr):
         synth_corpus(root, args.feed_clips, args.feed_seconds, seed=0)
         c = dict(cfg, root_dir=root, include_fast=True, include_slow=True)
         torch.manual_seed(4321)  # the same split and order on every rank

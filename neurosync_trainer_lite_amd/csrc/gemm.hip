@@ -781,7 +781,8 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
           }
         }
         char* dst = C + ((int64_t)i * ldc + j) * ESZ;
-        if (vec) {
+        if (p.debug_skip_epilogue == 2) {  // NSTL_GEMM_DEBUG=skip_store: timing experiments only
+        } else if (vec) {
           if (ESZ == 4)
             *(f32x4*)dst = (f32x4){v[0], v[1 % CW], v[2 % CW], v[3 % CW]};
           else
