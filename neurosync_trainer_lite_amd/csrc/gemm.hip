@@ -15,6 +15,8 @@
 #include <stdlib.h>
 
 #include "../../include/nstl.h"
+#include <map>
+#include <mutex>
 #include <string>
 
 #include "common.h"
@@ -846,10 +848,37 @@ NSTL_DEV void ring_epi_generic(const GemmParams& p, const f32x4 (&acc)[8][4], in
 constexpr int R_SMEM = R_STAGES * R_SLOT;
 static_assert(8 * RING_EPI_WAVE <= R_SMEM, "epilogue scratch must fit in the ring");
 
+// Diagnostic build only (make stamps -> libnstl_hip_stamps.so, tools/gemm_timeline.py):
+// wave 0 of every ring-GEMM workgroup records the global 100 MHz clock at tile
+// entry, after the prologue, after the K loop and after its epilogue stores have
+// retired, plus where it ran (HW_ID, XCC_ID).  No product build executes a stamp.
+#ifdef NSTL_STAMPS
+constexpr int STAMP_MAX = 1 << 16, STAMP_W = 8;
+__device__ unsigned long long g_nstl_stamps[STAMP_MAX * STAMP_W];
+NSTL_DEV unsigned long long rt_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define NSTL_STAMP(var) const unsigned long long var = rt_stamp()
+#else
+#define NSTL_STAMP(var)
+#endif
+
 // One 256 x 256 output tile of p: `id` is the tile's linear index in p's grid
 // (already XCD-remapped by the caller), `kz` its split-K chunk.
+// Flags of a persistent kernel's split tile (RT_*): the first piece of a tile
+// leaves its f32 accumulators in the workgroup's private slot `part` (lane-
+// linear: register g of thread t at part[g * 512 + t], 1 KB per wave store)
+// instead of an epilogue; the second piece starts from them.
+enum { RT_RESTORE = 1, RT_SAVE = 2 };
+
 template <bool AK, bool BKM, int EM>
-NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
+NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz0, int kz1, char* smem, int flags = 0,
+                        f32x4* part = nullptr) {
+  NSTL_STAMP(st_entry);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -863,13 +892,15 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
   const int in_g = id % per_group;
   const int tm = first_m + in_g % gm, tn = in_g / gm;
   const int m0 = tm * BIG, n0 = tn * BIG;
-  const int kz0 = kz * p.k_chunk;
-  const int kz1 = min(p.K, kz0 + p.k_chunk);
   const int nk = (kz1 - kz0) / R_BK;
   const uint32_t smem_u32 = lds_u32(smem);
   const RingSrc rs = ring_src<AK, BKM>(p, m0, n0, wave, lane);
 
   f32x4 acc[8][4];
+  // the parked slot through a buffer descriptor: one lane offset (tid * 16) and
+  // a scalar offset per register (global immediates reach only +-4 KB)
+  __amdgpu_buffer_rsrc_t prs;
+  if (flags) prs = __builtin_amdgcn_make_buffer_rsrc(part, 0, BIG * BIG * 4, 0x00020000);
 #pragma unroll
   for (int a = 0; a < 8; ++a)
 #pragma unroll
@@ -883,6 +914,7 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
   else if (nk == 2) NSTL_VMCNT(4);
   else NSTL_VMCNT(0);
   __builtin_amdgcn_s_barrier();
+  NSTL_STAMP(st_prologue);
   if (wm == 1) __builtin_amdgcn_s_barrier();  // the stagger
 
   // Branch-free steps (as the fp8 kernel): in the main loop both groups wait
@@ -945,25 +977,101 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz, char* smem) {
     for (int kt = 0; kt < nk; ++kt) step(kt, false, -1);
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger
-  if (p.debug_skip_epilogue == 1) {  // timing experiments only (NSTL_GEMM_DEBUG=skip_epi)
+  NSTL_STAMP(st_kloop);
+  if (flags & RT_RESTORE) {
+    // add the parked first piece (acc = second + first: f32 rounding differs
+    // from one chain by ~1 ulp).  Loaded one 16-VGPR group ahead: acc starting
+    // from the slot would keep 128 more VGPRs live through the prologue (spills).
+    f32x4 nx[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      nx[b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, tid * 16, b * BIG_NT * 16, 0));
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      f32x4 cur[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) cur[b] = nx[b];
+      if (a + 1 < 8) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          nx[b] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, tid * 16, ((a + 1) * 4 + b) * BIG_NT * 16, 0));
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] += cur[b];
+    }
+  }
+  if (flags & RT_SAVE) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, acc[a][b]), prs, tid * 16,
+                                               (a * 4 + b) * BIG_NT * 16, 0);
+  } else if (p.debug_skip_epilogue == 1) {  // timing experiments only (NSTL_GEMM_DEBUG=skip_epi)
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(acc[a][b]));
-    return;
+  } else {
+    __syncthreads();  // every wave is done with the ring: it becomes scratch
+    char* scr = smem + wave * RING_EPI_WAVE;
+    const int row0 = m0 + wm * 128, col0 = n0 + wn * 64;
+    if (EM == EM_GENERIC) ring_epi_generic(p, acc, row0, col0, lane, scr);
+    else ring_epi<EM, false>(p, acc, row0, col0, lane, scr);
   }
-  __syncthreads();  // every wave is done with the ring: it becomes scratch
-  char* scr = smem + wave * RING_EPI_WAVE;
-  const int row0 = m0 + wm * 128, col0 = n0 + wn * 64;
-  if (EM == EM_GENERIC) ring_epi_generic(p, acc, row0, col0, lane, scr);
-  else ring_epi<EM, false>(p, acc, row0, col0, lane, scr);
+#ifdef NSTL_STAMPS
+  NSTL_VMCNT(0);
+  NSTL_STAMP(st_epi);
+  if (wave == 0 && lane == 0) {
+    // slot: tile id (+ 2^15 for the second piece of a split tile)
+    const int slot = (id + blockIdx.y * gridDim.x + (kz0 > 0 && blockIdx.y == 0 ? 32768 : 0)) % STAMP_MAX;
+    unsigned long long* s = g_nstl_stamps + (int64_t)slot * STAMP_W;
+    s[0] = st_entry; s[1] = st_prologue; s[2] = st_kloop; s[3] = st_epi;
+    s[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    s[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    s[6] = id | ((unsigned long long)flags << 32); s[7] = nk;
+  }
+#endif
 }
 
 template <bool AK, bool BKM, int EM>
 __global__ __launch_bounds__(BIG_NT, 1) void gemm256r_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[R_SMEM];
   const int nt = ((p.M + BIG - 1) / BIG) * ((p.N + BIG - 1) / BIG);
-  ring_tile<AK, BKM, EM>(p, xcd_remap(blockIdx.x, nt), blockIdx.y, smem);
+  const int kb = blockIdx.y * p.k_chunk;
+  ring_tile<AK, BKM, EM>(p, xcd_remap(blockIdx.x, nt), kb, min(p.K, kb + p.k_chunk), smem);
+}
+
+// Persistent form for multi-round problems (tiles = rounds x gridDim.x): workgroup
+// w runs the tiles of blocks w, w + G, w + 2G, ... of the one-shot grid (same
+// XCD-aware tile order).  In the one-shot grid every CU finishes a round at the
+// same moment, so all 256 write their 32 MB of output at once (HBM-bound, the
+// MFMAs idle) and then wait for the next round's dispatch.  Here the eight XCDs
+// run out of phase: on XCD x (read from XCC_ID; placement only affects speed)
+// the first tile is cut at K-step x*nk/8, its first piece parked in the
+// workgroup's private f32 slot and finished last, so XCD x's tile boundaries
+// (epilogue bursts, prologue fills) fall x/8 of a tile later than XCD 0's.
+template <bool AK, bool BKM, int EM>
+__global__ __launch_bounds__(BIG_NT, 1) void gemm256p_kernel(GemmParams p, int rounds, f32x4* parts) {
+  __shared__ __attribute__((aligned(16))) char smem[R_SMEM];
+  const int G = gridDim.x, w = blockIdx.x;
+  const int nt = rounds * G;
+  const int nk = p.K / R_BK;
+  const int xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7;
+  const int cut = p.debug_skip_epilogue == 3 ? 0 : ((xcc * nk) >> 3) * R_BK;  // K index of the cut (0: none)
+  f32x4* part = parts + (int64_t)w * (BIG * BIG / 4);
+  // segments: [tile 0 to the cut, parked] tiles 1..rounds-1 [tile 0 from the cut]
+  // (one ring_tile call site: inlining it per segment kind spills registers)
+  const int nseg = rounds + (cut > 0 ? 1 : 0);
+  for (int sg = 0; sg < nseg; ++sg) {
+    const int j = sg < rounds ? sg : 0;
+    int kb = 0, ke = p.K, flags = 0;
+    if (cut > 0 && sg == 0) { ke = cut; flags = RT_SAVE; }
+    if (cut > 0 && sg == rounds) { kb = cut; flags = RT_RESTORE; }
+    if (sg > 0) __syncthreads();  // the previous tile's epilogue scratch is free
+    ring_tile<AK, BKM, EM>(p, xcd_remap(w + j * G, nt), kb, ke, smem, flags, part);
+  }
 }
 
 // Grouped launch: independent problems of one kind back to back in one grid
@@ -982,7 +1090,8 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm256r_group_kernel(GroupParams g
   const int gid = xcd_remap(blockIdx.x, gp.tile_end[gp.n - 1]);
   int g = 0;
   while (g + 1 < gp.n && gid >= gp.tile_end[g]) ++g;
-  ring_tile<AK, BKM, EM>(gp.g[g], gid - (g > 0 ? gp.tile_end[g - 1] : 0), 0, smem);
+  const GemmParams& p = gp.g[g];
+  ring_tile<AK, BKM, EM>(p, gid - (g > 0 ? gp.tile_end[g - 1] : 0), 0, p.K, smem);
 }
 
 // ===========================================================================
@@ -1206,11 +1315,81 @@ bool getenv_ring() {
   return v != 0;
 }
 
+// NSTL_GEMM_PERSIST=1 runs multi-round problems on the persistent XCD-phased
+// kernel (off: measured slower, DESIGN.md section 4 "Persistent, XCD-phased")
+bool getenv_persist() {
+  static const int v = [] {
+    const char* e = getenv("NSTL_GEMM_PERSIST");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v != 0;
+}
+
+// CUs of the current device (the persistent grid: one workgroup per CU)
+int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// the persistent kernel's split-tile slots: one 256 KB f32 slot per workgroup,
+// owned by the library per (device, stream) so launches on different streams
+// never share one
+f32x4* persist_slots(hipStream_t st, int G) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<f32x4*, int>> slots;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = slots[{dev, st}];
+  if (e.second < G) {
+    if (e.first) (void)hipFree(e.first);
+    e.first = nullptr;
+    e.second = 0;
+    if (hipMalloc((void**)&e.first, (size_t)G * BIG * BIG * sizeof(float)) != hipSuccess) return nullptr;
+    e.second = G;
+  }
+  return e.first;
+}
+
+template <bool AK, bool BKM>
+void launch_persist_em(int em, int G, int rounds, hipStream_t st, const GemmParams& p, f32x4* parts) {
+  dim3 grid(G), block(BIG_NT);
+  switch (em) {
+    case EM_BF16: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_BF16>), grid, block, 0, st, p, rounds, parts); break;
+    case EM_RELU_DROP: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_RELU_DROP>), grid, block, 0, st, p, rounds, parts); break;
+    case EM_ROPE: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_ROPE>), grid, block, 0, st, p, rounds, parts); break;
+    case EM_DRELU: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_DRELU>), grid, block, 0, st, p, rounds, parts); break;
+    default: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_F32>), grid, block, 0, st, p, rounds, parts); break;
+  }
+}
+
 int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t st) {
   const int nt = ((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
   dim3 grid(nt, splits), block(BIG_NT);
   if (getenv_ring()) {
     const int em = ring_epi_mode(a, p);
+    // multi-round problems with a lean epilogue: the persistent XCD-phased kernel
+    const int G = device_cus();
+    const bool lean = em == EM_BF16 || em == EM_RELU_DROP || em == EM_ROPE || em == EM_DRELU || em == EM_F32;
+    if (getenv_persist() && splits == 1 && lean && (a->a_kmajor || !a->b_kmajor) && G > 0 && nt % G == 0 &&
+        nt / G >= 2 && a->K % (8 * R_BK) == 0) {
+      f32x4* parts = persist_slots(st, G);
+      NSTL_CHECK_ARG(parts != nullptr, "nstl_gemm: persistent slot allocation failed");
+      if (a->a_kmajor && a->b_kmajor) launch_persist_em<true, true>(em, G, nt / G, st, p, parts);
+      else if (a->a_kmajor) launch_persist_em<true, false>(em, G, nt / G, st, p, parts);
+      else launch_persist_em<false, false>(em, G, nt / G, st, p, parts);
+      NSTL_LAUNCH_CHECK("nstl_gemm (256 persistent)");
+      nstl::count(NSTL_K_GEMM_RING);
+      nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt);
+      return 0;
+    }
     if (a->a_kmajor && a->b_kmajor) launch_ring_em<true, true>(em, grid, block, st, p);
     else if (a->a_kmajor && !a->b_kmajor) launch_ring_em<true, false>(em, grid, block, st, p);
     else if (!a->a_kmajor && !a->b_kmajor) launch_ring_em<false, false>(em, grid, block, st, p);
@@ -1253,7 +1432,7 @@ int launch_typed(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t
 int getenv_debug_skip_epi() {
   static const int v = [] {
     const char* e = getenv("NSTL_GEMM_DEBUG");
-    return !e ? 0 : std::string(e) == "skip_epi" ? 1 : std::string(e) == "skip_store" ? 2 : 0;
+    return !e ? 0 : std::string(e) == "skip_epi" ? 1 : std::string(e) == "skip_store" ? 2 : std::string(e) == "nocut" ? 3 : 0;
   }();
   return v;
 }
@@ -1463,3 +1642,16 @@ extern "C" int64_t nstl_gemm_relu_mask_words(const nstl_gemm_args* a) {
   if (em != EM_RELU_DROP && em != EM_DRELU) return 0;
   return (int64_t)((a->M + 63) / 64) * 8 * ((a->N + 7) / 8);
 }
+
+#ifdef NSTL_STAMPS
+// diagnostic build only (not declared in include/nstl.h): copy / clear the stamps
+extern "C" int nstl_debug_gemm_stamps(unsigned long long* host, int64_t n) {
+  n = std::min<int64_t>(n, (int64_t)STAMP_MAX * STAMP_W);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_nstl_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+extern "C" int nstl_debug_gemm_stamps_clear() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_nstl_stamps)) != hipSuccess) return 1;
+  return hipMemset(p, 0, sizeof(unsigned long long) * STAMP_MAX * STAMP_W) == hipSuccess ? 0 : 1;
+}
+#endif
