@@ -47,20 +47,58 @@ def frames_flops(W, T, D, n_attn=24):
     return 6 * W + 12 * T * D * n_attn
 
 
-def gemm_traffic():
-    """Per-launch HBM bytes of the GEMM family from the committed PMC summary
-    (tools/run_pmc_traffic.sh -> profiles/*_gemm_traffic.json), or None."""
+def _pmc_per_dispatch(d, counter):
+    """{dispatch id: summed counter} over the bf16 GEMM-family dispatches of a
+    rocprofv3 --output-format csv counter run."""
+    import csv
     import glob
-    import re
+    vals = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"]
+            if r["Counter_Name"] != counter or "gemm" not in name or "splitk" in name or "f8" in name:
+                continue
+            k = int(r["Dispatch_Id"])
+            vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
+    return vals
 
-    def version(f):  # r1_v10 after r1_v9 (natural order); untagged files first
-        m = re.search(r"r(\d+)_v(\d+)_gemm_traffic", os.path.basename(f))
-        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_gemm_traffic.json")), key=version)
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], HERE)
+
+def measure_gemm_traffic(args):
+    """HBM bytes per GEMM-family launch, measured on this box in this run: two
+    rocprofv3 counter passes (FETCH_SIZE, WRITE_SIZE: separate passes, as
+    MI355X_MICROARCH.md prescribes) over a child run of this same bench (1
+    warm-up + 1 step of the same workload), started before this process touches
+    the GPU.  bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950 FETCH_SIZE
+    counts streaming reads at half their bytes).  Returns (bytes, note)."""
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, "rocprofv3 absent: traffic not measured"
+    kib = {}
+    t0 = time.perf_counter()
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="nstl_pmc_", dir="/tmp")
+        cmd = ["timeout", "-s", "KILL", "240", exe, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv",
+               "--", sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+               "--no-parity", "--feature-steps", "0", "--feed-steps", "0", "--no-traffic",
+               "--batch", str(args.batch), "--seq", str(args.seq)]
+        env = dict(os.environ, TMPDIR="/tmp")
+        log("traffic: rocprofv3 --pmc %s pass (child bench, 1+1 steps)" % counter)
+        r = subprocess.run(cmd, env=env, cwd="/tmp", stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        if r.returncode != 0:
+            log("traffic: %s pass failed (rc %d): %s" % (counter, r.returncode, r.stderr[-400:]))
+            return None, "rocprofv3 %s pass failed (rc %d): traffic not measured" % (counter, r.returncode)
+        v = _pmc_per_dispatch(d, counter)
+        shutil.rmtree(d, ignore_errors=True)
+        if not v:
+            return None, "rocprofv3 %s pass recorded no GEMM dispatch: traffic not measured" % counter
+        kib[counter] = sum(v.values()) / len(v)
+    log("traffic: both passes in %.1fs" % (time.perf_counter() - t0))
+    return (round((2.0 * kib["FETCH_SIZE"] + kib["WRITE_SIZE"]) * 1024.0),
+            "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 1+1-step child run of "
+            "this workload, mean over its bf16 GEMM-family dispatches")
 
 
 def cpu_baseline(cfg, T, budget_s=20.0):
@@ -231,6 +269,8 @@ def main():
                          "the DataLoader with pinned non_blocking H2D); 0 = skip")
     ap.add_argument("--feed-clips", type=int, default=16)
     ap.add_argument("--feed-seconds", type=float, default=60.0)
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the rocprofv3 counter passes that measure the GEMM family's HBM traffic")
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE config C5: q/k/v + FFN forward GEMMs on e4m3 operands (row-wise scales); "
                          "C5 also doubles the clip length: --seq 256 --batch 64")
@@ -241,6 +281,10 @@ def main():
     from neurosync_trainer_lite_amd.config import training_config
     from neurosync_trainer_lite_amd.utils.model_utils import build_model, prepare_training_components
 
+    # PMC traffic passes first: child processes, started before this one touches the GPU
+    traffic, traffic_src = None, "skipped (--no-traffic or n>1)"
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_traffic:
+        traffic, traffic_src = measure_gemm_traffic(args)
     rank, world, local = parallel.init_from_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -342,7 +386,6 @@ def main():
     gemm_ms = sum(a.elapsed_time(b) for a, b, _, _, _ in ev16)
     gemm_flops = sum(f for _, _, f, _, _ in ev16)
     gemm_alg_bytes = sum(x for _, _, _, x, _ in ev16) / max(1, len(ev16))
-    traffic, traffic_src = gemm_traffic()
     n_launch = len(ev16)
     fp8_roof = None
     if ev8:
@@ -436,6 +479,8 @@ def main():
                          "achieved": round(achieved_tf, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)",
+                         "traffic_vs_algorithmic": (round(traffic / gemm_alg_bytes, 3) if traffic and gemm_alg_bytes
+                                                    else None),
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": round(gemm_alg_bytes),
                          "launches": n_launch, "avg_launch_us": round(gemm_ms * 1e3 / max(1, n_launch), 2),

@@ -7,7 +7,7 @@ OLD=$GRAFT_REPO_ROOT/neurosync_trainer_lite_amd/libnstl_hip_old.so
 for i in $(seq 1 $REPS); do
   for arm in new old; do
     if [ $arm = old ]; then export NSTL_LIB_PATH=$OLD; else unset NSTL_LIB_PATH; fi
-    timeout -k 10 300 python bench.py --no-cpu-baseline --no-parity --feature-steps 0 --feed-steps 0 --steps 30 2>gpurun_out/ab_lib_$arm.err \
+    timeout -k 10 300 python bench.py --no-traffic --no-cpu-baseline --no-parity --feature-steps 0 --feed-steps 0 --steps 30 2>gpurun_out/ab_lib_$arm.err \
       | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$arm', d['value'], d['ms_per_step'], d['roofline']['achieved'])" || exit 1
   done
 done

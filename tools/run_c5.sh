@@ -9,7 +9,7 @@ for shape in "--seq 256 --batch 64" "--seq 128 --batch 128"; do
   s=$(echo $shape | awk '{print "t"$2}')
   for mode in bf16 fp8 bf16 fp8; do
     flag=""; [ $mode = fp8 ] && flag="--fp8"
-    timeout -k 10 300 python bench.py $flag $shape --no-cpu-baseline --feature-steps 0 > gpurun_out/${TAG}_${mode}_$s.json 2> gpurun_out/${TAG}_${mode}_$s.err || { tail -5 gpurun_out/${TAG}_${mode}_$s.err; exit 1; }
+    timeout -k 10 300 python bench.py --no-traffic $flag $shape --no-cpu-baseline --feature-steps 0 > gpurun_out/${TAG}_${mode}_$s.json 2> gpurun_out/${TAG}_${mode}_$s.err || { tail -5 gpurun_out/${TAG}_${mode}_$s.err; exit 1; }
     python -c "import json; d=json.load(open('gpurun_out/${TAG}_${mode}_$s.json')); p=d.get('parity',{}); print('$mode', '$s', d['value'], d['ms_per_step'], 'mse_fp8', p.get('mse_fp8'), 'pass', p.get('pass'))"
   done
 done

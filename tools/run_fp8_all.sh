@@ -9,7 +9,7 @@ cat gpurun_out/${TAG}_micro.txt
 for i in 1 2; do
   for mode in bf16 fp8; do
     flag=""; [ $mode = fp8 ] && flag="--fp8"
-    timeout -k 10 200 python bench.py $flag --no-cpu-baseline --no-parity --feature-steps 0 > gpurun_out/${TAG}_${mode}_$i.json 2>/dev/null || exit 1
+    timeout -k 10 200 python bench.py --no-traffic $flag --no-cpu-baseline --no-parity --feature-steps 0 > gpurun_out/${TAG}_${mode}_$i.json 2>/dev/null || exit 1
     python -c "import json; d=json.load(open('gpurun_out/${TAG}_${mode}_$i.json')); print('$mode', $i, d['value'], d['ms_per_step'])"
   done
 done
