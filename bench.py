@@ -306,6 +306,10 @@ def main():
     src = torch.randn(B, T, cfg["input_dim"], device=dev, generator=g)
     trg = torch.randn(B, T, cfg["output_dim"], device=dev, generator=g) * 20
 
+    # as train_one_epoch sets it: the loop's next use of the parameters is its
+    # forward, so FusedAdam runs its update under that forward (same results)
+    opt.overlap_next_forward = world == 1
+
     def step(x=src, y=trg):
         opt.zero_grad()
         loss = crit(model(x), y)

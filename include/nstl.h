@@ -235,8 +235,18 @@ typedef struct nstl_adam_args {
   const float* sumsq_partial; int n_partial;   /* NULL: no clipping */
   float max_norm;
   float* norm_out;                     /* [1] pre-clip total norm, may be NULL */
+  const float* coef;                   /* device [1] clip coefficient from nstl_clip_coef, or NULL;
+                                          exclusive with sumsq_partial.  The kernel then uses no LDS,
+                                          so a range update can share CUs with a ring GEMM */
 } nstl_adam_args;
 int nstl_adam_step(const nstl_adam_args* args, void* stream);
+
+/* clip_grad_norm_'s coefficient min(1, max_norm / (norm + 1e-6)) from nstl_sumsq
+ * partials, into coef_out[0] (and the pre-clip norm into norm_out[0] when
+ * non-NULL): the form nstl_adam_step's coef reads when the update runs in
+ * several arena ranges (utils/training_utils.py:73-74). */
+int nstl_clip_coef(const float* partial, int n_partial, float max_norm, float* coef_out, float* norm_out,
+                   void* stream);
 
 /* 2-D strided copy with conversion: dst[i][j] = scale * src[i][j] for j < cols,
  * 0 for cols <= j < dst_cols (zero padding).  scale: device f32 scalar or NULL (1). */

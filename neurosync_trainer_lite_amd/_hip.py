@@ -91,6 +91,7 @@ class AdamArgs(ctypes.Structure):
         ("p_lowp", _vp), ("lowp_dtype", _i32), ("n", _i64),
         ("lr", _f32), ("beta1", _f32), ("beta2", _f32), ("eps", _f32), ("weight_decay", _f32),
         ("step", _i32), ("sumsq_partial", _vp), ("n_partial", _i32), ("max_norm", _f32), ("norm_out", _vp),
+        ("coef", _vp),
     ]
 
 
@@ -107,7 +108,7 @@ EXPORTS = [
     "nstl_attn_fwd", "nstl_attn_bwd", "nstl_attn_bias_rows", "nstl_ln_fwd", "nstl_ln_bwd",
     "nstl_reduce_rows", "nstl_reduce_rows_strided", "nstl_reduce_rows3", "nstl_reduce_rows_batch",
     "nstl_colsum", "nstl_rope",
-    "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
+    "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_clip_coef", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
     "nstl_features", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
     "nstl_version", "nstl_fp8_quant_rows", "nstl_kernel_counts", "nstl_kernel_counts_reset",
     "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs",
@@ -155,6 +156,7 @@ def lib():
         L.nstl_loss_fwd_bwd.argtypes = [P(LossArgs), _vp]
         L.nstl_sumsq.argtypes = [_vp, _i64, _vp, _i32, _vp]
         L.nstl_adam_step.argtypes = [P(AdamArgs), _vp]
+        L.nstl_clip_coef.argtypes = [_vp, _i32, _f32, _vp, _vp, _vp]
         L.nstl_cast.argtypes = [_i32, _vp, _i32, _vp, _i64, _vp]
         L.nstl_copy2d.argtypes = [_i32, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp]
         L.nstl_autocorr.argtypes = [_vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp]
@@ -392,6 +394,12 @@ def loss_fwd_bwd(a, stream=None):
 def sumsq(g, n, partial, n_partial, stream=None):
     check(lib().nstl_sumsq(g.data_ptr(), n, partial.data_ptr(), n_partial,
                            stream if stream is not None else stream_of()), "nstl_sumsq")
+
+
+def clip_coef(partial, n_partial, max_norm, coef, norm_out=None, stream=None):
+    check(lib().nstl_clip_coef(partial.data_ptr(), n_partial, float(max_norm), coef.data_ptr(),
+                               norm_out.data_ptr() if norm_out is not None else None,
+                               stream if stream is not None else stream_of()), "nstl_clip_coef")
 
 
 def adam_step(a, stream=None):

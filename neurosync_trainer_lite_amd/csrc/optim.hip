@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // Optimizer + small memory-bound kernels over flat f32 arenas.
 //   nstl_sumsq      : stage 1 of the global grad norm (clip_grad_norm_, utils/training_utils.py:73)
 //   nstl_adam_step  : clip coefficient + Adam with coupled L2 (torch.optim.Adam(weight_decay),
@@ -53,6 +54,7 @@ struct AdamParams {
   int64_t n;
   float lr, b1, b2, eps, wd, step_size, bc2_sqrt;
   const float* part; int n_part; float max_norm; float* norm_out;
+  const float* coef;  // precomputed clip coefficient (adam_gcoef_kernel)
 };
 
 NSTL_DEV void adam_elem(const AdamParams& a, float coef, int64_t i) {
@@ -74,27 +76,50 @@ NSTL_DEV void adam_elem(const AdamParams& a, float coef, int64_t i) {
   }
 }
 
+// clip_grad_norm_'s coefficient from the sumsq partials, by wave 0 of a block
+// (the reduction order every caller of clip_coef_wave shares)
+NSTL_DEV float clip_coef_wave(const float* part, int n_part, float max_norm, float* total_out) {
+  double s = 0;
+  for (int k = threadIdx.x; k < n_part; k += 64) s += part[k];
+  s = wave_sum_d(s);
+  const float total = (float)sqrt(s);
+  const float c = max_norm / (total + 1e-6f);
+  *total_out = total;
+  return c < 1.f ? c : 1.f;
+}
+
 __global__ __launch_bounds__(NT) void adam_kernel(AdamParams a) {
   __shared__ float coef_s;
   if (threadIdx.x < 64) {
-    double s = 0;
-    if (a.part) {
-      for (int k = threadIdx.x; k < a.n_part; k += 64) s += a.part[k];
-      s = wave_sum_d(s);
-    }
+    float coef = 1.f, total = 0.f;
+    if (a.part) coef = clip_coef_wave(a.part, a.n_part, a.max_norm, &total);
     if (threadIdx.x == 0) {
-      float coef = 1.f;
-      if (a.part) {
-        const float total = (float)sqrt(s);
-        const float c = a.max_norm / (total + 1e-6f);
-        coef = c < 1.f ? c : 1.f;
-        if (blockIdx.x == 0 && a.norm_out) a.norm_out[0] = total;
-      }
+      if (a.part && blockIdx.x == 0 && a.norm_out) a.norm_out[0] = total;
       coef_s = coef;
     }
   }
   __syncthreads();
   const float coef = coef_s;
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) adam_elem(a, coef, i);
+}
+
+// nstl_clip_coef: the coefficient (and the pre-clip norm) once, into device memory
+__global__ __launch_bounds__(64) void clip_coef_kernel(const float* part, int n_part, float max_norm, float* coef,
+                                                       float* norm_out) {
+  float total = 0.f;
+  const float c = clip_coef_wave(part, n_part, max_norm, &total);
+  if (threadIdx.x == 0) {
+    coef[0] = c;
+    if (norm_out) norm_out[0] = total;
+  }
+}
+
+// Adam with the coefficient read from device memory: no LDS, so its workgroups
+// fit on a CU beside a 160 KB ring-GEMM workgroup (the range updates that run
+// under the next forward, FusedAdam.overlap_next_forward)
+__global__ __launch_bounds__(NT) void adam_gcoef_kernel(AdamParams a) {
+  const float coef = *a.coef;
   const int64_t stride = (int64_t)gridDim.x * NT;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) adam_elem(a, coef, i);
 }
@@ -251,10 +276,30 @@ extern "C" int nstl_adam_step(const nstl_adam_args* a, void* stream) {
   p.step_size = (float)(a->lr / bc1);
   p.bc2_sqrt = (float)std::sqrt(bc2);
   p.part = a->sumsq_partial; p.n_part = a->n_partial; p.max_norm = a->max_norm; p.norm_out = a->norm_out;
+  p.coef = a->coef;
   // scalar, one element per thread and step: measured faster than 16-byte
   // vectorised forms (x1: +4 %, x2 unrolled: +4-8 %, tools/bench_adam.py)
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(a->n, 4)), dim3(NT), 0, (hipStream_t)stream, p);
+  if (a->coef) {
+    NSTL_CHECK_ARG(!a->sumsq_partial, "nstl_adam_step: coef and sumsq_partial are exclusive");
+    // NSTL_ADAM_GRID: cap on its workgroups (how many CUs a range update shares)
+    static const int cap = [] {
+      const char* e = getenv("NSTL_ADAM_GRID");
+      return e ? std::max(1, atoi(e)) : 8192;
+    }();
+    hipLaunchKernelGGL(adam_gcoef_kernel, dim3(std::min(grid_for(a->n, 4), cap)), dim3(NT), 0, (hipStream_t)stream, p);
+  } else {
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(a->n, 4)), dim3(NT), 0, (hipStream_t)stream, p);
+  }
   NSTL_LAUNCH_CHECK("nstl_adam_step");
+  return 0;
+}
+
+extern "C" int nstl_clip_coef(const float* partial, int n_partial, float max_norm, float* coef_out, float* norm_out,
+                              void* stream) {
+  NSTL_CHECK_ARG(partial && coef_out && n_partial > 0 && n_partial <= 1024, "nstl_clip_coef: bad args");
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, partial, n_partial, max_norm,
+                     coef_out, norm_out);
+  NSTL_LAUNCH_CHECK("nstl_clip_coef");
   return 0;
 }
 

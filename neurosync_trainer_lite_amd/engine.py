@@ -173,6 +173,8 @@ class Seq2SeqEngine:
         self.dh = self.D // self.H
         self.Fd = enc.transformer_encoder[0].ffn.linear1.out_features
         self.dropout = model.dropout_p
+        self._wpending = []        # (lo, hi, event): queued optimizer updates of arena ranges (queue_update)
+        self._upd_ranges = None    # [(stage key, (lo, hi))]: the update order of queue_update
         self._check_shapes()
         self._build_arena()
         self._bufs = {}
@@ -324,6 +326,7 @@ class Seq2SeqEngine:
         """Re-pack if someone replaced parameter storage (e.g. model.to())."""
         p0 = self._params[0][1]
         if p0.data_ptr() != self._first_ptr or p0.device != self.device:
+            self.sync_pending()
             with torch.no_grad():
                 for n, p in self._params:
                     o, k, shp = self.offsets[n]
@@ -340,6 +343,7 @@ class Seq2SeqEngine:
             self.refresh_shadow()
 
     def refresh_shadow(self):
+        self.sync_pending()
         if self.p16 is not self.p32:
             K.cast(self.p32, self.p16, stream=K.stream_of(self.device))
         self._versions = {n: p._version for n, p in self._params}
@@ -347,6 +351,60 @@ class Seq2SeqEngine:
     def zero_grad(self):
         """Next backward overwrites the gradient arena instead of accumulating."""
         self.grads_fresh = True
+
+    # ------------------------------------------------ deferred weight updates
+    # FusedAdam.overlap_next_forward: the optimizer's update is queued on a side
+    # stream in arena ranges -- the f32 vectors (biases, LayerNorm) first, then
+    # the matrices of each forward stage in forward order (embedding, encoder
+    # layers, decoder layers, head) -- and the next forward makes its stream wait
+    # for a stage's range just before that stage reads its weights, so the update
+    # of later layers runs under the forward of earlier ones.  Every other entry
+    # that reads or writes the arenas waits for all of it first (sync_pending).
+    def update_ranges(self):
+        if self._upd_ranges is None:
+            def rng(names):
+                return (min(self.offsets[n][0] for n in names),
+                        max(self.offsets[n][0] + _pad64(self.offsets[n][1]) for n in names))
+
+            def mats(prefix):
+                return [n for n in self.offsets if n.startswith(prefix) and len(self.offsets[n][2]) > 1]
+            st = [("vec", (self.n_shardable, self.numel)), ("emb", rng(["encoder.embedding.weight"]))]
+            st += [(("enc", l), rng(mats("encoder.transformer_encoder.%d." % l))) for l in range(self.L)]
+            st += [(("dec", l), rng(mats("decoder.transformer_decoder.%d." % l))) for l in range(self.L)]
+            st += [("head", rng(["decoder.fc_output.weight"]))]
+            self._upd_ranges = st
+            self._stage_rng = dict(st)
+        return self._upd_ranges
+
+    def queue_update(self, fn, stream):
+        """fn(lo, hi) enqueues the optimizer update of arena range [lo, hi) on
+        `stream` (a torch.cuda.Stream); ranges in update_ranges() order."""
+        self.sync_pending()
+        for _, (lo, hi) in self.update_ranges():
+            fn(lo, hi)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self._wpending.append((lo, hi, ev))
+
+    def _await(self, lo, hi):
+        main = torch.cuda.current_stream(self.device)
+        keep = []
+        for l, h, ev in self._wpending:
+            if l < hi and lo < h:
+                main.wait_event(ev)
+            else:
+                keep.append((l, h, ev))
+        self._wpending = keep
+
+    def await_stage(self, key):
+        """The current stream waits for the queued update of stage `key`'s weights."""
+        if self._wpending:
+            self._await(*self._stage_rng[key])
+
+    def sync_pending(self):
+        """The current stream waits for every queued update."""
+        if self._wpending:
+            self._await(0, self.numel)
 
     # views ----------------------------------------------------------------
     def w(self, name, rows=1):
@@ -744,6 +802,7 @@ class Seq2SeqEngine:
 
     # --------------------------------------------------------------- forward
     def _enc_layer(self, bb, l, x, T):
+        self.await_stage(("enc", l))
         D, B = self.D, bb.B
         pre = "encoder.transformer_encoder.%d." % l
         sd = lambda s: _seed(self.base_seed, True, l, s)
@@ -769,6 +828,7 @@ class Seq2SeqEngine:
         return x2
 
     def _dec_layer(self, bb, l, x, mem, T):
+        self.await_stage(("dec", l))
         D, B = self.D, bb.B
         pre = "decoder.transformer_decoder.%d." % l
         sd = lambda s: _seed(self.base_seed, False, l, s)
@@ -809,7 +869,9 @@ class Seq2SeqEngine:
         self.st = K.stream_of(self.device)
         self.p = float(self.dropout) if training else 0.0
         self._xq = {}  # e4m3 activation copies never outlive a forward
+        self.await_stage("vec")  # biases and LayerNorm parameters of every stage
         if self.fp8:
+            self.sync_pending()  # every fp8 weight is quantized up front
             self._fp8_weights()
 
     def encode(self, bb, src, T):
@@ -821,6 +883,7 @@ class Seq2SeqEngine:
             K.copy2d(src.reshape(M, self.in_dim), self.in_dim, bb.src, self.in_dim, M, self.in_dim, self.in_dim,
                      stream=self.st)
             x_src = bb.src
+        self.await_stage("emb")
         self._gemm_fwd(x_src, "encoder.embedding.weight", bb.x0, K.EPI_BIAS_ROPE,
                        rope=(*self.rope(T, self.D), T, self.D), rope_cols=self.D)
         self.x_src = x_src
@@ -841,6 +904,7 @@ class Seq2SeqEngine:
             x = self._dec_layer(bb, l, x, mem, T)
         self._ln(None, x, bb.xf, bb.decf_stats, "decoder.layer_norm", 0, (0, 0), None)
         pred = torch.empty(bb.M, 64, dtype=torch.float32, device=self.device)
+        self.await_stage("head")
         self._gemm_fwd(bb.xf, "decoder.fc_output.weight", pred, K.EPI_BIAS)
         return pred
 
@@ -870,6 +934,7 @@ class Seq2SeqEngine:
             raise RuntimeError("Seq2Seq forward was run again before backward of an earlier forward")
         bb, T = sv["bb"], sv["T"]
         self.ensure_bound()
+        self.sync_pending()
         self.cur = bb
         self._main = torch.cuda.current_stream(self.device)
         self.st = self._main.cuda_stream

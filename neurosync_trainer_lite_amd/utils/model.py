@@ -40,6 +40,11 @@ def _rope_apply(x, dim):
 # runs the whole Seq2Seq on the fused engine instead, so a module-level call in
 # training mode with dropout > 0, or one that would need autograd, raises.
 def _check_module_call(module, *xs, mask=None):
+    for q in module.parameters():  # an optimizer update may still be queued on the arena
+        eng = getattr(q, "_nstl_engine", None)
+        if eng is not None and eng() is not None:
+            eng().sync_pending()
+        break
     if mask is not None:
         raise NotImplementedError("attention masks are not used by the reference model (mask=None only)")
     for x in xs:
@@ -308,10 +313,18 @@ class Seq2Seq(nn.Module):
 
     def state_dict(self, *args, **kwargs):
         eng = self.__dict__.get("_engine")
+        if eng is not None:
+            eng.sync_pending()
         if eng is not None and eng.master_stale:
             raise RuntimeError("parameters are sharded across ranks (FusedAdam.shard): call "
                                "optimizer.consolidate() on every rank before state_dict()")
         return super().state_dict(*args, **kwargs)
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        eng = self.__dict__.get("_engine")
+        if eng is not None:
+            eng.sync_pending()
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
 
     def engine(self, device=None):
         """The MI355X engine owning this model's parameter arena (built on first use)."""

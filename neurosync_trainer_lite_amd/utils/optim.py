@@ -8,6 +8,8 @@ reference checkpoints load and ours load into torch.optim.Adam.  One
 per-tensor norms and Adam's ~5 foreach passes (training_utils.py:73-74), and the
 norm stays on the device (the reference syncs 344 ``.item()``s per step).
 """
+import os
+
 import torch
 
 from .. import _hip as K
@@ -32,6 +34,18 @@ class FusedAdam(torch.optim.Optimizer):
         self.last_norm = None
         self._comm = None            # parallel.ShardComm when sharded (ZeRO-1)
         self._moments_stale = False  # sharded: m/v outside this rank's shard are old
+        # The caller's next use of the parameters is the model's forward (the
+        # training loop sets this): the update is queued on a side stream in arena
+        # ranges that the forward waits for stage by stage (Seq2SeqEngine.
+        # queue_update), so it runs under the forward of earlier layers.  Results
+        # are identical; any other reader of the parameters syncs first
+        # (state_dict, module-level forwards, backward).
+        # Opt-in (NSTL_ADAM_OVERLAP=1): measured no faster at the 228M config
+        # (562.0k vs 561.3k frames/s): the ring GEMMs lose ~5 % to any kernel that
+        # holds CUs beside them, about what the update saves
+        self.overlap_next_forward = False
+        self._overlap_allowed = os.environ.get("NSTL_ADAM_OVERLAP", "0") == "1"
+        self._upd_stream = None
 
     # --------------------------------------------------------------- arena
     def _bind(self):
@@ -50,6 +64,7 @@ class FusedAdam(torch.optim.Optimizer):
             self.v = torch.zeros_like(eng.p32)
             self.partial = torch.empty(N_PARTIAL, dtype=torch.float32, device=eng.device)
             self.norm = torch.zeros(1, dtype=torch.float32, device=eng.device)
+            self.coef = torch.ones(1, dtype=torch.float32, device=eng.device)
             for p in params:
                 old = self.state.get(p, {})
                 views = self._state_views(p)
@@ -127,7 +142,34 @@ class FusedAdam(torch.optim.Optimizer):
             if max_norm is not None:
                 K.sumsq(grads, grads.numel(), partial, N_PARTIAL, stream=st)
 
+        if self._comm is None and self.overlap_next_forward and self._overlap_allowed and closure is None:
+            # clip coefficient on the current stream, the update in arena ranges on
+            # the side stream (nstl_adam_step reads the coefficient: no LDS, so its
+            # workgroups fit beside the forward's ring-GEMM workgroups)
+            main = torch.cuda.current_stream(eng.device)
+            if max_norm is not None:
+                sumsq_fn(eng.g32, self.partial)
+                K.clip_coef(self.partial, N_PARTIAL, max_norm, self.coef, self.norm, stream=st)
+            else:
+                self.coef.fill_(1.0)
+            if self._upd_stream is None:
+                self._upd_stream = torch.cuda.Stream(eng.device)
+            side = self._upd_stream
+            side.wait_stream(main)
+            a.sumsq_partial, a.n_partial, a.norm_out, a.coef = None, 0, None, self.coef.data_ptr()
+
+            def upd(lo, hi):
+                a.p, a.g, a.m, a.v = (eng.p32[lo:].data_ptr(), eng.g32[lo:].data_ptr(), self.m[lo:].data_ptr(),
+                                      self.v[lo:].data_ptr())
+                if eng.p16 is not eng.p32:
+                    a.p_lowp = eng.p16[lo:].data_ptr()
+                a.n = hi - lo
+                K.adam_step(a, stream=side.cuda_stream)
+            eng.queue_update(upd, side)
+            self._snapshot_norm(max_norm)
+            return loss
         if self._comm is None:
+            eng.sync_pending()
             sumsq_fn(eng.g32, self.partial)
             adam_fn(0, eng.numel, eng.g32, self.partial)
             self._snapshot_norm(max_norm)
@@ -159,7 +201,13 @@ class FusedAdam(torch.optim.Optimizer):
             super().zero_grad(set_to_none)
 
     # ------------------------------------------------------------ state io
+    def _sync(self):
+        eng = self._engine
+        if eng is not None:
+            eng.sync_pending()
+
     def state_dict(self):
+        self._sync()
         if self._moments_stale:
             raise RuntimeError("sharded FusedAdam: call consolidate() on every rank before state_dict()")
         if self._engine is not None:
@@ -173,6 +221,7 @@ class FusedAdam(torch.optim.Optimizer):
         return sd
 
     def load_state_dict(self, state_dict):
+        self._sync()
         super().load_state_dict(state_dict)
         params = self.param_groups[0]["params"]
         loaded = {p: dict(self.state[p]) for p in params if p in self.state}

@@ -91,6 +91,11 @@ def train_one_epoch(epoch, model, dataloader, criterion, optimizer, device, clip
     val_steps, val_losses = [], []
     val_iter = iter(val_dataloader) if val_dataloader is not None else None
     pending = _Pending()
+    # the next use of the parameters is this loop's forward: the fused optimizer
+    # may run its update under that forward (FusedAdam.overlap_next_forward)
+    fused = isinstance(optimizer, FusedAdam) and optimizer._comm is None
+    if fused:
+        optimizer.overlap_next_forward = True
 
     def report(done):
         nonlocal epoch_loss
@@ -119,6 +124,9 @@ def train_one_epoch(epoch, model, dataloader, criterion, optimizer, device, clip
             val_steps.append(batch_step)
             val_losses.append(vl)
     report(pending.flush())
+    if fused:
+        optimizer.overlap_next_forward = False
+        optimizer._sync()
     print_epoch_summary(epoch, total_epochs, epoch_loss, n_batches, time.time() - start_time)
     save_loss_plot(epoch, train_steps, train_losses, val_steps, val_losses, save_dir="dataset/validation_plots/loss")
     save_gradient_norm_plot(epoch, gradient_norms, save_dir="dataset/validation_plots/gradient_norms")

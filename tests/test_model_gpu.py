@@ -360,3 +360,42 @@ def test_module_level_forwards_match_reference_layers(golden):
     enc.ffn.dropout.p = 0.3
     with pytest.raises(RuntimeError, match="inference-only"), torch.no_grad():
         enc(x)
+
+
+@pytest.mark.parametrize("amp", [True, False])
+def test_update_overlapped_with_next_forward_is_identical(amp):
+    """FusedAdam.overlap_next_forward: the update runs on a side stream in arena
+    ranges that the next forward waits for stage by stage.  Same kernels, same
+    order per element: parameters, moments, losses and norms are bit-identical
+    to the in-order step; state_dict() after a queued update sees the new weights."""
+    D, H, L, B, T = 256, 4, 2, 4, 64
+    runs = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        cfg, model, crit, opt, _ = make(D, H, L, 31, amp=amp, dropout=0.1)
+        model.train()
+        opt.overlap_next_forward = overlap
+        opt._overlap_allowed = True  # the path is opt-in (NSTL_ADAM_OVERLAP=1)
+        g = torch.Generator().manual_seed(5)
+        losses, norms = [], []
+        for s in range(4):
+            src = torch.randn(B, T, 256, generator=g).to(DEV)
+            trg = (torch.randn(B, T, 61, generator=g) * 20).to(DEV)
+            opt.zero_grad()
+            loss = crit(model(src), trg)
+            loss.backward()
+            opt.step(max_norm=2.0)
+            losses.append(loss.detach().clone())
+            norms.append(opt.last_norm.clone())
+        if overlap:
+            assert model.engine()._wpending, "the last update should still be queued"
+        sd = {k: v.clone() for k, v in model.state_dict().items()}  # syncs a queued update
+        eng = model.engine()
+        assert not eng._wpending
+        torch.cuda.synchronize()
+        runs.append((sd, opt.m.clone(), opt.v.clone(), torch.stack(losses), torch.cat(norms)))
+    (sd0, m0, v0, l0, n0), (sd1, m1, v1, l1, n1) = runs
+    assert torch.equal(l0, l1) and torch.equal(n0, n1)
+    assert torch.equal(m0, m1) and torch.equal(v0, v1)
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
