@@ -263,6 +263,14 @@ int nstl_cast(int src_dtype, const void* src, int dst_dtype, void* dst, int64_t 
 int nstl_autocorr(const float* y, int64_t n_samples, int frame_length, int hop_length, int n_lags,
                   double* out, int n_frames, void* stream);
 
+/* Fused STFT -> power -> mel (BASELINE config C5's fused STFT/mel kernel;
+ * utils/audio/extraction/extract_features_utils.py:17-30 up to the dB step):
+ * centre-padded periodic-Hann frames of n_fft = int(0.01667 sr) every n_fft/2
+ * samples, mixed-radix FFT (n_fft over radices 2, 3, 4, 5, 7), |X|^2 of bins
+ * 0..n_fft/2, 128 Slaney mel filters.  mel_out: f32 [n_frames][128] power,
+ * n_frames = 1 + n_samples / (n_fft/2).  nstl_features runs the same kernel. */
+int nstl_stft_mel(const float* y, int64_t n_samples, int sr, float* mel_out, int n_frames, void* stream);
+
 /* Combined per-clip audio features: extract_and_combine_features after the
  * load (utils/audio/extraction/extract_features.py:6-46 with
  * extract_features_utils.py:5-44,54-128): MFCC(23, CMVN) + delta + delta2

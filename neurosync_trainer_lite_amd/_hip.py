@@ -109,7 +109,7 @@ EXPORTS = [
     "nstl_reduce_rows", "nstl_reduce_rows_strided", "nstl_reduce_rows3", "nstl_reduce_rows_batch",
     "nstl_colsum", "nstl_rope",
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_clip_coef", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
-    "nstl_features", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
+    "nstl_features", "nstl_stft_mel", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
     "nstl_version", "nstl_fp8_quant_rows", "nstl_kernel_counts", "nstl_kernel_counts_reset",
     "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs",
 ]
@@ -161,6 +161,7 @@ def lib():
         L.nstl_copy2d.argtypes = [_i32, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp]
         L.nstl_autocorr.argtypes = [_vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp]
         L.nstl_features.argtypes = [_vp, _i64, _i32, _vp, _i64, _i32, _vp, _i64, _vp]
+        L.nstl_stft_mel.argtypes = [_vp, _i64, _i32, _vp, _i32, _vp]
         L.nstl_features_workspace_bytes.argtypes = [_i64, _i32]
         L.nstl_features_workspace_bytes.restype = _i64
         L.nstl_features_frames.argtypes = [_i64, _i32]
@@ -400,6 +401,12 @@ def clip_coef(partial, n_partial, max_norm, coef, norm_out=None, stream=None):
     check(lib().nstl_clip_coef(partial.data_ptr(), n_partial, float(max_norm), coef.data_ptr(),
                                norm_out.data_ptr() if norm_out is not None else None,
                                stream if stream is not None else stream_of()), "nstl_clip_coef")
+
+
+def stft_mel(y, n_samples, sr, mel, n_frames, stream=None):
+    """Fused STFT -> power -> mel power [n_frames][128] (nstl_stft_mel)."""
+    check(lib().nstl_stft_mel(y.data_ptr(), n_samples, sr, mel.data_ptr(), n_frames,
+                              stream if stream is not None else stream_of()), "nstl_stft_mel")
 
 
 def adam_step(a, stream=None):

@@ -177,6 +177,7 @@ extern "C" int nstl_autocorr(const float* y, int64_t n_samples, int frame_length
 // absent from this image): parity for this branch is unpinned, see DESIGN.md.
 // ============================================================================
 namespace {
+constexpr int FFT_MAX = 4096;  // largest n_fft of the fused STFT/mel path
 constexpr int N_MELS = 128;
 constexpr int N_MFCC = 23;
 constexpr int N_AC = 187;
@@ -190,7 +191,25 @@ struct FeatTables {
   int nbp = 0;
   float* dct = nullptr;     // [N_MFCC][N_MELS]
   float* sg = nullptr;      // [2 orders][SG_W fit positions][SG_W taps]
+  // fused STFT/mel (stft_mel_kernel): radices of n_fft (nf = 0: n_fft has a prime
+  // factor > 7, the DFT-GEMM path serves it), twiddles, mel filters as bands
+  int nf = 0, radix[16] = {};
+  float2* tw = nullptr;     // [n_fft] exp(-2 pi i k / n_fft), built in f64
+  int* band = nullptr;      // [N_MELS][3]: first bin, bin count, offset in bw of each filter
+  float* bw = nullptr;      // [nnz] filter weights, band after band
+  int nnz = 0;
 };
+
+// n over {4, 2, 3, 5, 7} (fours first); 0 when another prime factor remains
+int fft_radices(int n, int* f) {
+  int k = 0;
+  for (int r : {4, 2, 3, 5, 7})
+    while (n % r == 0 && k < 16) {
+      f[k++] = r;
+      n /= r;
+    }
+  return n == 1 ? k : 0;
+}
 
 double hz_to_mel(double f) {
   const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = std::log(6.4) / 27.0;
@@ -304,7 +323,34 @@ int get_tables(int sr, const FeatTables** out) {
   float sg[2 * SG_W * SG_W];
   savgol_table(1, sg);
   savgol_table(2, sg + SG_W * SG_W);
+  // fused STFT/mel tables
+  t->nf = n_fft <= FFT_MAX ? fft_radices(n_fft, t->radix) : 0;
+  std::vector<float2> tw(n_fft);
+  for (int k = 0; k < n_fft; ++k) {
+    const double ph = 2.0 * M_PI * k / n_fft;
+    tw[k] = make_float2((float)std::cos(ph), (float)-std::sin(ph));
+  }
+  std::vector<int> band(3 * N_MELS, 0);
+  std::vector<float> bw;
+  for (int i = 0; i < N_MELS; ++i) {
+    int lo = -1, hi = -1;
+    for (int b = 0; b < nb; ++b)
+      if (melK[(size_t)i * t->nbp + b] != 0.f) {
+        if (lo < 0) lo = b;
+        hi = b;
+      }
+    band[3 * i] = lo < 0 ? 0 : lo;
+    band[3 * i + 1] = lo < 0 ? 0 : hi - lo + 1;
+    band[3 * i + 2] = (int)bw.size();
+    for (int b = lo; lo >= 0 && b <= hi; ++b) bw.push_back(melK[(size_t)i * t->nbp + b]);
+  }
+  t->nnz = (int)bw.size();
+  // stft_mel_kernel's LDS (stft_mel_lds): within the 64 KB a launch gets without opt-in
+  if (t->nf > 0 && (size_t)3 * n_fft * 8 + (size_t)n_fft * 4 + 3 * N_MELS * 4 + (size_t)t->nnz * 4 > 65536) t->nf = 0;
   int rc = upload((void**)&t->basis, basis.data(), basis.size() * 4);
+  if (!rc) rc = upload((void**)&t->tw, tw.data(), tw.size() * sizeof(float2));
+  if (!rc) rc = upload((void**)&t->band, band.data(), band.size() * sizeof(int));
+  if (!rc) rc = upload((void**)&t->bw, bw.data(), std::max<size_t>(1, bw.size()) * 4);
   if (!rc) rc = upload((void**)&t->window, win.data(), win.size() * 4);
   if (!rc) rc = upload((void**)&t->melK, melK.data(), melK.size() * 4);
   if (!rc) rc = upload((void**)&t->dct, dct.data(), dct.size() * 4);
@@ -326,6 +372,123 @@ __global__ __launch_bounds__(256) void stft_frames_kernel(const float* __restric
     row[k] = (k < n_fft && i >= 0 && i < n) ? y[i] * win[k] : 0.f;
   }
 }
+
+// ---------------------------------------------------------------------------
+// Fused STFT -> power -> mel (BASELINE C5's fused STFT/mel kernel;
+// extract_features_utils.py:17-30 up to the dB step, librosa.feature.melspectrogram
+// restated): per frame the centre-padded (zeros), periodic-Hann-windowed frame
+// goes through a mixed-radix (4, 2, 3, 5, 7) Stockham FFT in LDS -- f32, twiddles
+// rounded from an f64 table -- then |X|^2 of bins 0..n_fft/2 and the 128 Slaney
+// filters as contiguous bands of weights.  Writes mel power [F][128] and the
+// clip-wide max (the dB floor's reference).  Replaces frames -> DFT GEMM
+// (4.3 MFLOP per frame on the f32 MFMA) -> |X|^2 -> mel GEMM -> max: one launch,
+// ~0.1 MFLOP per frame, the audio read once per frame (L2) and 512 B written.
+constexpr int FFT_NT = 256, FFT_FPB = 8;  // threads, frames per workgroup (tables loaded once)
+
+NSTL_DEV float2 cmul(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+
+// One Stockham pass of radix R: n/R butterflies, each combining R interleaved
+// sub-transforms of length ns into one of length ns*R (natural order after the
+// last pass).  Twiddles tw[k] = exp(-2 pi i k / n); W_R^m = tw[m n / R].
+template <int R>
+NSTL_DEV void fft_pass(const float2* src, float2* dst, int n, int ns, const float2* tw) {
+  const int m = n / R, ts = n / (ns * R);
+  float2 W[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) W[k] = tw[k * m];
+  for (int j = threadIdx.x; j < m; j += FFT_NT) {
+    const int jn = j % ns;
+    float2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = src[j + r * m];
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * jn * ts]);  // r jn ts < n
+    const int base = (j - jn) * R + jn;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      float2 acc = v[0];
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        const float2 w = W[(r * q) % R];
+        acc.x = fmaf(v[r].x, w.x, fmaf(-v[r].y, w.y, acc.x));
+        acc.y = fmaf(v[r].x, w.y, fmaf(v[r].y, w.x, acc.y));
+      }
+      dst[base + q * ns] = acc;
+    }
+  }
+}
+
+struct FftPlanArg { int n, nf, radix[16]; };
+
+// dynamic LDS: twiddles [n] float2 | buffers 2 x [n] float2 | window [n] | band [3*128] int | weights [nnz]
+__global__ __launch_bounds__(FFT_NT) void stft_mel_kernel(const float* __restrict__ y, int64_t n_samples, int hop,
+                                                          FftPlanArg plan, const float2* __restrict__ tw_g,
+                                                          const float* __restrict__ win_g,
+                                                          const int* __restrict__ band_g,
+                                                          const float* __restrict__ bw_g, int nnz, int F,
+                                                          float* __restrict__ mel, int* __restrict__ key) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int n = plan.n, tid = threadIdx.x;
+  float2* tw = (float2*)smem;
+  float2* buf0 = tw + n;
+  float2* buf1 = buf0 + n;
+  float* win = (float*)(buf1 + n);
+  int* band = (int*)(win + n);
+  float* bw = (float*)(band + 3 * N_MELS);
+  for (int k = tid; k < n; k += FFT_NT) {
+    tw[k] = tw_g[k];
+    win[k] = win_g[k];
+  }
+  for (int k = tid; k < 3 * N_MELS; k += FFT_NT) band[k] = band_g[k];
+  for (int k = tid; k < nnz; k += FFT_NT) bw[k] = bw_g[k];
+  float vmax = 0.f;
+  const int nb = n / 2 + 1;
+  for (int fi = 0; fi < FFT_FPB; ++fi) {
+    const int f = blockIdx.x * FFT_FPB + fi;
+    if (f >= F) break;  // uniform over the workgroup
+    __syncthreads();    // tables loaded / the previous frame's mel reads are done
+    const int64_t start = (int64_t)f * hop - n / 2;  // center=True, zero padding
+    for (int k = tid; k < n; k += FFT_NT) {
+      const int64_t i = start + k;
+      buf0[k] = make_float2(i >= 0 && i < n_samples ? y[i] * win[k] : 0.f, 0.f);
+    }
+    __syncthreads();
+    float2* src = buf0;
+    float2* dst = buf1;
+    int ns = 1;
+    for (int p = 0; p < plan.nf; ++p) {
+      const int r = plan.radix[p];
+      switch (r) {
+        case 2: fft_pass<2>(src, dst, n, ns, tw); break;
+        case 3: fft_pass<3>(src, dst, n, ns, tw); break;
+        case 4: fft_pass<4>(src, dst, n, ns, tw); break;
+        case 5: fft_pass<5>(src, dst, n, ns, tw); break;
+        default: fft_pass<7>(src, dst, n, ns, tw); break;
+      }
+      ns *= r;
+      float2* t = src;
+      src = dst;
+      dst = t;
+      __syncthreads();
+    }
+    float* pw = (float*)dst;  // |X|^2 of bins 0..nb-1 into the free buffer
+    for (int b = tid; b < nb; b += FFT_NT) pw[b] = src[b].x * src[b].x + src[b].y * src[b].y;
+    __syncthreads();
+    if (tid < N_MELS) {
+      const int lo = band[3 * tid], cnt = band[3 * tid + 1], off = band[3 * tid + 2];
+      float acc = 0.f;
+      for (int t = 0; t < cnt; ++t) acc = fmaf(bw[off + t], pw[lo + t], acc);
+      mel[(int64_t)f * N_MELS + tid] = acc;
+      vmax = fmaxf(vmax, acc);
+    }
+  }
+  if (key != nullptr) {
+    vmax = wave_max(vmax);
+    if ((tid & 63) == 0 && tid < N_MELS) atomicMax(key, __float_as_int(vmax));
+  }
+}
+
+size_t stft_mel_lds(int n, int nnz) { return (size_t)3 * n * 8 + (size_t)n * 4 + 3 * N_MELS * 4 + (size_t)nnz * 4; }
 
 // |X|^2 for bins 0..nb-1 into rows of nbp (zero tail): the mel GEMM's A operand
 __global__ __launch_bounds__(256) void power_kernel(const float* __restrict__ X, int F, int nb, int nbp,
@@ -461,7 +624,44 @@ FeatLayout feat_layout(int64_t n_samples, int sr) {
 }
 
 __global__ void init_key(int* k) { *k = 0; }  // mel power >= 0: bits of 0.f
+
+// NSTL_FEATURES_FFT=0: the frames -> DFT GEMM -> power -> mel GEMM path instead
+// of the fused STFT/mel kernel (A/B comparisons; also any n_fft with a prime
+// factor > 7)
+bool use_fft(const FeatTables* T) {
+  static const int on = [] {
+    const char* e = getenv("NSTL_FEATURES_FFT");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on && T->nf > 0;
+}
+
+int launch_stft_mel(const FeatTables* T, const float* y, int64_t n_samples, int hop, int F, float* mel, int* key,
+                    hipStream_t st) {
+  FftPlanArg plan;
+  plan.n = T->n_fft;
+  plan.nf = T->nf;
+  for (int i = 0; i < 16; ++i) plan.radix[i] = T->radix[i];
+  const size_t lds = stft_mel_lds(T->n_fft, T->nnz);
+  NSTL_CHECK_ARG(lds <= 160 * 1024, "nstl_features: n_fft %d too large for the fused STFT/mel kernel", T->n_fft);
+  hipLaunchKernelGGL(stft_mel_kernel, dim3((F + FFT_FPB - 1) / FFT_FPB), dim3(FFT_NT), lds, st, y, n_samples, hop,
+                     plan, T->tw, T->window, T->band, T->bw, T->nnz, F, mel, key);
+  NSTL_LAUNCH_CHECK("nstl_features stft_mel");
+  return 0;
+}
 }  // namespace
+
+extern "C" int nstl_stft_mel(const float* y, int64_t n_samples, int sr, float* mel_out, int n_frames, void* stream) {
+  NSTL_CHECK_ARG(y && mel_out, "nstl_stft_mel: null pointer");
+  NSTL_CHECK_ARG(sr >= 8000 && sr <= 192000, "nstl_stft_mel: sr %d out of range", sr);
+  const FeatLayout L = feat_layout(n_samples, sr);
+  NSTL_CHECK_ARG(n_samples >= L.n_fft, "nstl_stft_mel: %lld samples < one frame", (long long)n_samples);
+  NSTL_CHECK_ARG(n_frames == L.F, "nstl_stft_mel: n_frames %d != %d", n_frames, L.F);
+  const FeatTables* T = nullptr;
+  if (int rc = get_tables(sr, &T)) return rc;
+  NSTL_CHECK_ARG(T->nf > 0, "nstl_stft_mel: n_fft %d has a prime factor > 7", T->n_fft);
+  return launch_stft_mel(T, y, n_samples, L.hop, L.F, mel_out, nullptr, (hipStream_t)stream);
+}
 
 extern "C" int64_t nstl_features_workspace_bytes(int64_t n_samples, int sr) {
   return (int64_t)feat_layout(n_samples, sr).total;
@@ -493,6 +693,11 @@ extern "C" int nstl_features(const float* y, int64_t n_samples, int sr, float* o
   double* ac = (double*)(ws + L.ac);
   int* key = (int*)(ws + L.key);
 
+  if (use_fft(T)) {
+    // fused STFT/mel: mel power -> db buffer, clip-wide max -> key
+    hipLaunchKernelGGL(init_key, dim3(1), dim3(1), 0, st, key);
+    if (int rc = launch_stft_mel(T, y, n_samples, L.hop, L.F, db, key, st)) return rc;
+  } else {
   hipLaunchKernelGGL(stft_frames_kernel, dim3(L.F), dim3(256), 0, st, y, n_samples, L.n_fft, L.hop, L.kp, T->window,
                      frames);
   NSTL_LAUNCH_CHECK("nstl_features frames");
@@ -517,6 +722,7 @@ extern "C" int nstl_features(const float* y, int64_t n_samples, int sr, float* o
   hipLaunchKernelGGL(melmax_kernel, dim3((unsigned)std::min<int64_t>((nm + 255) / 256, 1024)), dim3(256), 0, st, db,
                      nm, key);
   NSTL_LAUNCH_CHECK("nstl_features mel");
+  }
   hipLaunchKernelGGL(dct_kernel, dim3((L.F + 63) / 64), dim3(256), 0, st, db, L.F, T->dct, key, mf);
   NSTL_LAUNCH_CHECK("nstl_features dct");
   hipLaunchKernelGGL(cmvn_delta_reduce_kernel, dim3(N_MFCC), dim3(1024), 0, st, mf, L.F, N_MFCC, T->sg, out, ld_out,

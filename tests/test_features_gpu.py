@@ -139,3 +139,31 @@ def test_cmvn_and_pair_reduce_match_reference_fixtures(golden, key):
     for o in (1, 2):
         want = data_ref.reduce_features(data_ref.savgol_delta(cm, o)).T
         np.testing.assert_allclose(got[:, o * C:(o + 1) * C], want, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("seconds,seed,silent", [(0.6, 11, False), (0.35, 12, True)])
+def test_fused_stft_mel_matches_f64(seconds, seed, silent):
+    """nstl_stft_mel (mixed-radix f32 FFT in LDS, |X|^2, Slaney bands) against the
+    f64 numpy STFT power times the f64 mel basis (oracle/data_ref.mfcc_120's
+    first steps).  Tolerance per frame: 2e-6 of the frame's largest band plus
+    2e-5 relative (f32 FFT rounding ~ log2(n) eps)."""
+    from neurosync_trainer_lite_amd import _hip as K
+    sr, n_fft, hop = 88200, 1470, 735
+    y = synth_audio(seconds, seed)
+    if silent:  # a silent lead-in: bands near zero in the first frames
+        y[:4000] = 0
+    F = 1 + len(y) // hop
+    yp = np.pad(y.astype(np.float64), n_fft // 2, mode="constant")
+    frames = data_ref.frame_signal(yp, n_fft, hop)[:, :F]
+    win = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(n_fft) / n_fft)
+    power = np.abs(np.fft.rfft(frames * win[:, None], axis=0)) ** 2
+    ref = (data_ref.mel_basis(sr, n_fft).astype(np.float64) @ power).T  # [F, 128]
+    yd = torch.tensor(y, device="cuda:0")
+    mel = torch.empty(F, 128, device="cuda:0")
+    K.stft_mel(yd, len(y), sr, mel, F)
+    torch.cuda.synchronize()
+    got = mel.double().cpu().numpy()
+    bound = 2e-6 * ref.max(axis=1, keepdims=True) + 2e-5 * np.abs(ref)
+    assert np.all(np.abs(got - ref) <= bound + 1e-30), np.max(np.abs(got - ref) / (bound + 1e-30))
+    with pytest.raises(RuntimeError, match="n_frames"):
+        K.stft_mel(yd, len(y), sr, mel, F + 1)
