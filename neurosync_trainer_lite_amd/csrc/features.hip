@@ -94,6 +94,93 @@ __global__ __launch_bounds__(NT) void autocorr_kernel(const float* y, int64_t n,
     for (int lag = tid; lag < n_lags; lag += NT) out[(int64_t)f * n_lags + lag] /= ac0;
 }
 
+// Register-tiled form (default; NSTL_AUTOCORR_V1=1 keeps the kernel above):
+// a thread owns 16 consecutive lags over one 16-aligned chunk of the sample
+// index and, per block of 16 samples, reads a[16] = w[k..k+15] and b[31] =
+// w[k+l0..k+l0+30] from LDS (16-byte reads) for 256 f64 FMAs -- no register
+// shifting (the sliding window above moves 7 registers per 8 FMAs).  12 lag
+// groups x 20 chunks = 240 threads; chunk partials summed in LDS in chunk order.
+constexpr int AC2_LG = 16, AC2_GROUPS = 12, AC2_CHUNKS = 20;
+constexpr int AC2_NT = 256;
+
+size_t ac2_chunk(int L) { return ((size_t)(L + AC2_CHUNKS - 1) / AC2_CHUNKS + AC2_LG - 1) / AC2_LG * AC2_LG; }
+size_t ac2_wlen(int L) { return ac2_chunk(L) * AC2_CHUNKS + AC2_LG * AC2_GROUPS + 2 * AC2_LG; }
+size_t ac2_lds(int L) { return (ac2_wlen(L) + (size_t)AC2_CHUNKS * AC2_LG * AC2_GROUPS + 8) * sizeof(double); }
+
+__global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64_t n, int L, int hop, int n_lags,
+                                                            const double* __restrict__ hann, double* out, int chunk,
+                                                            int wlen) {
+  extern __shared__ __attribute__((aligned(16))) double ac2_smem[];
+  double* w = ac2_smem;                  // [wlen]: the windowed frame, zero tail
+  double* part = w + wlen;               // [AC2_CHUNKS][AC2_LG * AC2_GROUPS]
+  double* red = part + AC2_CHUNKS * AC2_LG * AC2_GROUPS;  // [4] wave sums, [4] lag 0
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int64_t start = (int64_t)f * hop - L / 2;
+  double s = 0.0;
+  for (int k = tid; k < L; k += AC2_NT) {
+    int64_t i = start + k;
+    if (i < 0) i = -i;                   // numpy 'reflect' (edge not repeated)
+    if (i >= n) i = 2 * (n - 1) - i;
+    const double v = (double)y[i];
+    w[k] = v;
+    s += v;
+  }
+  for (int k = L + tid; k < wlen; k += AC2_NT) w[k] = 0.0;
+  s = wave_sum_d(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  const double mean = (red[0] + red[1] + red[2] + red[3]) / L;
+  // the reference subtracts the mean in float32 (frames are float32 until the
+  // float64 window multiplies them)
+  const float mean_f = (float)mean;
+  for (int k = tid; k < L; k += AC2_NT) {
+    const float c = (float)w[k] - mean_f;
+    w[k] = (double)c * hann[k];
+  }
+  __syncthreads();
+  if (tid < AC2_GROUPS * AC2_CHUNKS) {
+    const int g = tid % AC2_GROUPS, c = tid / AC2_GROUPS;
+    const int l0 = g * AC2_LG;
+    const int k0 = c * chunk, k1 = min(L, k0 + chunk);
+    double acc[AC2_LG];
+#pragma unroll
+    for (int r = 0; r < AC2_LG; ++r) acc[r] = 0.0;
+    for (int kb = k0; kb < k1; kb += AC2_LG) {
+      double a[AC2_LG], b[2 * AC2_LG];
+#pragma unroll
+      for (int j = 0; j < AC2_LG; j += 2) {
+        const double2 t = *(const double2*)(w + kb + j);
+        a[j] = t.x;
+        a[j + 1] = t.y;
+      }
+#pragma unroll
+      for (int j = 0; j < 2 * AC2_LG; j += 2) {
+        const double2 t = *(const double2*)(w + kb + l0 + j);
+        b[j] = t.x;
+        b[j + 1] = t.y;
+      }
+#pragma unroll
+      for (int j = 0; j < AC2_LG; ++j)
+#pragma unroll
+        for (int r = 0; r < AC2_LG; ++r) acc[r] = fma(a[j], b[j + r], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < AC2_LG; ++r) part[c * AC2_LG * AC2_GROUPS + l0 + r] = acc[r];
+  }
+  __syncthreads();
+  double* ac0 = red + 4;
+  for (int lag = tid; lag <= n_lags; lag += AC2_NT) {
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < AC2_CHUNKS; ++c) acc += part[c * AC2_LG * AC2_GROUPS + lag];
+    if (lag == 0) *ac0 = acc;
+    if (lag > 0) out[(int64_t)f * n_lags + (lag - 1)] = acc;
+  }
+  __syncthreads();
+  if (*ac0 != 0.0)
+    for (int lag = tid; lag < n_lags; lag += AC2_NT) out[(int64_t)f * n_lags + lag] /= *ac0;
+}
+
 // np.hanning(L) (symmetric), computed on the host in f64 once per (device, L)
 int get_hann(int L, const double** out) {
   static std::mutex mu;
@@ -151,8 +238,18 @@ extern "C" int nstl_autocorr(const float* y, int64_t n_samples, int frame_length
   hipStream_t st = (hipStream_t)stream;
   const double* hann = nullptr;
   if (int rc = get_hann(frame_length, &hann)) return rc;
-  hipLaunchKernelGGL(autocorr_kernel, dim3(n_frames), dim3(NT), 0, st, y, n_samples, frame_length, hop_length,
-                     n_lags, hann, out);
+  static const bool v1 = [] {
+    const char* e = getenv("NSTL_AUTOCORR_V1");
+    return e && e[0] == '1';
+  }();
+  if (!v1 && n_lags < AC2_LG * AC2_GROUPS && ac2_lds(frame_length) <= 65536) {
+    hipLaunchKernelGGL(autocorr2_kernel, dim3(n_frames), dim3(AC2_NT), ac2_lds(frame_length), st, y, n_samples,
+                       frame_length, hop_length, n_lags, hann, out, (int)ac2_chunk(frame_length),
+                       (int)ac2_wlen(frame_length));
+  } else {
+    hipLaunchKernelGGL(autocorr_kernel, dim3(n_frames), dim3(NT), 0, st, y, n_samples, frame_length, hop_length,
+                       n_lags, hann, out);
+  }
   NSTL_LAUNCH_CHECK("nstl_autocorr");
   hipLaunchKernelGGL(autocorr_edges, dim3(1), dim3(256), 0, st, out, n_frames, n_lags);
   NSTL_LAUNCH_CHECK("nstl_autocorr edges");
