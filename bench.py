@@ -216,6 +216,53 @@ def data_feed(cfg, args, step_fn, dev, rank, world):
                     "-> non_blocking H2D -> train step"}
 
 
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md
+FP64_VECTOR_PEAK_TFLOPS = 78.6   # half the FP32 vector rate (a wave64 f64 FMA takes 4 cycles on SIMD-32)
+
+
+def feature_rooflines(K, audio, n_samp, sr, dev):
+    """The feature path's two kernels timed alone on the feature leg's audio (HIP
+    events, median of 5), against the resource that bounds each:
+    - autocorrelation (the dominant one): 2 * n_fft * (n_lags + 1) f64 FLOP per
+      120 Hz frame (direct lag products, as the reference's f64 np.correlate)
+      vs the FP64 vector peak;
+    - fused STFT/mel: 5 n log2 n FLOP per frame (the radix-agnostic FFT count)
+      + |X|^2 + mel bands, vs the FP32 vector peak; its algorithmic bytes (audio
+      read once, mel power written) vs HBM."""
+    import math
+    n_fft, hop, n_lags = int(0.01667 * sr), int(0.01667 * sr) // 2, 187
+    F = 1 + n_samp // hop
+
+    def med(fn):
+        ts = []
+        for _ in range(6):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        return sorted(ts[1:])[2] * 1e-3
+    ac = torch.empty(F, n_lags, dtype=torch.float64, device=dev)
+    mel = torch.empty(F, 128, dtype=torch.float32, device=dev)
+    t_ac = med(lambda: K.autocorr(audio, n_fft, hop, n_lags, ac, F))
+    t_sm = med(lambda: K.stft_mel(audio, n_samp, sr, mel, F))
+    ac_flop = 2.0 * n_fft * (n_lags + 1) * F
+    sm_flop = (5.0 * n_fft * math.log2(n_fft) + 3 * (n_fft // 2 + 1) + 2 * 2 * (n_fft // 2 + 1)) * F
+    sm_bytes = 4.0 * n_samp + 4.0 * 128 * F
+    return {"frames_120hz": F,
+            "roofline": {"kernel": "autocorr2_kernel (f64 lag products, the feature path's longest kernel)",
+                         "bound": "fp64 VALU", "achieved": round(ac_flop / t_ac / 1e12, 2),
+                         "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(ac_flop / t_ac / 1e12 / FP64_VECTOR_PEAK_TFLOPS, 4),
+                         "us": round(t_ac * 1e6, 1), "algorithmic_flop": ac_flop},
+            "stft_mel": {"kernel": "stft_mel_kernel (fused STFT/mel, mixed-radix f32 FFT in LDS)",
+                         "us": round(t_sm * 1e6, 1), "achieved_tflops": round(sm_flop / t_sm / 1e12, 3),
+                         "frac_fp32_vector": round(sm_flop / t_sm / 1e12 / FP32_VECTOR_PEAK_TFLOPS, 4),
+                         "achieved_gbs": round(sm_bytes / t_sm / 1e9, 1),
+                         "frac_hbm": round(sm_bytes / t_sm / 1e9 / PEAK_HBM_GBS, 4)}}
+
+
 def fwd_parity(cfg, dev, T, windows=2):
     """BASELINE metric's "MSE vs ref" (SURVEY.md 8(d)(i)): forward output of the
     full 228M config (all 8+8 layers) vs the fp32 CPU oracle on the same batch
@@ -455,6 +502,8 @@ def main():
                 "feature_ms_per_step": round(e0.elapsed_time(e1), 3),
                 "workload": "per step: %.1f s of synthetic 88.2 kHz audio per GPU -> GPU MFCC(+d,dd)+autocorr "
                             "features [%d frames x 256] -> the same train step" % (n_samp / sr, B * T)}
+        feat.update(feature_rooflines(K, audio, n_samp, sr, dev))
+        feat["roofline"]["share_of_features"] = round(feat["roofline"]["us"] * 1e-3 / feat["feature_ms_per_step"], 3)
 
     feed = None
     if args.feed_steps > 0:
