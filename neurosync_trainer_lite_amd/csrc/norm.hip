@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // Post-LN residual tails of the NeuroSync Seq2Seq layers (utils/model.py:175-180,
 // :198-207, final norms :228-229/:249-250):
 //   forward : s = x + y * m1 * m2 / (1-p)^n ; out = (s - mean) * rstd * gamma + beta
@@ -237,6 +238,39 @@ NSTL_DEV void load4(const T* p, float (&v)[4]) {
     v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
   }
 }
+// G consecutive columns of a row (G = 8: one 16-byte bf16 access, two for f32)
+template <typename T, int G>
+NSTL_DEV void loadG(const T* p, float (&v)[G]) {
+  if constexpr (G == 4) {
+    load4<T>(p, v);
+  } else if constexpr (sizeof(T) == 2) {
+    const uint4 u = *(const uint4*)p;
+    const T* e = (const T*)&u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = to_f32(e[j]);
+  } else {
+    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+template <typename T>
+NSTL_DEV void store4(T* p, const float* v);
+template <typename T, int G>
+NSTL_DEV void storeG(T* p, const float* v) {
+  if constexpr (G == 4) {
+    store4<T>(p, v);
+  } else if constexpr (sizeof(T) == 2) {
+    uint4 u;
+    T* e = (T*)&u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = from_f32<T>(v[j]);
+    *(uint4*)p = u;
+  } else {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
 template <typename T>
 NSTL_DEV void store4(T* p, const float* v) {
   if constexpr (sizeof(T) == 2) {
@@ -250,9 +284,10 @@ NSTL_DEV void store4(T* p, const float* v) {
   }
 }
 
-template <typename T, int VPL>
+template <typename T, int VPL, int G>
 __global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
-  constexpr int NK = VPL / 4;  // 4-column groups per lane
+  constexpr int NK = VPL / G;  // G-column groups per lane
+  constexpr int SPAN = 64 * G;
   constexpr int NWB = NTB / 64;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -260,25 +295,27 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
 #pragma unroll
   for (int k = 0; k < NK; ++k)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      gam[4 * k + e] = p.gamma[k * 256 + 4 * lane + e];
-      dg[4 * k + e] = db[4 * k + e] = dyb[4 * k + e] = 0.f;
+    for (int e = 0; e < G; ++e) {
+      gam[G * k + e] = p.gamma[k * SPAN + G * lane + e];
+      dg[G * k + e] = db[G * k + e] = dyb[G * k + e] = 0.f;
     }
   const int stride = gridDim.x * NWB;
   int row = blockIdx.x * NWB + w;
   float xh[VPL], gy[VPL], mean = 0.f, rstd = 0.f;
   auto load = [&](int r, float (&x)[VPL], float (&g)[VPL], float& mu, float& rs) {
-    const int64_t base = (int64_t)r * p.D + 4 * lane;
+    const int64_t base = (int64_t)r * p.D + G * lane;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      float t4[4], g4[4], a4[4] = {0.f, 0.f, 0.f, 0.f};
-      load4<T>((const T*)p.s_in + base + k * 256, t4);
-      load4<float>(p.dout + base + k * 256, g4);
-      if (p.dout2) load4<T>((const T*)p.dout2 + base + k * 256, a4);
+      float t4[G], g4[G], a4[G];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        x[4 * k + e] = t4[e];
-        g[4 * k + e] = g4[e] + a4[e];
+      for (int e = 0; e < G; ++e) a4[e] = 0.f;
+      loadG<T, G>((const T*)p.s_in + base + k * SPAN, t4);
+      loadG<float, G>(p.dout + base + k * SPAN, g4);
+      if (p.dout2) loadG<T, G>((const T*)p.dout2 + base + k * SPAN, a4);
+#pragma unroll
+      for (int e = 0; e < G; ++e) {
+        x[G * k + e] = t4[e];
+        g[G * k + e] = g4[e] + a4[e];
       }
     }
     mu = p.mean[r];
@@ -289,7 +326,7 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
     const int nxt = row + stride;
     float xn[VPL], gn[VPL], mn = 0.f, rn = 0.f;
     if (nxt < p.rows) load(nxt, xn, gn, mn, rn);
-    const int64_t base = (int64_t)row * p.D + 4 * lane;
+    const int64_t base = (int64_t)row * p.D + G * lane;
     float a1 = 0.f, a2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
@@ -305,23 +342,23 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
 #pragma unroll
     for (int j = 0; j < VPL; ++j) d[j] = rstd * (gy[j] * gam[j] - m1 - xh[j] * m2);
 #pragma unroll
-    for (int k = 0; k < NK; ++k) store4<float>(p.ds + base + k * 256, d + 4 * k);
+    for (int k = 0; k < NK; ++k) storeG<float, G>(p.ds + base + k * SPAN, d + G * k);
     if (p.dbranch) {
       if (p.thresh && p.n_masks > 0) {
 #pragma unroll
         for (int k = 0; k < NK; ++k)
 #pragma unroll
-          for (int e = 0; e < 4; e += 2) {
+          for (int e = 0; e < G; e += 2) {
             float s0, s1;
-            branch_scale2(p, (uint64_t)base + k * 256 + e, s0, s1);
-            d[4 * k + e] *= s0;
-            d[4 * k + e + 1] *= s1;
+            branch_scale2(p, (uint64_t)base + k * SPAN + e, s0, s1);
+            d[G * k + e] *= s0;
+            d[G * k + e + 1] *= s1;
           }
       }
 #pragma unroll
       for (int j = 0; j < VPL; ++j) d[j] = to_f32(from_f32<T>(d[j]));  // sum what is stored
 #pragma unroll
-      for (int k = 0; k < NK; ++k) store4<T>((T*)p.dbranch + base + k * 256, d + 4 * k);
+      for (int k = 0; k < NK; ++k) storeG<T, G>((T*)p.dbranch + base + k * SPAN, d + G * k);
 #pragma unroll
       for (int j = 0; j < VPL; ++j) dyb[j] += d[j];
     }
@@ -338,11 +375,11 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
 #pragma unroll
   for (int k = 0; k < NK; ++k)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = k * 256 + 4 * lane + e;
-      red[0][w][c] = dg[4 * k + e];
-      red[1][w][c] = db[4 * k + e];
-      red[2][w][c] = dyb[4 * k + e];
+    for (int e = 0; e < G; ++e) {
+      const int c = k * SPAN + G * lane + e;
+      red[0][w][c] = dg[G * k + e];
+      red[1][w][c] = db[G * k + e];
+      red[2][w][c] = dyb[G * k + e];
     }
   __syncthreads();
   for (int c = threadIdx.x; c < p.D; c += NTB) {
@@ -361,34 +398,37 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
 
 // Forward with the interleaved column map of ln_bwd_kernel_il (D % 256 == 0):
 // lane l owns columns k*256 + 4l .. +3, one row per wave.
-template <typename T, int VPL>
+template <typename T, int VPL, int G>
 __global__ __launch_bounds__(NT) void ln_fwd_kernel_il(LnParams p) {
-  constexpr int NK = VPL / 4;
+  constexpr int NK = VPL / G;
+  constexpr int SPAN = 64 * G;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   if (row >= p.rows) return;
-  const int64_t base = (int64_t)row * p.D + 4 * lane;
+  const int64_t base = (int64_t)row * p.D + G * lane;
   float s[VPL], xv[VPL];
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
-    float y4[4], x4[4] = {0.f, 0.f, 0.f, 0.f};
-    load4<T>((const T*)p.y + base + k * 256, y4);
-    if (p.x) load4<T>((const T*)p.x + base + k * 256, x4);
+    float y4[G], x4[G];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      s[4 * k + e] = y4[e];
-      xv[4 * k + e] = x4[e];
+    for (int e = 0; e < G; ++e) x4[e] = 0.f;
+    loadG<T, G>((const T*)p.y + base + k * SPAN, y4);
+    if (p.x) loadG<T, G>((const T*)p.x + base + k * SPAN, x4);
+#pragma unroll
+    for (int e = 0; e < G; ++e) {
+      s[G * k + e] = y4[e];
+      xv[G * k + e] = x4[e];
     }
   }
   if (p.thresh && p.n_masks > 0) {
 #pragma unroll
     for (int k = 0; k < NK; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; e += 2) {
+      for (int e = 0; e < G; e += 2) {
         float m0, m1;
-        branch_scale2(p, (uint64_t)base + k * 256 + e, m0, m1);
-        s[4 * k + e] *= m0;
-        s[4 * k + e + 1] *= m1;
+        branch_scale2(p, (uint64_t)base + k * SPAN + e, m0, m1);
+        s[G * k + e] *= m0;
+        s[G * k + e + 1] *= m1;
       }
   }
   float sum = 0.f;
@@ -408,14 +448,14 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel_il(LnParams p) {
   float o[VPL];
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
-    if (p.s_out) store4<T>((T*)p.s_out + base + k * 256, s + 4 * k);
+    if (p.s_out) storeG<T, G>((T*)p.s_out + base + k * SPAN, s + G * k);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = k * 256 + 4 * lane + e;
+    for (int e = 0; e < G; ++e) {
+      const int c = k * SPAN + G * lane + e;
       // round to the storage type first so `rot_out` rotates exactly what `out` holds
-      o[4 * k + e] = to_f32(from_f32<T>((s[4 * k + e] - mean) * rstd * p.gamma[c] + p.beta[c]));
+      o[G * k + e] = to_f32(from_f32<T>((s[G * k + e] - mean) * rstd * p.gamma[c] + p.beta[c]));
     }
-    store4<T>((T*)p.out + base + k * 256, o + 4 * k);
+    storeG<T, G>((T*)p.out + base + k * SPAN, o + G * k);
   }
   if (lane == 0) {
     p.mean[row] = mean;
@@ -430,57 +470,58 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel_il(LnParams p) {
     if (lane == 0) p.q8_scale[row] = am > 0.f ? am / 448.f : 1.f;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      float v[4];
+      float v[G];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fminf(fmaxf(o[4 * k + e] * inv, -448.f), 448.f);
-      const uint32_t b = ((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false) & 0xffffu) |
-                         (((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], 0, false) & 0xffffu) << 16);
-      *(uint32_t*)(p.q8 + (int64_t)row * p.ldq8 + k * 256 + 4 * lane) = b;
-    }
-  }
-  if (p.q8) {  // the same arithmetic as nstl_fp8_quant_rows on the stored row
-    float am = 0.f;
+      for (int e = 0; e < G; ++e) v[e] = fminf(fmaxf(o[G * k + e] * inv, -448.f), 448.f);
+      uint32_t b[G / 4];
 #pragma unroll
-    for (int j = 0; j < VPL; ++j) am = fmaxf(am, fabsf(o[j]));
-    am = wave_max(am);
-    const float inv = am > 0.f ? 448.f / am : 1.f;
-    if (lane == 0) p.q8_scale[row] = am > 0.f ? am / 448.f : 1.f;
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fminf(fmaxf(o[4 * k + e] * inv, -448.f), 448.f);
-      const uint32_t b = ((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false) & 0xffffu) |
-                         (((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], 0, false) & 0xffffu) << 16);
-      *(uint32_t*)(p.q8 + (int64_t)row * p.ldq8 + k * 256 + 4 * lane) = b;
+      for (int h = 0; h < G / 4; ++h)
+        b[h] = ((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h], v[4 * h + 1], 0, false) & 0xffffu) |
+               (((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h + 2], v[4 * h + 3], 0, false) & 0xffffu) << 16);
+      uint8_t* q = p.q8 + (int64_t)row * p.ldq8 + k * SPAN + G * lane;
+      if constexpr (G == 8) *(uint2*)q = make_uint2(b[0], b[1]);
+      else *(uint32_t*)q = b[0];
     }
   }
   if (p.rot_out) {
     const int t = row % p.rope_T, half = p.D >> 1;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      float r[4];
+      float r[G];
 #pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        const int pr = (k * 256 + 4 * lane + e) >> 1;
+      for (int e = 0; e < G; e += 2) {
+        const int pr = (k * SPAN + G * lane + e) >> 1;
         const float c = p.rope_cos[t * half + pr], sn = p.rope_sin[t * half + pr];
-        r[e] = o[4 * k + e] * c - o[4 * k + e + 1] * sn;
-        r[e + 1] = o[4 * k + e] * sn + o[4 * k + e + 1] * c;
+        r[e] = o[G * k + e] * c - o[G * k + e + 1] * sn;
+        r[e + 1] = o[G * k + e] * sn + o[G * k + e + 1] * c;
       }
-      store4<T>((T*)p.rot_out + base + k * 256, r);
+      storeG<T, G>((T*)p.rot_out + base + k * SPAN, r);
     }
   }
+}
+
+// NSTL_LN_G8=0: four-column lane groups (8-byte bf16 accesses) when D % 512 == 0
+bool ln_g8() {
+  static const int v = [] {
+    const char* e = getenv("NSTL_LN_G8");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return v != 0;
 }
 
 template <typename T, bool BWD>
 int dispatch(const LnParams& p, int grid, hipStream_t st) {
 #define NSTL_LN_CASE(V)                                                                     \
   case V:                                                                                   \
-    if (BWD && V % 4 == 0)                                                                  \
-      hipLaunchKernelGGL((ln_bwd_kernel_il<T, (V % 4 == 0 ? V : 4)>), dim3(grid), dim3(NTB), 0, st, p); \
+    if (BWD && V % 8 == 0 && ln_g8())                                                       \
+      hipLaunchKernelGGL((ln_bwd_kernel_il<T, (V % 8 == 0 ? V : 8), 8>), dim3(grid), dim3(NTB), 0, st, p); \
+    else if (BWD && V % 4 == 0)                                                             \
+      hipLaunchKernelGGL((ln_bwd_kernel_il<T, (V % 4 == 0 ? V : 4), 4>), dim3(grid), dim3(NTB), 0, st, p); \
     else if (BWD) hipLaunchKernelGGL((ln_bwd_kernel<T, V>), dim3(grid), dim3(NT), 0, st, p); \
+    else if (V % 8 == 0 && ln_g8())                                                         \
+      hipLaunchKernelGGL((ln_fwd_kernel_il<T, (V % 8 == 0 ? V : 8), 8>), dim3(grid), dim3(NT), 0, st, p); \
     else if (V % 4 == 0)                                                                    \
-      hipLaunchKernelGGL((ln_fwd_kernel_il<T, (V % 4 == 0 ? V : 4)>), dim3(grid), dim3(NT), 0, st, p); \
+      hipLaunchKernelGGL((ln_fwd_kernel_il<T, (V % 4 == 0 ? V : 4), 4>), dim3(grid), dim3(NT), 0, st, p); \
     else hipLaunchKernelGGL((ln_fwd_kernel<T, V>), dim3(grid), dim3(NT), 0, st, p);        \
     break;
   switch (p.D / 64) {
