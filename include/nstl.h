@@ -70,6 +70,11 @@ typedef struct nstl_gemm_args {
                                           "kept and positive" of the FFN hidden, 1 bit/element */
   const float* a_scale;                /* dtype NSTL_FP8: f32 row scales of A [M] and of B [N]   */
   const float* b_scale;                /* (nstl_fp8_quant_rows); C = a_scale[i] b_scale[j] acc   */
+  float* sq_part;                      /* optional, nstl_gemm_grouped with f32 C only: [tiles][8] f32,
+                                          tile t = its 256x256 tile index in the problem (row-major over
+                                          ceil(M/256) x ceil(N/256)): the sums of squares of C as stored,
+                                          one per wave -- the weight gradients' share of clip_grad_norm_
+                                          (utils/training_utils.py:73) without re-reading them */
 } nstl_gemm_args;
 int nstl_gemm(const nstl_gemm_args* args, void* stream);
 /* Rows of colsum_part for these arguments, or 0 when the call cannot produce it. */
@@ -242,9 +247,9 @@ typedef struct nstl_adam_args {
 int nstl_adam_step(const nstl_adam_args* args, void* stream);
 
 /* clip_grad_norm_'s coefficient min(1, max_norm / (norm + 1e-6)) from nstl_sumsq
- * partials, into coef_out[0] (and the pre-clip norm into norm_out[0] when
- * non-NULL): the form nstl_adam_step's coef reads when the update runs in
- * several arena ranges (utils/training_utils.py:73-74). */
+ * partials (and/or nstl_gemm_args.sq_part partials), n_partial <= 2^20, into
+ * coef_out[0] (and the pre-clip norm into norm_out[0] when non-NULL): the form
+ * nstl_adam_step's coef reads (utils/training_utils.py:73-74). */
 int nstl_clip_coef(const float* partial, int n_partial, float max_norm, float* coef_out, float* norm_out,
                    void* stream);
 

@@ -37,7 +37,7 @@ class GemmArgs(ctypes.Structure):
         ("p_drop", _f32), ("seed", _u64),
         ("rope_cos", _vp), ("rope_sin", _vp), ("rope_T", _i32), ("rope_dim", _i32), ("rope_cols", _i32),
         ("split_k", _i32), ("workspace", _vp), ("workspace_bytes", _i64), ("colsum_part", _vp),
-        ("relu_mask", _vp), ("a_scale", _vp), ("b_scale", _vp),
+        ("relu_mask", _vp), ("a_scale", _vp), ("b_scale", _vp), ("sq_part", _vp),
     ]
 
 
@@ -265,7 +265,7 @@ def gemm_grouped(problems, stream=None):
 def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None,
               alpha=1.0, beta=0.0, epilogue=EPI_NONE, bias=None, aux=None, ld_aux=0, p_drop=0.0, seed=0,
               rope=None, rope_cols=0, split_k=1, workspace=None, colsum_part=None, relu_mask=None,
-              a_scale=None, b_scale=None):
+              a_scale=None, b_scale=None, sq_part=None):
     a = GemmArgs()
     a.dtype = dtype_code(A.dtype)
     a.c_dtype = dtype_code(C.dtype)
@@ -293,6 +293,7 @@ def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=N
     a.colsum_part = ptr(colsum_part)
     a.relu_mask = ptr(relu_mask)
     a.a_scale, a.b_scale = ptr(a_scale), ptr(b_scale)
+    a.sq_part = ptr(sq_part)
     return a
 
 

@@ -44,6 +44,7 @@ struct GemmParams {
   float* colsum_part;  // [ceil(M/128)][N]: column sums of C as stored (dReLU ring epilogue)
   uint64_t* relu_mask;  // ReLU-dropout keep&positive bits, ring epilogue layout (relu_mask_index)
   const float* a_scale; const float* b_scale;  // fp8: row scales of A [M] and of B [N]
+  float* sq_part;  // grouped f32 ring epilogue: sum of squares of C as stored, per (tile, wave) [tiles][8]
 };
 
 // Epilogue over a wave's MT x 4 grid of 16x16 accumulators whose origin is
@@ -604,7 +605,8 @@ NSTL_DEV void stage_half(const f32x16 (&acc)[4][2], int half, const GemmParams& 
 
 // SC: fp8 operands -- values come scaled by a_scale[row] (stage_half); times b_scale[col] here
 template <int EM, bool SC, typename ACC>
-NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, int lane, char* scr) {
+NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, int lane, char* scr,
+                       int sq_slot = 0) {
   constexpr bool F32OUT = EM == EM_F32 || EM == EM_WS;
   constexpr int ESZ = F32OUT ? 4 : 2;
   constexpr int CW = 16 / ESZ;   // columns per lane per store (8 bf16 / 4 f32)
@@ -646,6 +648,11 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
 #pragma unroll
   for (int e = 0; e < CW; ++e) csum[e] = 0.f;
   const bool rmask = (EM == EM_RELU_DROP || EM == EM_DRELU) && p.relu_mask != nullptr;
+  // f32 out (the weight gradients): sum of squares of the stored values, the
+  // clip norm's partial (clip_grad_norm_, utils/training_utils.py:73) without
+  // re-reading the gradient arena
+  const bool sq_on = EM == EM_F32 && p.sq_part != nullptr;
+  float ssq = 0.f;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
    const int ib = row0 + half * 64 + r0;
@@ -781,6 +788,11 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
 #pragma unroll
             for (int e = 0; e < CW; ++e) v[e] += p.beta * o[e % 4];
           }
+          if (sq_on) {
+#pragma unroll
+            for (int e = 0; e < CW; ++e)
+              if (vec || j + e < p.N) ssq += v[e] * v[e];
+          }
         }
         char* dst = C + ((int64_t)i * ldc + j) * ESZ;
         if (p.debug_skip_epilogue == 2) {  // NSTL_GEMM_DEBUG=skip_store: timing experiments only
@@ -812,6 +824,10 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
    }
    if (EM == EM_RELU_DROP && rmask && colok && ib < p.M) p.relu_mask[midx] = mword;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (sq_on) {
+    const double t = wave_sum_d((double)ssq);
+    if (lane == 0) p.sq_part[sq_slot] = (float)t;
   }
   if (csum_on) {
     // lanes l, l + LPR, ... share columns: fold them, then LPR lanes write the
@@ -1018,7 +1034,7 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz0, int kz1, char* sme
     char* scr = smem + wave * RING_EPI_WAVE;
     const int row0 = m0 + wm * 128, col0 = n0 + wn * 64;
     if (EM == EM_GENERIC) ring_epi_generic(p, acc, row0, col0, lane, scr);
-    else ring_epi<EM, false>(p, acc, row0, col0, lane, scr);
+    else ring_epi<EM, false>(p, acc, row0, col0, lane, scr, id * 8 + wave);
   }
 #ifdef NSTL_STAMPS
   NSTL_VMCNT(0);
@@ -1503,6 +1519,7 @@ int make_params(const nstl_gemm_args* a, GemmParams& p) {
   p.relu_mask = a->relu_mask;
   p.a_scale = a->a_scale;
   p.b_scale = a->b_scale;
+  p.sq_part = a->sq_part;
   return 0;
 }
 
@@ -1541,6 +1558,7 @@ bool big_ok(const nstl_gemm_args* a) {
 extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   GemmParams p;
   if (int rc = make_params(a, p)) return rc;
+  NSTL_CHECK_ARG(!a->sq_part, "nstl_gemm: sq_part is produced by nstl_gemm_grouped only");
   if (a->dtype == NSTL_FP8) return gemm_f8(a, p, (hipStream_t)stream);
   const int esz = a->dtype == NSTL_F32 ? 4 : 2;
 
@@ -1605,6 +1623,8 @@ extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream
   }
   const int em = ring_epi_mode(args, gp.g[0]);
   NSTL_CHECK_ARG(em == EM_F32 || em == EM_BF16, "nstl_gemm_grouped: f32 output, or bf16 without beta");
+  for (int g = 0; g < n; ++g)
+    NSTL_CHECK_ARG(!args[g].sq_part || em == EM_F32, "nstl_gemm_grouped: sq_part needs f32 output");
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(tiles), block(BIG_NT);
 #define NSTL_GROUP_LAUNCH(AKv, BKv)                                                                        \

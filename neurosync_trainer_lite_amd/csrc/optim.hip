@@ -115,6 +115,27 @@ __global__ __launch_bounds__(64) void clip_coef_kernel(const float* part, int n_
   }
 }
 
+// the same over many partials (the ring GEMM's per-(tile, wave) sums of squares
+// of the weight gradients + the rest of the arena's nstl_sumsq partials): one
+// 1024-thread block, double sums in a fixed order
+__global__ __launch_bounds__(1024) void clip_coef_many_kernel(const float* part, int n_part, float max_norm,
+                                                             float* coef, float* norm_out) {
+  __shared__ double red[16];
+  double s = 0;
+  for (int k = threadIdx.x; k < n_part; k += 1024) s += part[k];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    const float total = (float)sqrt(t);
+    const float c = max_norm / (total + 1e-6f);
+    coef[0] = c < 1.f ? c : 1.f;
+    if (norm_out) norm_out[0] = total;
+  }
+}
+
 // Adam with the coefficient read from device memory: no LDS, so its workgroups
 // fit on a CU beside a 160 KB ring-GEMM workgroup (the range updates that run
 // under the next forward, FusedAdam.overlap_next_forward)
@@ -296,9 +317,13 @@ extern "C" int nstl_adam_step(const nstl_adam_args* a, void* stream) {
 
 extern "C" int nstl_clip_coef(const float* partial, int n_partial, float max_norm, float* coef_out, float* norm_out,
                               void* stream) {
-  NSTL_CHECK_ARG(partial && coef_out && n_partial > 0 && n_partial <= 1024, "nstl_clip_coef: bad args");
-  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, partial, n_partial, max_norm,
-                     coef_out, norm_out);
+  NSTL_CHECK_ARG(partial && coef_out && n_partial > 0 && n_partial <= (1 << 20), "nstl_clip_coef: bad args");
+  if (n_partial <= 1024)
+    hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, partial, n_partial, max_norm,
+                       coef_out, norm_out);
+  else
+    hipLaunchKernelGGL(clip_coef_many_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, partial, n_partial,
+                       max_norm, coef_out, norm_out);
   NSTL_LAUNCH_CHECK("nstl_clip_coef");
   return 0;
 }

@@ -120,10 +120,12 @@ class _Buffers:
             self.dattn = e(M, D)
             self.dqkv = e(M, 3 * D)
             self.dq = e(M, D)
-            self.dkv = e(M, 2 * D)
-            # cross-attention k|v gradients of every decoder layer side by side: the
-            # memory gradient is then ONE GEMM over K = L * 2D (Engine.dmem_concat)
-            self.dkv_all = e(M, nl * 2 * D)
+            # cross-attention k|v gradients: with Engine.dmem_concat every decoder
+            # layer's side by side (the memory gradient is then ONE GEMM over
+            # K = L * 2D), else one layer's.  Only the active mode's buffer exists
+            # (dkv_all is 512 MB at the 228M shape); kv_grad() allocates on a switch.
+            self.dkv = None if eng.dmem_concat else e(M, 2 * D)
+            self.dkv_all = e(M, nl * 2 * D) if eng.dmem_concat else None
             self.dh = e(M, Fd)
             self.demb = e(M, D)
             self.dpred = torch.zeros(M, 64, dtype=dt, device=dev)
@@ -155,6 +157,17 @@ class _Buffers:
 
     def layer(self, lst, l):
         return lst[l if self.save else 0]
+
+    def kv_grad(self, eng, l):
+        """Decoder layer l's cross-attention k|v gradient buffer [M, 2D]."""
+        D = eng.D
+        if eng.dmem_concat:
+            if self.dkv_all is None:
+                self.dkv_all = torch.empty(self.M, eng.L * 2 * D, dtype=eng.dt, device=eng.device)
+            return self.dkv_all[:, 2 * D * l:2 * D * (l + 1)]
+        if self.dkv is None:
+            self.dkv = torch.empty(self.M, 2 * D, dtype=eng.dt, device=eng.device)
+        return self.dkv
 
 
 class Seq2SeqEngine:
@@ -221,6 +234,16 @@ class Seq2SeqEngine:
         self._fp8_w = None         # (weight name, rows) -> (e4m3 [rows*N, K], f32 scales [rows*N])
         self._fp8_act = {}         # M -> (e4m3 scratch [M, max(D, Fd)], scales [M], e4m3 mem, mem scales)
         self._xq = {}              # data_ptr of an activation -> its live e4m3 copy (q, scales)
+        # NSTL_FUSED_NORM=0: the clip norm re-reads the whole gradient arena
+        # (nstl_sumsq) instead of taking the grouped weight-gradient GEMMs' per-tile
+        # sums of squares (their epilogue, nstl_gemm_args.sq_part) plus nstl_sumsq
+        # over the rest of the arena (head, embedding, vectors: ~0.3 % of it)
+        self.fused_norm_on = os.environ.get("NSTL_FUSED_NORM", "1") != "0"
+        self._sq_buf = None        # f32 [tiles * 8] partials of the grouped dW launches
+        self._sq_used = 0
+        self._sq_ok = False
+        self.sq_state = None       # (g32._version, partial count) after a backward that produced them
+        self.sq_rest_partials = 64  # nstl_sumsq partials per norm_rest range (FusedAdam.step)
         self._red = None           # pending (part, ld, n_part, cols, out, beta) jobs
         self._ln_slot = 0          # next LayerNorm partial buffer of the layer
         self._ab_slot = 0          # next attention bias partial buffer of the layer
@@ -299,6 +322,17 @@ class Seq2SeqEngine:
             if named[n].dim() > 1:
                 hi = o + _pad64(k)
             self.end_of[n] = hi
+        # arena ranges whose gradients the grouped dW launches do NOT produce (the
+        # head and embedding weights take the split-K path; the vectors come from
+        # reductions): the fused clip norm runs nstl_sumsq over these only
+        lo = _pad64(named["decoder.fc_output.weight"].numel())
+        hi = self.offsets["encoder.embedding.weight"][0]
+        for n in mats:
+            o = self.offsets[n][0]
+            assert (lo <= o < hi) == (".transformer_" in n), n
+        self.norm_rest = [(0, lo), (hi, off)]
+        self.sq_tiles = sum(((named[n].shape[0] + 255) // 256) * ((named[n].shape[1] + 255) // 256)
+                            for n in mats if ".transformer_" in n)
         self.master_stale = False  # sharded optimizer: p32 matrices outside this rank's shard are old
         dev = self.device
         self.p32 = torch.zeros(off, dtype=torch.float32, device=dev)
@@ -590,6 +624,8 @@ class Seq2SeqEngine:
                 bname = wname.replace(".weight", ".bias")
                 K.colsum(dy, dy.stride(0), m, n, self.cur.col_part, self.gb(bname, rows), bf, stream=self.st)
             return
+        if ".transformer_" in wname:
+            self._sq_ok = False  # a layer weight gradient without the grouped epilogue's partials
         s = self.splits(n, k, m)
         st = self._side_begin()
         K.gemm(dy, x, G, n, k, m, a_kmajor=False, b_kmajor=False, beta=bf, split_k=s, workspace=ws, stream=st)
@@ -605,10 +641,17 @@ class Seq2SeqEngine:
         ok = all(self.dt == torch.bfloat16 and G.shape[0] >= 256 and G.shape[1] >= 256 and dy.shape[0] >= 256
                  and dy.shape[0] % 64 == 0 for dy, x, G, bf in jobs) and len(jobs) <= K.GEMM_GROUP_MAX
         if ok:
-            K.gemm_grouped([(dy, x, G, G.shape[0], G.shape[1], dy.shape[0],
-                             dict(a_kmajor=False, b_kmajor=False, beta=bf)) for dy, x, G, bf in jobs],
-                           stream=self.st)
+            probs = []
+            for dy, x, G, bf in jobs:
+                kw = dict(a_kmajor=False, b_kmajor=False, beta=bf)
+                if self._sq_ok:
+                    nt = ((G.shape[0] + 255) // 256) * ((G.shape[1] + 255) // 256) * 8
+                    kw["sq_part"] = self._sq_buf[self._sq_used:self._sq_used + nt]
+                    self._sq_used += nt
+                probs.append((dy, x, G, G.shape[0], G.shape[1], dy.shape[0], kw))
+            K.gemm_grouped(probs, stream=self.st)
             return
+        self._sq_ok = False
         for dy, x, G, bf in jobs:
             n, k = G.shape
             m = dy.shape[0]
@@ -945,6 +988,13 @@ class Seq2SeqEngine:
         self._dadd_pending = False
         self._red = None
         bf = 0.0 if self.grads_fresh else 1.0
+        self.sq_state = None
+        self._sq_ok = self.fused_norm_on and self.dt == torch.bfloat16 and self.grad_reducer is None
+        self._sq_used = 0
+        if self._sq_ok and self._sq_buf is None:
+            # + the rest-of-arena nstl_sumsq partials FusedAdam appends (sq_rest_partials per range)
+            self._sq_buf = torch.empty(self.sq_tiles * 8 + self.sq_rest_partials * len(self.norm_rest),
+                                       dtype=torch.float32, device=self.device)
         M, D, L = bb.M, self.D, self.L
         ws = bb.ws
         dres = bb.dres
@@ -998,6 +1048,17 @@ class Seq2SeqEngine:
         if red is not None:
             red.finish()
         self.grads_fresh = False
+        if self._sq_ok and self._sq_used == self.sq_tiles * 8:
+            self.sq_state = (self.g32._version, self._sq_used)
+
+    def take_sq_partials(self):
+        """The grouped dW launches' sums of squares of the last backward, if the
+        gradient arena is still what that backward left (torch bumps g32's version
+        on any in-place write through a p.grad view); consumed once."""
+        st, self.sq_state = self.sq_state, None
+        if st is None or st[0] != self.g32._version:
+            return None
+        return self._sq_buf[:st[1]]
 
     def _ready(self, red, upto):
         """Gradient arena prefix final: its all-reduce is ordered after both streams
@@ -1071,7 +1132,7 @@ class Seq2SeqEngine:
         self._dw(dyx, bb.d_oc[l], m + "out_linear.weight", 1, bf, ws, bias=False)
         self._dx(dyx, m + "out_linear.weight", 1, bb.dattn, 0.0)
         kvc = bb.d_kvc[l]
-        dkv = bb.dkv_all[:, 2 * D * l:2 * D * (l + 1)] if self.dmem_concat else bb.dkv
+        dkv = bb.kv_grad(self, l)
         fused = self._attn_bwd(bb.d_qc[l], kvc[:, :D], kvc[:, D:], bb.d_oc[l], bb.d_lsec[l], bb.dattn,
                                bb.dq, dkv[:, :D], dkv[:, D:], sd("xattn"), T, bb.B, mask=bb.d_maskc[l],
                                bias=[(0, D, self.gb(m + "q_linear.bias")), (D, 2 * D, self.gb(m + "k_linear.bias", 2))],

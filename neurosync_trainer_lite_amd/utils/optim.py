@@ -170,8 +170,22 @@ class FusedAdam(torch.optim.Optimizer):
             return loss
         if self._comm is None:
             eng.sync_pending()
-            sumsq_fn(eng.g32, self.partial)
-            adam_fn(0, eng.numel, eng.g32, self.partial)
+            sq = eng.take_sq_partials() if max_norm is not None else None
+            if sq is not None:
+                # the weight gradients' sums of squares came from the grouped dW
+                # epilogues; nstl_sumsq covers the rest of the arena (head, embedding,
+                # vectors), then one reduction gives the coefficient Adam reads
+                parts, rp = self._norm_parts(sq), eng.sq_rest_partials
+                o = sq.numel()
+                for lo, hi in eng.norm_rest:
+                    K.sumsq(eng.g32[lo:hi], hi - lo, parts[o:o + rp], rp, stream=st)
+                    o += rp
+                K.clip_coef(parts, o, max_norm, self.coef, self.norm, stream=st)
+                a.sumsq_partial, a.n_partial, a.norm_out, a.coef = None, 0, None, self.coef.data_ptr()
+                adam_fn(0, eng.numel, eng.g32, None)
+            else:
+                sumsq_fn(eng.g32, self.partial)
+                adam_fn(0, eng.numel, eng.g32, self.partial)
             self._snapshot_norm(max_norm)
             return loss
         from .. import parallel
@@ -183,6 +197,15 @@ class FusedAdam(torch.optim.Optimizer):
         self._moments_stale = True
         self._snapshot_norm(max_norm)
         return loss
+
+    def _norm_parts(self, sq):
+        """sq (the engine's dW partial buffer) followed by room for the rest-of-arena
+        partials, as one contiguous buffer (sq is a prefix view of it)."""
+        need = sq.numel() + self._engine.sq_rest_partials * len(self._engine.norm_rest)
+        base = sq._base if sq._base is not None else sq
+        if base.numel() < need or sq.data_ptr() != base.data_ptr():
+            raise RuntimeError("fused norm: partial buffer layout")
+        return base[:need]
 
     def _snapshot_norm(self, max_norm):
         # self.norm is one device word every step overwrites; callers that read a

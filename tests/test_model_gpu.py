@@ -399,3 +399,49 @@ def test_update_overlapped_with_next_forward_is_identical(amp):
     assert torch.equal(m0, m1) and torch.equal(v0, v1)
     for k in sd0:
         assert torch.equal(sd0[k], sd1[k]), k
+
+
+@pytest.mark.parametrize("steps", [1, 2])
+def test_fused_clip_norm_matches_arena_sumsq(monkeypatch, steps):
+    """The clip norm from the grouped dW epilogues' per-tile sums of squares plus
+    nstl_sumsq over the rest of the arena (NSTL_FUSED_NORM=1, default) equals the
+    norm of the gradients as stored (float64 on the host) and the arena re-read
+    (NSTL_FUSED_NORM=0); the update then agrees to f32 rounding of the clip
+    coefficient.  steps=2 accumulates two backwards (beta = 1 in the grouped
+    GEMMs) before the step.  An in-place write to a p.grad view invalidates the
+    partials (torch's version counter), and the step falls back to the re-read."""
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("NSTL_FUSED_NORM", fused)
+        cfg, model, crit, opt, params = make(256, 4, 2, 11, amp=True, dropout=0.0)
+        g = torch.Generator().manual_seed(6)
+        src = torch.randn(4, 128, 256, generator=g).to(DEV)
+        trg = (torch.randn(4, 128, 61, generator=g) * 20).to(DEV)
+        model.train()
+        opt.zero_grad()
+        for _ in range(steps):
+            crit(model(src), trg).backward()
+        eng = opt._bind()
+        assert (eng.sq_state is not None) == (fused == "1")
+        ref = torch.cat([p.grad.detach().double().flatten().cpu() for p in model.parameters()]).norm().item()
+        opt.step(max_norm=0.5)  # clipping active
+        torch.cuda.synchronize()
+        assert eng.sq_state is None
+        norm = opt.last_norm.item()
+        assert abs(norm - ref) <= 1e-5 * ref, (fused, norm, ref)
+        out.append((norm, {k: p.detach().double().cpu().clone() for k, p in model.named_parameters()}))
+    assert abs(out[0][0] - out[1][0]) <= 1e-5 * out[1][0]
+    for k in out[0][1]:
+        assert (out[0][1][k] - out[1][1][k]).abs().max().item() < 1e-6, k
+    # an in-place edit of a gradient after backward: the step re-reads the arena
+    monkeypatch.setenv("NSTL_FUSED_NORM", "1")
+    cfg, model, crit, opt, params = make(256, 4, 2, 11, amp=True, dropout=0.0)
+    opt.zero_grad()
+    crit(model(src), trg).backward()
+    eng = opt._bind()
+    assert eng.sq_state is not None
+    w = model.decoder.transformer_decoder[0].ffn.linear1.weight
+    w.grad.mul_(3.0)
+    ref = torch.cat([p.grad.detach().double().flatten().cpu() for p in model.parameters()]).norm().item()
+    opt.step(max_norm=0.5)
+    assert abs(opt.last_norm.item() - ref) <= 1e-5 * ref
