@@ -93,8 +93,8 @@ def test_data_parallel_gloo(tmp_path, monkeypatch):
         torch.testing.assert_close(a[k], v, rtol=1e-5, atol=1e-6)
 
 
-def _shard_worker(rank, port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+def _shard_worker(rank, port, out_dir, world=WORLD):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     from neurosync_trainer_lite_amd import parallel
@@ -102,7 +102,7 @@ def _shard_worker(rank, port, out_dir):
     ns = 64 * 840  # one ARENA_ALIGN unit: splits for 1..8 ranks
     n = ns + 192   # + a replicated tail (the arena's f32 vectors)
     comm = parallel.ShardComm(ns)
-    assert (comm.shard, comm.lo) == (ns // WORLD, rank * ns // WORLD)
+    assert (comm.shard, comm.lo) == (ns // world, rank * ns // world)
     g = torch.Generator().manual_seed(1)
     p = torch.randn(n, generator=g)
     m, v = torch.zeros(n), torch.zeros(n)
@@ -128,19 +128,22 @@ def _shard_worker(rank, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_sharded_optimizer_step_gloo(tmp_path):
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_optimizer_step_gloo(tmp_path, world):
     """ZeRO-1 orchestration (parallel.ShardComm / zero1_step, the FusedAdam
     sharded path with CPU stand-ins for the two kernels): reduce-scatter, global
     norm from per-shard partial sums, Adam on each shard, all-gather -- equal to
-    one process clipping and stepping the summed gradient."""
-    mp.spawn(_shard_worker, args=(_port(), str(tmp_path)), nprocs=WORLD, join=True)
-    r0 = torch.load(tmp_path / "s0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "s1.pt", weights_only=True)
-    for k in r0:
-        torch.testing.assert_close(r0[k], r1[k], rtol=0, atol=0)
+    one process clipping and stepping the summed gradient, at the 2 / 4 / 8 ranks
+    of the scaling runs (the arena's ARENA_ALIGN unit splits evenly for each)."""
+    mp.spawn(_shard_worker, args=(_port(), str(tmp_path), world), nprocs=world, join=True)
+    res = [torch.load(tmp_path / ("s%d.pt" % r), weights_only=True) for r in range(world)]
+    r0 = res[0]
+    for rr in res[1:]:
+        for k in r0:
+            torch.testing.assert_close(r0[k], rr[k], rtol=0, atol=0)
     n = 64 * 840 + 192
     p = torch.randn(n, generator=torch.Generator().manual_seed(1))
-    gsum = sum(torch.randn(n, generator=torch.Generator().manual_seed(10 + r)) * (r + 1) for r in range(WORLD))
+    gsum = sum(torch.randn(n, generator=torch.Generator().manual_seed(10 + r)) * (r + 1) for r in range(world))
     coef = min(1.0, 2.0 / (float((gsum.double() ** 2).sum()) ** 0.5 + 1e-6))
     gg = gsum * coef + 1e-5 * p
     m, v = 0.1 * gg, 0.001 * gg * gg
