@@ -152,6 +152,22 @@ NSTL_DEV void nstl_keep2(uint64_t seed, uint64_t idx, uint32_t thresh, bool& k0,
   k0 = (h & 0xFFFFu) >= thresh;
   k1 = (h >> 16) >= thresh;
 }
+// The same hash with the index already in 32-bit pair form.  For element
+// indices below 2^33 (hi == 0 above) nstl_pair_hash(seed, idx) ==
+// nstl_pair_hash32(nstl_seed_term(seed), idx >> 1): identical masks, but a hot
+// loop then forms its pair indices with 32-bit adds instead of 64-bit element
+// indices, shifts and the high-word fold (the attention forward built its 16
+// hashes per lane from ~18 vector instructions each, the fmix being 8 of them).
+// Launchers that use it check nstl_pair_index32_ok on the tensor's element count.
+NSTL_DEV uint32_t nstl_seed_term(uint64_t seed) { return (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x27D4EB2Fu); }
+NSTL_DEV uint32_t nstl_pair_hash32(uint32_t seed_term, uint32_t pair) { return nstl_fmix32(pair ^ seed_term); }
+NSTL_DEV void nstl_keep2_32(uint32_t seed_term, uint32_t pair, uint32_t thresh, bool& k0, bool& k1) {
+  const uint32_t h = nstl_pair_hash32(seed_term, pair);
+  k0 = (h & 0xFFFFu) >= thresh;
+  k1 = (h >> 16) >= thresh;
+}
+static inline bool nstl_pair_index32_ok(uint64_t elements) { return elements <= (1ull << 33); }
+
 // threshold on a 16-bit uniform; 0 = no dropout
 static inline uint32_t nstl_drop_thresh(float p) {
   double t = (double)p * 65536.0 + 0.5;

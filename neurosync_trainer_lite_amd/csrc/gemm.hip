@@ -638,6 +638,7 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
     for (int e = 0; e < CW; ++e) bias[e] = j + e < p.N ? p.bias[j + e] : 0.f;
   }
   const bool rope_col = EM == EM_ROPE && j < p.rope_cols;
+  const uint32_t seed_term = nstl_seed_term(p.seed);
   const int rhalf = p.rope_dim >> 1;
   // cos/sin of 8 columns = 4 consecutive table entries (16 B) when rope_dim % 8 == 0
   const bool rope_vec = (p.rope_dim & 7) == 0;
@@ -743,11 +744,12 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
 #pragma unroll
           for (int e = 0; e < CW; ++e) v[e] = fmaxf(v[e], 0.f);
           if (p.thresh) {
-            const uint64_t idx = (uint64_t)i * p.N + j;  // even: N even, j % 8 == 0
+            // pair index of element (i, j): N even, j % 8 == 0; 32-bit (launcher check)
+            const uint32_t pair = (uint32_t)i * (uint32_t)(p.N >> 1) + (uint32_t)(j >> 1);
 #pragma unroll
             for (int e = 0; e < CW; e += 2) {
               bool k0, k1;
-              nstl_keep2(p.seed, idx + e, p.thresh, k0, k1);
+              nstl_keep2_32(seed_term, pair + (e >> 1), p.thresh, k0, k1);
               v[e] = k0 ? v[e] * p.inv_keep : 0.f;
               v[e + 1] = k1 ? v[e + 1] * p.inv_keep : 0.f;
             }
@@ -1497,6 +1499,8 @@ int make_params(const nstl_gemm_args* a, GemmParams& p) {
   }
   if (a->epilogue == NSTL_EPI_DRELU_DROP) NSTL_CHECK_ARG(a->aux != nullptr, "nstl_gemm: aux missing");
   NSTL_CHECK_ARG(a->p_drop >= 0.f && a->p_drop < 1.f, "nstl_gemm: p_drop out of range");
+  NSTL_CHECK_ARG(a->p_drop == 0.f || nstl_pair_index32_ok((uint64_t)a->M * a->N),
+                 "nstl_gemm: M*N past 2^33 dropout elements (32-bit pair index)");
 
   p.A = (const char*)a->A; p.lda = a->lda;
   p.B = (const char*)a->B; p.ldb = a->ldb;

@@ -69,10 +69,12 @@ struct LnParams {
 };
 
 // dropout scale of the element pair (idx, idx+1), idx even: 1 or 2 stacked masks
+// (32-bit pair index idx / 2: the launcher checks rows * D <= 2^33)
 NSTL_DEV void branch_scale2(const LnParams& p, uint64_t idx, float& m0, float& m1) {
   bool a0, a1, b0 = true, b1 = true;
-  nstl_keep2(p.seed1, idx, p.thresh, a0, a1);
-  if (p.n_masks >= 2) nstl_keep2(p.seed2, idx, p.thresh, b0, b1);
+  const uint32_t pair = (uint32_t)(idx >> 1);
+  nstl_keep2_32(nstl_seed_term(p.seed1), pair, p.thresh, a0, a1);
+  if (p.n_masks >= 2) nstl_keep2_32(nstl_seed_term(p.seed2), pair, p.thresh, b0, b1);
   const float s = p.n_masks >= 2 ? p.inv_keep * p.inv_keep : p.inv_keep;
   m0 = (a0 && b0) ? s : 0.f;
   m1 = (a1 && b1) ? s : 0.f;
@@ -543,6 +545,8 @@ int fill(LnParams& p, const nstl_ln_args* a) {
   NSTL_CHECK_ARG(a->rows > 0 && a->D > 0 && a->D % 64 == 0 && a->D <= 1024, "nstl_ln: bad shape");
   NSTL_CHECK_ARG(a->gamma && a->beta, "nstl_ln: gamma/beta missing");
   NSTL_CHECK_ARG(a->n_masks >= 0 && a->n_masks <= 2 && a->p_drop >= 0.f && a->p_drop < 1.f, "nstl_ln: dropout");
+  NSTL_CHECK_ARG(a->p_drop == 0.f || nstl_pair_index32_ok((uint64_t)a->rows * a->D),
+                 "nstl_ln: rows*D past 2^33 dropout elements (32-bit pair index)");
   p.x = (const char*)a->x; p.y = (const char*)a->y;
   p.rows = a->rows; p.D = a->D;
   p.n_masks = a->n_masks;

@@ -41,7 +41,7 @@ extra = {}
 mask = None
 if os.environ.get("NSTL_ATTN_MASK", "1") == "1":   # stored keep bits (0: re-hash in backward)
     mask = torch.empty(B * H * T * T // 8, dtype=torch.uint8, device=dev)
-for p in (0.3, 0.0):
+for p in [float(x) for x in os.environ.get("NSTL_BENCH_P", "0.3,0.0").split(",")]:
     def args():
         a = K.attn_args(K.BF16, B, T, H, qkv.data_ptr(), 3 * D, qkv[:, D:].data_ptr(), 3 * D,
                         qkv[:, 2 * D:].data_ptr(), 3 * D, o.data_ptr(), D, lse.data_ptr(), p, 77)

@@ -1,5 +1,6 @@
-"""Per-kernel mean of SQ counters over the GEMM dispatches of a rocprofv3 --pmc run.
-  python tools/pmc_gemm_counters.py <dir>"""
+"""Per-kernel mean of SQ counters over the GEMM (or other: 2nd argument, a name
+substring) dispatches of a rocprofv3 --pmc run.
+  python tools/pmc_gemm_counters.py <dir> [name-filter]"""
 import csv
 import glob
 import os
@@ -7,11 +8,12 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
+flt = sys.argv[2] if len(sys.argv) > 2 else "gemm"
 vals = defaultdict(lambda: defaultdict(dict))
 for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        if "gemm" not in n:
+        if flt not in n:
             continue
         k = int(r["Dispatch_Id"])
         c = r["Counter_Name"]
