@@ -53,6 +53,11 @@ struct AttnParams {
 // 2^-126 is 0 either way)
 NSTL_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+template <int N>
+NSTL_DEV void vmcnt_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // LDS-DMA rows [0, nrows) of a (b, h) slice (64 elements per row) into an
 // ImgK<RB> image.  One wave instruction moves 1 KB = 1024/RB rows; the image
 // swizzle is applied to the per-lane source chunk.
@@ -184,53 +189,84 @@ NSTL_DEV void store_tile16x64(const float (&v)[4][4], char* scr, char* gbase, in
 // dropout, then O = P V with P taken from the score registers (acc_frag).
 constexpr int FWD_NT = 512, FWD_QB = 16 * FWD_NT / 64;
 
-// NKT = T/16 key tiles (score registers sized to T); T <= 128: 6 waves per SIMD (3
-// workgroups per CU) without spills; longer T: 4 / 3
-template <typename T, int NKT>
-__global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void attn_fwd_kernel(AttnParams p) {
+// One wave's 16 queries q0 .. q0+15 of head bh (tokens from tok0, head column
+// h*DH) against all keys of the K / V images: scores, exact softmax, dropout
+// (keep bits to p.mask), O and the LSE.  fq: the wave's Q fragments.
+// ImgK<128> fragment reads as inline asm (bf16): with a prefetch DMA in flight
+// into the other buffer the compiler would put vmcnt(0) in front of its own LDS
+// reads (it cannot tell the images apart), draining the prefetch; the caller
+// orders them with an explicit lgkmcnt(0) + sched_barrier before the MFMAs.
+NSTL_DEV uint32_t lds_addr(const char* p) { return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p; }
+typedef int i32x4a __attribute__((ext_vector_type(4)));
+typedef int i32x2a __attribute__((ext_vector_type(2)));
+NSTL_DEV void asm_row128(bf16x8& f, const char* img, int row, int r) {
+  i32x4a v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(img + ImgK<128>::off(row, r * 2))));
+  f = __builtin_bit_cast(bf16x8, v);
+}
+NSTL_DEV void asm_col2_128(bf16x8& f, const char* img, int col16, int r0, int lane) {  // frag_col2<ImgK<128>>
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int byte = (col16 + 4 * pp) * 2;
+  i32x2a v0, v1;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v0) : "v"(lds_addr(img + ImgK<128>::off(r0 + 4 * g + q, byte))));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v1) : "v"(lds_addr(img + ImgK<128>::off(r0 + 16 + 4 * g + q, byte))));
+  const bf16x4 b0 = __builtin_bit_cast(bf16x4, v0), b1 = __builtin_bit_cast(bf16x4, v1);
+  f = (bf16x8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+}
+NSTL_DEV void lgkm_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+struct NoHook {
+  NSTL_DEV void operator()() const {}
+};
+
+// AR: the Q fragments come from the wave's 16-row Q image Qw (ImgK<128>) and
+// every K / V / Q fragment read is inline asm (bf16 only; the persistent kernel);
+// after_qk() runs once the wave is done with its Q image (the S products)
+template <typename T, int NKT, bool AR = false, typename Hook = NoHook>
+NSTL_DEV void fwd_queries(const AttnParams& p, const char* Kimg, const char* Vimg,
+                          const typename FragT<T>::type (&fq_in)[2], const char* Qw, int bh, int h, int64_t tok0,
+                          int q0, int lane, Hook after_qk = Hook()) {
   typedef typename FragT<T>::type Frag;
-  constexpr int ESZ = (int)sizeof(T);
-  constexpr int RBK = DH * ESZ;   // 128 (bf16) / 256 (f32)
+  constexpr int RBK = DH * (int)sizeof(T);
   typedef ImgK<RBK> Img;
-  constexpr int NW = FWD_NT / 64;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int T_ = p.T;
   constexpr int nkt = NKT;
-  char* Kimg = smem;
-  char* Vimg = Kimg + T_ * RBK;
-
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
-  const int qb0 = blockIdx.x * FWD_QB;
-  const int nq = min(FWD_QB, T_ - qb0);
-  const int64_t tok0 = (int64_t)b * T_;
-
-  dma_rows<RBK, NW>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
-  dma_rows<RBK, NW>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
-  const int q0 = qb0 + w * 16;  // this wave's first query
-  const bool act = w * 16 < nq;
-  Frag fq[2];
-  if (act) {
-    const T* qrow = (const T*)p.q + (tok0 + q0 + c) * p.q_ld + h * DH;
-    gload_frag<T>(fq[0], qrow, 8 * g);
-    gload_frag<T>(fq[1], qrow, 32 + 8 * g);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (!act) return;
-
+  const int T_ = p.T, g = lane >> 4, c = lane & 15;
   // s[kt][r] = score(query q0 + c, key 16kt + 4g + r)
   f32x4 s[NKT];
+  if constexpr (AR) {
+    static_assert(sizeof(T) == 2 && NKT % 2 == 0, "asm reads: bf16");
+    Frag fq[2];
+    asm_row128(fq[0], Qw, c, 8 * g);
+    asm_row128(fq[1], Qw, c, 32 + 8 * g);
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-    s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (kt < nkt) {
-      Frag fk;
-      frag_row<Img>(fk, Kimg, kt * 16 + c, 8 * g);
-      mma16(s[kt], fk, fq[0]);
-      frag_row<Img>(fk, Kimg, kt * 16 + c, 32 + 8 * g);
-      mma16(s[kt], fk, fq[1]);
+    for (int kt = 0; kt < NKT; kt += 2) {  // two key tiles (4 reads) per wait
+      Frag fk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) asm_row128(fk[u], Kimg, (kt + (u >> 1)) * 16 + c, 32 * (u & 1) + 8 * g);
+      lgkm_fence();
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        s[kt + u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        mma16(s[kt + u], fk[2 * u], fq[0]);
+        mma16(s[kt + u], fk[2 * u + 1], fq[1]);
+      }
+    }
+    after_qk();
+  } else {
+    const Frag(&fq)[2] = fq_in;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      s[kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (kt < nkt) {
+        Frag fk;
+        frag_row<Img>(fk, Kimg, kt * 16 + c, 8 * g);
+        mma16(s[kt], fk, fq[0]);
+        frag_row<Img>(fk, Kimg, kt * 16 + c, 32 + 8 * g);
+        mma16(s[kt], fk, fq[1]);
+      }
     }
   }
   const float c2 = p.scale * LOG2E;
@@ -259,12 +295,14 @@ __global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void at
     // kt*4 + r takes it by v_writelane (the select-by-lane-index form cost ~7
     // vector instructions per ballot).
     const int q = q0 + c;
-    const uint64_t row = drop_idx(bh, T_, q, 4 * g);
+    // pair index of drop_idx(bh, T, q, 4g) (even): 32-bit, checked by the launcher
+    const uint32_t pair0 = ((uint32_t)bh * T_ + q) * (uint32_t)(T_ >> 1) + 2 * g;
+    const uint32_t st = nstl_seed_term(p.seed);
     uint32_t mlo = 0, mhi = 0;  // lane kt*4 + r: keep bits of (kt, r)
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       if (kt < nkt) {
-        const uint32_t h0 = nstl_pair_hash(p.seed, row + kt * 16), h1 = nstl_pair_hash(p.seed, row + kt * 16 + 2);
+        const uint32_t h0 = nstl_pair_hash32(st, pair0 + kt * 8), h1 = nstl_pair_hash32(st, pair0 + kt * 8 + 1);
         const bool k[4] = {(h0 & 0xFFFFu) >= p.thresh, (h0 >> 16) >= p.thresh, (h1 & 0xFFFFu) >= p.thresh,
                            (h1 >> 16) >= p.thresh};
 #pragma unroll
@@ -290,11 +328,20 @@ __global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void at
 #pragma unroll
   for (int j = 0; j < NKT / 2; ++j) {
     const Frag fp = acc_frag<T>(s[2 * j], s[2 * j + 1]);
+    if constexpr (AR) {
+      Frag fv[4];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      Frag fv;
-      frag_col2<Img>(fv, Vimg, dt * 16, 32 * j, lane);
-      mma16(o[dt], fv, fp);
+      for (int dt = 0; dt < 4; ++dt) asm_col2_128(fv[dt], Vimg, dt * 16, 32 * j, lane);
+      lgkm_fence();
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) mma16(o[dt], fv[dt], fp);
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        Frag fv;
+        frag_col2<Img>(fv, Vimg, dt * 16, 32 * j, lane);
+        mma16(o[dt], fv, fp);
+      }
     }
   }
   // normalise (dropout's 1/(1-p) applied to O instead of P) and store
@@ -303,6 +350,138 @@ __global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void at
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) store4<T>(orow + 16 * dt, o[dt] * inv);
   if (g == 0) p.lse[(int64_t)bh * T_ + q0 + c] = m * p.scale + logf(sum);
+}
+
+// NKT = T/16 key tiles (score registers sized to T); T <= 128: 6 waves per SIMD (3
+// workgroups per CU) without spills; longer T: 4 / 3
+template <typename T, int NKT>
+__global__ __launch_bounds__(FWD_NT, NKT <= 8 ? 6 : (NKT <= 12 ? 4 : 3)) void attn_fwd_kernel(AttnParams p) {
+  typedef typename FragT<T>::type Frag;
+  constexpr int ESZ = (int)sizeof(T);
+  constexpr int RBK = DH * ESZ;   // 128 (bf16) / 256 (f32)
+  constexpr int NW = FWD_NT / 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int T_ = p.T;
+  char* Kimg = smem;
+  char* Vimg = Kimg + T_ * RBK;
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int qb0 = blockIdx.x * FWD_QB;
+  const int nq = min(FWD_QB, T_ - qb0);
+  const int64_t tok0 = (int64_t)b * T_;
+
+  dma_rows<RBK, NW>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * ESZ, p.k_ld * ESZ, T_, w, lane);
+  dma_rows<RBK, NW>(Vimg, p.v + (tok0 * p.v_ld + h * DH) * ESZ, p.v_ld * ESZ, T_, w, lane);
+  const int q0 = qb0 + w * 16;  // this wave's first query
+  const bool act = w * 16 < nq;
+  Frag fq[2];
+  if (act) {
+    const T* qrow = (const T*)p.q + (tok0 + q0 + c) * p.q_ld + h * DH;
+    gload_frag<T>(fq[0], qrow, 8 * g);
+    gload_frag<T>(fq[1], qrow, 32 + 8 * g);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!act) return;
+  fwd_queries<T, NKT>(p, Kimg, Vimg, fq, nullptr, bh, h, tok0, q0, lane);
+}
+
+// Persistent form for the production shape (bf16, T = 128: one workgroup's 8
+// waves cover a head's 128 queries).  The one-shot grid above runs 2048 (b, h)
+// workgroups, 3 per CU, each of which loads its K / V / Q, waits, computes and
+// stores: every workgroup pays a full memory latency with nothing of its own to
+// overlap, and the 2.7 rounds of workgroups leave the last one a third empty.
+// Here a grid of 2 workgroups per CU walks the heads (item = blockIdx.x + i * G)
+// with two K / V image buffers and one Q image (2 KB per wave), all filled by
+// LDS-DMA: the next head's K / V are issued before the current head is
+// computed, a wave's next Q rows as soon as its S products no longer need its
+// Q image, and the O / LSE / keep-bit stores stay in flight across the next
+// head's wait (the counted vmcnt retires only the loads issued before them).
+// No operand goes to VGPRs by a load the compiler tracks, so it adds no wait
+// of its own.  LDS: 2 x 32 KB + 16 KB = 80 KB, two workgroups per CU.
+// Per wave and head: 4 K / V + 2 Q DMA, 4 O + 1 LSE (+ 1 keep-bit word with
+// MK) stores.
+constexpr int PF_T = 128, PF_IMG = PF_T * DH * 2, PF_KV = 4;
+constexpr size_t PF_LDS = 2 * 2 * (size_t)PF_IMG + 8 * 2048;
+// raw barrier: __syncthreads() would also wait for every outstanding memory
+// operation (vmcnt(0)), i.e. for the next head's prefetch
+NSTL_DEV void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+NSTL_DEV void dma1k(const char* src, char* dst) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+}
+template <bool MK>
+__global__ __launch_bounds__(FWD_NT, 4) void attn_fwd_persist_kernel(AttnParams p, int nitems) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PF_STORES = MK ? 6 : 5;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x;
+  char* const Qw = smem + 4 * PF_IMG + w * 2048;
+  // per-lane byte offsets inside a head's slab, once (ImgK<128> swizzle on the
+  // source chunk, as dma_rows): the wave's two 1 KB pieces of the K and V
+  // images (rows 8(w + 8u) ..) and of its own Q rows (16w + 8u ..)
+  uint32_t offk[2], offv[2], offq[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = (w + 8 * u) * 8 + (lane >> 3), lc = (lane & 7) ^ ((row >> 1) & 7);
+    offk[u] = (uint32_t)(row * p.k_ld * 2 + lc * 16);
+    offv[u] = (uint32_t)(row * p.v_ld * 2 + lc * 16);
+    const int qr = 8 * u + (lane >> 3), qc = (lane & 7) ^ ((qr >> 1) & 7);
+    offq[u] = (uint32_t)((w * 16 + qr) * p.q_ld * 2 + qc * 16);
+  }
+  auto head = [&](int it, const char* base, int64_t ld) {
+    const int b = it / p.H, h = it % p.H;
+    return base + ((int64_t)b * PF_T * ld + h * DH) * 2;
+  };
+  auto issue_kv = [&](int it, int buf) {
+    const char* kb = head(it, p.k, p.k_ld);
+    const char* vb = head(it, p.v, p.v_ld);
+    char* img = smem + buf * 2 * PF_IMG;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      dma1k(kb + offk[u], img + (w + 8 * u) * 1024);
+      dma1k(vb + offv[u], img + PF_IMG + (w + 8 * u) * 1024);
+    }
+  };
+  auto issue_q = [&](int it) {
+    const char* qb = head(it, p.q, p.q_ld);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) dma1k(qb + offq[u], Qw + u * 1024);
+  };
+  int it = blockIdx.x;
+  if (it >= nitems) return;
+  issue_kv(it, 0);
+  issue_q(it);
+  const bf16x8 nofq[2] = {};
+  for (int i = 0; it < nitems; ++i, it += G) {
+    const int buf = i & 1;
+    const bool next = it + G < nitems;
+    if (next) issue_kv(it + G, buf ^ 1);  // buffer of head i-1: free since the barrier ending it
+    // retire head i's K / V / Q: younger are head i-1's stores (i > 0) and head i+1's K / V
+    if (i == 0) {
+      if (next) vmcnt_wait<PF_KV>();
+      else vmcnt_wait<0>();
+    } else {
+      if (next) vmcnt_wait<PF_KV + PF_STORES>();
+      else vmcnt_wait<PF_STORES>();
+    }
+    raw_barrier();  // every wave's DMA share of head i has landed
+    const int b = it / p.H, h = it % p.H;
+    const char* img = smem + buf * 2 * PF_IMG;
+    auto after_qk = [&]() {
+      if (next) issue_q(it + G);  // this wave's own Q image: no other wave reads it
+    };
+    fwd_queries<bf16, PF_T / 16, true>(p, img, img + PF_IMG, nofq, Qw, it, h, (int64_t)b * PF_T, w * 16, lane,
+                                       after_qk);
+    raw_barrier();  // every wave is done reading buffer `buf`
+  }
 }
 
 // RoPE^T: rotate (row t, col d) accumulator elements back by -theta
@@ -1193,16 +1372,40 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   p.thresh = nstl_drop_thresh(a->p_drop);
   p.inv_keep = 1.0f / (1.0f - a->p_drop);
   p.seed = a->seed;
+  NSTL_CHECK_ARG(!p.thresh || nstl_pair_index32_ok((uint64_t)a->B * a->H * a->T * a->T),
+                 "nstl_attn: B*H*T*T past 2^33 dropout elements (32-bit pair index)");
   return 0;
 }
 
-template <typename K>
-int launch(K kern, dim3 grid, size_t lds, hipStream_t st, const AttnParams& p, const char* what, int nt = NT) {
+template <typename K, typename... X>
+int launch(K kern, dim3 grid, size_t lds, hipStream_t st, const AttnParams& p, const char* what, int nt = NT,
+           X... extra) {
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return nstl::fail((int)e, "%s: LDS request %zu: %s", what, lds, hipGetErrorString(e));
-  hipLaunchKernelGGL(kern, grid, dim3(nt), lds, st, p);
+  hipLaunchKernelGGL(kern, grid, dim3(nt), lds, st, p, extra...);
   NSTL_LAUNCH_CHECK(what);
   return 0;
+}
+
+// compute units of the current device (the persistent grid's size)
+int cu_count() {
+  static int n[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+
+// the persistent forward (bf16, T = 128, enough heads to fill the grid);
+// NSTL_ATTN_FWD=oneshot selects the one-workgroup-per-head kernel (A/B; read per call)
+bool use_persist_fwd(const nstl_attn_args* a) {
+  const char* e = getenv("NSTL_ATTN_FWD");
+  if (e && e[0] == 'o') return false;
+  return a->dtype == NSTL_BF16 && a->T == PF_T && a->dh == DH;
 }
 
 // the split backward: dQ (also writes D = rowsum(dO * O)), then dK / dV
@@ -1230,6 +1433,14 @@ extern "C" int nstl_attn_fwd(const nstl_attn_args* a, void* stream) {
     return launch(attn_fwd_generic<float>, grid, lds, st, p, "nstl_attn_fwd generic");
   }
   nstl::count(NSTL_K_ATTN_FWD);
+  if (use_persist_fwd(a)) {
+    const int nitems = a->B * a->H;
+    const int G = std::min(nitems, 2 * cu_count());
+    const size_t lds = PF_LDS;
+    if (p.thresh && p.mask)
+      return launch(attn_fwd_persist_kernel<true>, dim3(G), lds, st, p, "nstl_attn_fwd persistent", FWD_NT, nitems);
+    return launch(attn_fwd_persist_kernel<false>, dim3(G), lds, st, p, "nstl_attn_fwd persistent", FWD_NT, nitems);
+  }
   dim3 grid((a->T + FWD_QB - 1) / FWD_QB, a->B * a->H);
   const size_t lds = fwd_lds_bytes(a->T, esz);
   // T % 32 == 0 and T <= 256 on this path: NKT in {2, 4, ..., 16}

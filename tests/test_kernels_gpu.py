@@ -375,6 +375,35 @@ def test_attention_stored_mask_bits(dt, T):
     assert abs(frac - (1 - p)) < 0.01, frac
 
 
+@pytest.mark.parametrize("B,H,p,stored", [(2, 3, 0.3, True), (65, 16, 0.3, True), (128, 16, 0.3, True),
+                                          (65, 16, 0.0, False), (65, 16, 0.3, False)])
+def test_attention_fwd_persistent_matches_oneshot(B, H, p, stored, monkeypatch):
+    """The persistent forward (bf16, T=128: heads walked by 2 workgroups per CU with
+    the next head's K / V / Q prefetched by LDS-DMA) against the one-workgroup-per-head
+    kernel: O, LSE and the stored keep bits bit-identical.  B*H = 6 (fewer heads than
+    workgroups), 1040 (some workgroups take 3 heads, others 2) and 2048 (the 228M step)."""
+    T, dh = 128, 64
+    M, D = B * T, H * dh
+    qkv = rnd(M, 3 * D, dtype=torch.bfloat16, scale=0.5, seed=95)
+    outs = []
+    for mode in ("oneshot", "persist"):
+        monkeypatch.setenv("NSTL_ATTN_FWD", mode)
+        o = torch.full((M, D), float("nan"), dtype=torch.bfloat16, device=DEV)
+        lse = torch.full((B * H * T,), float("nan"), dtype=torch.float32, device=DEV)
+        mask = torch.full((B * H * T * T // 64,), -1, dtype=torch.int64, device=DEV)
+        a = K.attn_args(K.BF16, B, T, H, qkv.data_ptr(), 3 * D, qkv[:, D:].data_ptr(), 3 * D,
+                        qkv[:, 2 * D:].data_ptr(), 3 * D, o.data_ptr(), D, lse.data_ptr(), p, 1234, dh=dh)
+        if stored:
+            a.mask_bits = mask.data_ptr()
+        K.attn_fwd(a)
+        torch.cuda.synchronize()
+        outs.append((o, lse, mask))
+    assert not torch.isnan(outs[1][0].float()).any() and not torch.isnan(outs[1][1]).any()
+    assert torch.equal(outs[0][0], outs[1][0]), "O"
+    assert torch.equal(outs[0][1], outs[1][1]), "LSE"
+    assert torch.equal(outs[0][2], outs[1][2]), "keep bits"
+
+
 @pytest.mark.parametrize("dt,T", [(torch.bfloat16, 128), (torch.bfloat16, 64), (torch.bfloat16, 256),
                                   (torch.float32, 96)])
 def test_attention_bias_partials(dt, T):
