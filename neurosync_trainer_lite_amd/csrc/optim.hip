@@ -376,6 +376,25 @@ extern "C" int nstl_colsum(int dtype, const void* x, int64_t ld, int rows, int c
   return 0;
 }
 
+// Column j of rows rg, rg + 16, rg + 32, ... of a [n_part][ld] f32 matrix, summed in
+// that order (the order reduce_rows3 / reduce_batch have always used, so results
+// are unchanged), with the loads of 8 rows issued before their adds: the plain
+// loop waited one memory latency per row (latency-bound: ~11 us for a decoder
+// layer's 12 MB of partials).
+NSTL_DEV float strided_col_sum(const float* pm, int64_t ld, int n_part, int rg, int j) {
+  float s = 0.f;
+  int k = rg;
+  for (; k + 7 * 16 < n_part; k += 8 * 16) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = pm[(int64_t)(k + 16 * u) * ld + j];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; k < n_part; k += 16) s += pm[(int64_t)k * ld + j];
+  return s;
+}
+
 // Up to three [n_part][cols] partial-sum matrices (stride mat_stride floats)
 // reduced over rows into three outputs in one launch: 64 columns x 16 row
 // groups per block, blockIdx.y = matrix.
@@ -385,9 +404,7 @@ __global__ __launch_bounds__(1024) void reduce_rows3_kernel(const float* part, i
   const int j = blockIdx.x * 64 + cl;
   float* out = blockIdx.y == 0 ? o0 : blockIdx.y == 1 ? o1 : o2;
   const float* pm = part + blockIdx.y * mat_stride;
-  float s = 0.f;
-  if (j < cols)
-    for (int k = rg; k < n_part; k += 16) s += pm[(int64_t)k * cols + j];
+  const float s = j < cols ? strided_col_sum(pm, cols, n_part, rg, j) : 0.f;
   __shared__ float red[16][64];
   red[rg][cl] = s;
   __syncthreads();
@@ -433,9 +450,7 @@ __global__ __launch_bounds__(1024) void reduce_batch_kernel(ReduceBatch rb) {
   const int j = blk * 64 + cl, cols = rb.cols[jb], n_part = rb.n_part[jb];
   const float* pm = rb.part[jb];
   const int64_t ld = rb.ld[jb];
-  float s = 0.f;
-  if (j < cols)
-    for (int k = rg; k < n_part; k += 16) s += pm[(int64_t)k * ld + j];
+  const float s = j < cols ? strided_col_sum(pm, ld, n_part, rg, j) : 0.f;
   __shared__ float red[16][64];
   red[rg][cl] = s;
   __syncthreads();
