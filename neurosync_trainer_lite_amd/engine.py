@@ -272,11 +272,18 @@ class Seq2SeqEngine:
             order += [b + "ffn.linear2.weight", b + "ffn.linear2.bias", b + "ffn.linear1.weight", b + "ffn.linear1.bias"]
             m = b + "multihead_attn."
             order += [m + "out_linear.weight", m + "out_linear.bias", m + "q_linear.weight", m + "q_linear.bias",
-                      m + "k_linear.weight", m + "v_linear.weight", m + "k_linear.bias", m + "v_linear.bias"]
+                      m + "k_linear.bias", m + "v_linear.bias"]
             s = b + "self_attn."
             order += [s + "out_linear.weight", s + "out_linear.bias",
                       s + "q_linear.weight", s + "k_linear.weight", s + "v_linear.weight",
                       s + "q_linear.bias", s + "k_linear.bias", s + "v_linear.bias"]
+        # the cross-attention k|v weights of all decoder layers, in layer order: the
+        # B operand [W_kv_0; ...; W_kv_{L-1}] of the memory-gradient GEMM is then a
+        # view of the arena (_kv_weights).  After the decoder layers, so the prefix
+        # a decoder layer's backward completes still holds only final gradients.
+        for l in range(L):
+            m = "decoder.transformer_decoder.%d.multihead_attn." % l
+            order += [m + "k_linear.weight", m + "v_linear.weight"]
         order += ["encoder.layer_norm.weight", "encoder.layer_norm.bias"]
         for l in reversed(range(L)):
             b = "encoder.transformer_encoder.%d." % l
@@ -400,12 +407,20 @@ class Seq2SeqEngine:
                 return (min(self.offsets[n][0] for n in names),
                         max(self.offsets[n][0] + _pad64(self.offsets[n][1]) for n in names))
 
+            def is_kv(n):  # the cross-attention k|v block (after the decoder layers)
+                return ".multihead_attn.k_linear.weight" in n or ".multihead_attn.v_linear.weight" in n
+
             def mats(prefix):
-                return [n for n in self.offsets if n.startswith(prefix) and len(self.offsets[n][2]) > 1]
+                return [n for n in self.offsets
+                        if n.startswith(prefix) and len(self.offsets[n][2]) > 1 and not is_kv(n)]
             st = [("vec", (self.n_shardable, self.numel)), ("emb", rng(["encoder.embedding.weight"]))]
             st += [(("enc", l), rng(mats("encoder.transformer_encoder.%d." % l))) for l in range(self.L)]
+            st += [("dec_kv", rng([n for n in self.offsets if is_kv(n)]))]
             st += [(("dec", l), rng(mats("decoder.transformer_decoder.%d." % l))) for l in range(self.L)]
             st += [("head", rng(["decoder.fc_output.weight"]))]
+            # the stages partition the arena: an update range never covers a parameter twice
+            cuts = sorted(r for _, r in st)
+            assert all(a[1] <= b[0] for a, b in zip(cuts, cuts[1:])), cuts
             self._upd_ranges = st
             self._stage_rng = dict(st)
         return self._upd_ranges
@@ -431,9 +446,12 @@ class Seq2SeqEngine:
         self._wpending = keep
 
     def await_stage(self, key):
-        """The current stream waits for the queued update of stage `key`'s weights."""
+        """The current stream waits for the queued update of stage `key`'s weights
+        (a decoder layer's include its cross-attention k|v, kept in their own block)."""
         if self._wpending:
             self._await(*self._stage_rng[key])
+            if isinstance(key, tuple) and key[0] == "dec":
+                self._await(*self._stage_rng["dec_kv"])
 
     def sync_pending(self):
         """The current stream waits for every queued update."""
@@ -453,9 +471,14 @@ class Seq2SeqEngine:
     def _kv_weights(self):
         """The decoder cross-attention k|v weights (compute dtype) stacked in one
         contiguous [L * 2D, D] slab, the B operand of the concatenated memory-gradient
-        GEMM; refreshed every backward (the optimizer has moved the weights).  Runs
-        on the current stream, which backward() makes the engine's stream."""
+        GEMM: a view of the arena (_arena_order keeps them side by side in layer
+        order); otherwise copied every backward (the optimizer has moved the
+        weights) on the current stream, which backward() makes the engine's stream."""
         D, L = self.D, self.L
+        k0 = self.offsets["decoder.transformer_decoder.0.multihead_attn.k_linear.weight"][0]
+        if all(self.offsets["decoder.transformer_decoder.%d.multihead_attn.%s_linear.weight" % (l, kv)][0]
+               == k0 + (2 * l + (kv == "v")) * D * D for l in range(L) for kv in ("k", "v")):
+            return self.p16[k0:k0 + L * 2 * D * D].view(L * 2 * D, D)
         if self._wkv is None:
             self._wkv = torch.empty(L * 2 * D, D, dtype=self.dt, device=self.device)
         for l in range(L):
