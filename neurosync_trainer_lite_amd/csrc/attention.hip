@@ -276,13 +276,17 @@ NSTL_DEV void fwd_queries(const AttnParams& p, const char* Kimg, const char* Vim
     if (kt < nkt) m = fmaxf(fmaxf(fmaxf(m, s[kt][0]), fmaxf(s[kt][1], s[kt][2])), s[kt][3]);
   m = fmaxf(m, __shfl_xor(m, 16));
   m = fmaxf(m, __shfl_xor(m, 32));
+  // bf16: 2^(s*c2 - m*c2), one FMA per score instead of a subtract and a multiply.
+  // f32 (parity mode) keeps (s - m)*c2: s - m is exact near the max, where the
+  // rounded m*c2 of the FMA form would cancel (the fp32 gradient norm moved by 1e-4)
+  const float mc = m * c2;
   float sum = 0.f;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt)
     if (kt < nkt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = fast_exp2((s[kt][r] - m) * c2);
+        const float e = fast_exp2(sizeof(T) == 2 ? fmaf(s[kt][r], c2, -mc) : (s[kt][r] - m) * c2);
         s[kt][r] = e;
         sum += e;
       }
