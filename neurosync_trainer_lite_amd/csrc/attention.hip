@@ -274,8 +274,8 @@ NSTL_DEV void fwd_queries(const AttnParams& p, const char* Kimg, const char* Vim
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt)
     if (kt < nkt) m = fmaxf(fmaxf(fmaxf(m, s[kt][0]), fmaxf(s[kt][1], s[kt][2])), s[kt][3]);
-  m = fmaxf(m, __shfl_xor(m, 16));
-  m = fmaxf(m, __shfl_xor(m, 32));
+  m = max_xor16(m);
+  m = max_xor32(m);
   // bf16: 2^(s*c2 - m*c2), one FMA per score instead of a subtract and a multiply.
   // f32 (parity mode) keeps (s - m)*c2: s - m is exact near the max, where the
   // rounded m*c2 of the FMA form would cancel (the fp32 gradient norm moved by 1e-4)
@@ -291,8 +291,8 @@ NSTL_DEV void fwd_queries(const AttnParams& p, const char* Kimg, const char* Vim
         sum += e;
       }
     }
-  sum += __shfl_xor(sum, 16);
-  sum += __shfl_xor(sum, 32);
+  sum = sum_xor16(sum);
+  sum = sum_xor32(sum);
   if (p.thresh) {
     // dropout on P: keys (r, r+1) of this lane's query share one hash.  The keep
     // compare is an SGPR lane mask already -- the ballot of (kt, r) -- and lane
@@ -554,8 +554,8 @@ NSTL_DEV void wave_colsum16x64(const float (&v)[4][4], float* red, int w, int la
     float cs = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) cs += to_f32(from_f32<T>(v[dt][r]));
-    cs += __shfl_xor(cs, 16);
-    cs += __shfl_xor(cs, 32);
+    cs = sum_xor16(cs);
+    cs = sum_xor32(cs);
     if (lane < 16) red[w * 64 + dt * 16 + lane] = cs;
   }
 }
@@ -627,8 +627,8 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int e = 0; e < 8; ++e) dpart += to_f32(fo[u][e]) * to_f32(oo[u][e]);
-    dpart += __shfl_xor(dpart, 16);
-    dpart += __shfl_xor(dpart, 32);
+    dpart = sum_xor16(dpart);
+    dpart = sum_xor32(dpart);
     if (g == 0) p.dsum[(int64_t)bh * T_ + qr] = dpart;
     dqv = dpart;
     lq = p.lse[(int64_t)bh * T_ + qr] * LOG2E;
@@ -929,8 +929,8 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
 #pragma unroll
       for (int e = 0; e < 8; ++e) dpart += (float)fo[e] * (float)oo[u][e];
     }
-    dpart += __shfl_xor(dpart, 16);
-    dpart += __shfl_xor(dpart, 32);
+    dpart = sum_xor16(dpart);
+    dpart = sum_xor32(dpart);
     if (g == 0) d_s[k0 + c] = dpart;
   }
   __syncthreads();

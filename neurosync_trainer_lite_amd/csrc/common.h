@@ -181,15 +181,40 @@ static inline uint32_t nstl_drop_thresh(float p) {
 // VALU-writes-SGPR -> v_writelane wait states (inline asm would not)
 __device__ int nstl_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
-// wave-level reductions (64 lanes)
+// x (op) x[lane ^ 16] and x (op) x[lane ^ 32] with the gfx950 permlane swaps: one
+// VALU exchange each (the compiler pads its hazard), where __shfl_xor is an LDS
+// ds_bpermute plus its address arithmetic.  The pairs are the same, so the
+// results equal the __shfl_xor forms bit for bit.  Every lane must be active.
+NSTL_DEV float sum_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+NSTL_DEV float sum_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+NSTL_DEV float max_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+NSTL_DEV float max_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// wave-level reductions (64 lanes; the same pairing order as a 32, 16, ..., 1 butterfly)
 NSTL_DEV float wave_sum(float v) {
+  v = sum_xor32(v);
+  v = sum_xor16(v);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
 NSTL_DEV float wave_max(float v) {
+  v = max_xor32(v);
+  v = max_xor16(v);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
   return v;
 }
 NSTL_DEV double wave_sum_d(double v) {
