@@ -45,6 +45,7 @@ struct GemmParams {
   uint64_t* relu_mask;  // ReLU-dropout keep&positive bits, ring epilogue layout (relu_mask_index)
   const float* a_scale; const float* b_scale;  // fp8: row scales of A [M] and of B [N]
   float* sq_part;  // grouped f32 ring epilogue: sum of squares of C as stored, per (tile, wave) [tiles][8]
+  int direct_epi;  // EM_BF16 ring epilogue from registers (permlane swaps) on full tiles; 0: LDS staging
 };
 
 // Epilogue over a wave's MT x 4 grid of 16x16 accumulators whose origin is
@@ -863,6 +864,45 @@ NSTL_DEV void ring_epi_generic(const GemmParams& p, const f32x4 (&acc)[8][4], in
   }
 }
 
+// EM_BF16 on a full tile without the LDS staging pass.  Lane (g, c) holds row
+// 16a + c, columns 16b + 4g .. +3 of acc[a][b]; after the bias and the bf16 packing,
+// a permlane16 swap of the chunks of b and b + 1 (odd 16-lane rows of the first
+// operand <-> even rows of the second) leaves lane g even with columns 16b + 4g .. +7
+// and lane g odd with 16(b + 1) + 4(g - 1) .. +7: one 16-byte store per lane and
+// pair of column blocks, 64 contiguous bytes per row per wave instruction.  The
+// ring is not reused, so no barrier precedes it.
+NSTL_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  const bf16 a = (bf16)lo, b = (bf16)hi;
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+NSTL_DEV void ring_epi_bf16_direct(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, int col0, int lane) {
+  const int g = lane >> 4, c = lane & 15, odd = g & 1;
+  const float alpha = p.alpha;
+  float bias[4][4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[b][e] = p.bias != nullptr ? p.bias[col0 + 16 * b + 4 * g + e] : 0.f;
+  bf16* const cbase = (bf16*)p.C + (int64_t)(row0 + c) * p.ldc + col0;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    bf16* crow = cbase + (int64_t)(16 * a) * p.ldc;
+#pragma unroll
+    for (int bp = 0; bp < 4; bp += 2) {
+      const f32x4 u = acc[a][bp], v = acc[a][bp + 1];
+      uint32_t x0 = pack_bf16x2(u[0] * alpha + bias[bp][0], u[1] * alpha + bias[bp][1]);
+      uint32_t x1 = pack_bf16x2(u[2] * alpha + bias[bp][2], u[3] * alpha + bias[bp][3]);
+      uint32_t y0 = pack_bf16x2(v[0] * alpha + bias[bp + 1][0], v[1] * alpha + bias[bp + 1][1]);
+      uint32_t y1 = pack_bf16x2(v[2] * alpha + bias[bp + 1][2], v[3] * alpha + bias[bp + 1][3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      const int col = 16 * (bp + odd) + 4 * (g - odd);
+      if (p.debug_skip_epilogue != 2)
+        *(uint4*)(crow + col) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
+}
+
 constexpr int R_SMEM = R_STAGES * R_SLOT;
 static_assert(8 * RING_EPI_WAVE <= R_SMEM, "epilogue scratch must fit in the ring");
 
@@ -1031,6 +1071,8 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz0, int kz1, char* sme
     for (int a = 0; a < 8; ++a)
 #pragma unroll
       for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(acc[a][b]));
+  } else if (EM == EM_BF16 && p.direct_epi && m0 + BIG <= p.M && n0 + BIG <= p.N) {
+    ring_epi_bf16_direct(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
   } else {
     __syncthreads();  // every wave is done with the ring: it becomes scratch
     char* scr = smem + wave * RING_EPI_WAVE;
@@ -1518,6 +1560,12 @@ int make_params(const nstl_gemm_args* a, GemmParams& p) {
   p.rope_T = a->rope_T; p.rope_dim = a->rope_dim; p.rope_cols = a->rope_cols;
   p.ws = nullptr;
   p.debug_skip_epilogue = getenv_debug_skip_epi();
+  // NSTL_GEMM_DIRECT=0: the LDS-staged EM_BF16 epilogue (A/B; read per call).  The
+  // direct one needs 16-byte aligned rows of C.
+  {
+    const char* e = getenv("NSTL_GEMM_DIRECT");
+    p.direct_epi = !(e && e[0] == '0') && (a->ldc % 8) == 0 && ((uintptr_t)a->C % 16) == 0;
+  }
   p.k_chunk = a->K;
   p.colsum_part = a->colsum_part;
   p.relu_mask = a->relu_mask;
