@@ -202,20 +202,28 @@ NSTL_DEV float max_xor32(float x) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-// wave-level reductions (64 lanes; the same pairing order as a 32, 16, ..., 1 butterfly)
+// x[lane ^ 1], x[lane ^ 2] (quad_perm) and the 8- / 16-lane mirrors (row_half_mirror,
+// row_mirror) as DPP moves: inside a 16-lane row, after the quad steps every quad
+// holds one value, so the mirrors pair quad 0 with 1 and half 0 with 1.
+#define NSTL_DPP(x, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), ctrl, 0xF, 0xF, false))
+
+// wave-level reductions (64 lanes): four DPP steps inside 16-lane rows, then the two
+// permlane swaps; every lane ends with the result
 NSTL_DEV float wave_sum(float v) {
-  v = sum_xor32(v);
+  v += NSTL_DPP(v, 0xB1);   // quad_perm [1, 0, 3, 2]
+  v += NSTL_DPP(v, 0x4E);   // quad_perm [2, 3, 0, 1]
+  v += NSTL_DPP(v, 0x141);  // row_half_mirror
+  v += NSTL_DPP(v, 0x140);  // row_mirror
   v = sum_xor16(v);
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  return sum_xor32(v);
 }
 NSTL_DEV float wave_max(float v) {
-  v = max_xor32(v);
+  v = fmaxf(v, NSTL_DPP(v, 0xB1));
+  v = fmaxf(v, NSTL_DPP(v, 0x4E));
+  v = fmaxf(v, NSTL_DPP(v, 0x141));
+  v = fmaxf(v, NSTL_DPP(v, 0x140));
   v = max_xor16(v);
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
+  return max_xor32(v);
 }
 NSTL_DEV double wave_sum_d(double v) {
 #pragma unroll
