@@ -836,9 +836,13 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
     // lanes l, l + LPR, ... share columns: fold them, then LPR lanes write the
     // wave's 64 column sums as one partial row (this wave's 128 rows)
 #pragma unroll
-    for (int e = 0; e < CW; ++e)
-#pragma unroll
-      for (int o = LPR; o < 64; o <<= 1) csum[e] += __shfl_xor(csum[e], o);
+    for (int e = 0; e < CW; ++e) {
+      // the xor-LPR, 16, 32 butterfly (bit-identical pairs) on DPP / permlane moves
+      if (LPR == 8) csum[e] += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(csum[e]), 0x128, 0xF, 0xF, false));
+      else if (LPR != 16) csum[e] += __shfl_xor(csum[e], LPR);  // row_ror:8 above = lane ^ 8 in a 16-lane row
+      csum[e] = sum_xor16(csum[e]);
+      csum[e] = sum_xor32(csum[e]);
+    }
     if (lane < LPR && colok) {
       float* dst = p.colsum_part + (int64_t)(row0 >> 7) * p.N + j;
 #pragma unroll
