@@ -57,19 +57,28 @@ struct AdamParams {
   const float* coef;  // precomputed clip coefficient (adam_gcoef_kernel)
 };
 
+// NT: the f32 master, gradient and moments stream through once per step with
+// nontemporal loads / stores (their next use is a whole step later), leaving the
+// caches to the bf16 shadow the next forward's GEMMs read
+template <bool NT_ = false>
 NSTL_DEV void adam_elem(const AdamParams& a, float coef, int64_t i) {
-  const float pv = a.p[i];
-  float g = a.g[i] * coef;
+  auto ld = [](const float* q) { return NT_ ? __builtin_nontemporal_load(q) : *q; };
+  auto st = [](float* q, float x) {
+    if (NT_) __builtin_nontemporal_store(x, q);
+    else *q = x;
+  };
+  const float pv = ld(a.p + i);
+  float g = ld(a.g + i) * coef;
   g = g + a.wd * pv;
-  float m = a.m[i];
+  float m = ld(a.m + i);
   m = m + (1.f - a.b1) * (g - m);
-  float v = a.v[i];
+  float v = ld(a.v + i);
   v = v * a.b2 + (1.f - a.b2) * g * g;
   const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
   const float np = pv + (-a.step_size) * (m / denom);
-  a.p[i] = np;
-  a.m[i] = m;
-  a.v[i] = v;
+  st(a.p + i, np);
+  st(a.m + i, m);
+  st(a.v + i, v);
   if (a.lowp) {
     if (a.lowp_bf16) ((bf16*)a.lowp)[i] = (bf16)np;
     else ((float*)a.lowp)[i] = np;
@@ -139,10 +148,11 @@ __global__ __launch_bounds__(1024) void clip_coef_many_kernel(const float* part,
 // Adam with the coefficient read from device memory: no LDS, so its workgroups
 // fit on a CU beside a 160 KB ring-GEMM workgroup (the range updates that run
 // under the next forward, FusedAdam.overlap_next_forward)
+template <bool NT_>
 __global__ __launch_bounds__(NT) void adam_gcoef_kernel(AdamParams a) {
   const float coef = *a.coef;
   const int64_t stride = (int64_t)gridDim.x * NT;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) adam_elem(a, coef, i);
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) adam_elem<NT_>(a, coef, i);
 }
 
 __global__ void cast_kernel(int src_bf16, const void* src, int dst_bf16, void* dst, int64_t n) {
@@ -307,7 +317,15 @@ extern "C" int nstl_adam_step(const nstl_adam_args* a, void* stream) {
       const char* e = getenv("NSTL_ADAM_GRID");
       return e ? std::max(1, atoi(e)) : 8192;
     }();
-    hipLaunchKernelGGL(adam_gcoef_kernel, dim3(std::min(grid_for(a->n, 4), cap)), dim3(NT), 0, (hipStream_t)stream, p);
+    // NSTL_ADAM_NT=0: plain loads / stores (A/B; read per call).  Nontemporal is the
+    // default: +0.4 % step rate same-box (586.7k vs 584.3k frames/s, 3 reps)
+    const char* ne = getenv("NSTL_ADAM_NT");
+    if (!(ne && ne[0] == '0'))
+      hipLaunchKernelGGL(adam_gcoef_kernel<true>, dim3(std::min(grid_for(a->n, 4), cap)), dim3(NT), 0,
+                         (hipStream_t)stream, p);
+    else
+      hipLaunchKernelGGL(adam_gcoef_kernel<false>, dim3(std::min(grid_for(a->n, 4), cap)), dim3(NT), 0,
+                         (hipStream_t)stream, p);
   } else {
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(a->n, 4)), dim3(NT), 0, (hipStream_t)stream, p);
   }
