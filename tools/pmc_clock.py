@@ -1,55 +1,40 @@
-"""Effective clock of each kernel family under load (MI355X_MICROARCH.md, 'DVFS
-give-back'): GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 / kernel wall time,
-from one rocprofv3 run with --pmc GRBM_GUI_ACTIVE and --kernel-trace.
-
-  python tools/pmc_clock.py <dir> <out.json> <tag>"""
+"""Effective clock and MFMA busy fraction per kernel of a rocprofv3 --pmc run
+with GRBM_GUI_ACTIVE and SQ_VALU_MFMA_BUSY_CYCLES (MI355X_MICROARCH.md, 'DVFS
+give-back': clock ~ GRBM_GUI_ACTIVE / 8 XCDs / wall; SQ_VALU_MFMA_BUSY_CYCLES
+counts MFMA cycles summed over the SIMDs, so busy = MFMA / (clock cycles x 1024
+SIMDs)).  Profiled runs clock a few % below un-profiled ones.
+  python tools/pmc_clock.py <dir> [min_calls]"""
 import csv
 import glob
-import json
 import os
 import sys
+from collections import defaultdict
 
-
-def family(name):
-    for key, fam in (("gemm256r_group", "gemm_grouped_dW"), ("gemm256f8", "gemm_fp8"), ("gemm256r", "gemm_ring"),
-                     ("gemm_kernel", "gemm_128"), ("attn_bwd", "attn_bwd"), ("attn_fwd", "attn_fwd"),
-                     ("ln_bwd", "ln_bwd"), ("ln_fwd", "ln_fwd"), ("adam", "adam")):
-        if key in name:
-            return fam
-    return None
-
-
-def main():
-    d, out, tag = sys.argv[1:4]
-    active = {}
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
-                k = int(r["Dispatch_Id"])
-                active[k] = active.get(k, 0.0) + float(r["Counter_Value"])
-    dur, names = {}, {}
-    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            k = int(r["Dispatch_Id"])
-            dur[k] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-            names[k] = r["Kernel_Name"]
-    fams = {}
-    for k, a in active.items():
-        if k not in dur or dur[k] < 3e-4:  # the quotient reads high below ~0.3 ms (guide)
-            continue
-        fam = family(names[k])
-        if fam is None:
-            continue
-        s = fams.setdefault(fam, [0.0, 0.0, 0])
-        s[0] += a / 8.0
-        s[1] += dur[k]
-        s[2] += 1
-    res = {"tag": tag, "method": "rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace; clock = sum(GRBM_GUI_ACTIVE/8) / sum(wall) "
-                                 "over dispatches >= 0.3 ms of the profiled bench run (profiled runs clock ~2-5 % low)",
-           "families": {f: {"dispatches": n, "ghz": round(c / t / 1e9, 3)} for f, (c, t, n) in fams.items()}}
-    json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps(res))
-
-
-if __name__ == "__main__":
-    main()
+d = sys.argv[1]
+min_calls = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+disp = defaultdict(lambda: {"c": defaultdict(float)})
+for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        e = disp[int(r["Dispatch_Id"])]
+        e["name"] = r["Kernel_Name"]
+        e["ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        e["c"][r["Counter_Name"]] += float(r["Counter_Value"])
+per = defaultdict(list)
+for e in disp.values():
+    per[e["name"]].append(e)
+tot_ns = sum(e["ns"] for e in disp.values())
+rows = []
+for n, es in per.items():
+    if len(es) < min_calls:
+        continue
+    ns = sum(e["ns"] for e in es)
+    grbm = sum(e["c"]["GRBM_GUI_ACTIVE"] for e in es)
+    mfma = sum(e["c"]["SQ_VALU_MFMA_BUSY_CYCLES"] for e in es)
+    clk = grbm / 8 / ns if ns else 0.0        # GHz
+    busy = mfma / (grbm / 8 * 1024) if grbm else 0.0
+    rows.append((ns, n, len(es), clk, busy))
+rows.sort(reverse=True)
+print("%-62s %6s %9s %7s %8s %6s" % ("kernel", "calls", "mean us", "GHz", "MFMA busy", "share"))
+for ns, n, k, clk, busy in rows[:25]:
+    short = n.replace("void ", "", 1).replace("(anonymous namespace)::", "").split("(")[0][:62]
+    print("%-62s %6d %9.1f %7.3f %8.3f %6.3f" % (short, k, ns / k / 1e3, clk, busy, ns / tot_ns))
