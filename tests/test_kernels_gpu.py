@@ -167,6 +167,45 @@ def test_gemm_drelu_colsum_partials(M, N):
         K.gemm(dY, W, out, M, N, Kd, a_kmajor=True, b_kmajor=False, colsum_part=part)
 
 
+def _keep_pattern_np(seed, M, N, p):
+    """Keep decision of element (i, j) under common.h's dropout hash:
+    nstl_fmix32(pair ^ seed_term), low / high 16 bits against the threshold."""
+    import numpy as np
+    seed_term = (seed & 0xFFFFFFFF) ^ (((seed >> 32) * 0x27D4EB2F) & 0xFFFFFFFF)
+    thresh = int(p * 65536.0 + 0.5)
+    pair = (np.arange(M, dtype=np.uint64)[:, None] * (N // 2) + np.arange(N // 2, dtype=np.uint64)[None, :])
+    h = (pair.astype(np.uint32) ^ np.uint32(seed_term)).astype(np.uint64)
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    keep = np.empty((M, N), dtype=bool)
+    keep[:, 0::2] = (h & 0xFFFF) >= thresh
+    keep[:, 1::2] = (h >> 16) >= thresh
+    return keep
+
+
+@pytest.mark.parametrize("Kd", [256, 1024, 2048])
+def test_gemm_relu_dropout_keep_pattern_matches_hash(Kd):
+    """The ring kernel hashes the ReLU-dropout keep bits inside its K loop (one
+    unit per K-step; units past a short K loop after it): with every
+    pre-activation positive, the zero pattern is exactly the hash's, for K loops
+    shorter than, equal to and longer than the 16 units."""
+    M, N = 2048, 1024
+    X = rnd(M, Kd, dtype=torch.bfloat16, seed=150)
+    W = rnd(N, Kd, dtype=torch.bfloat16, seed=151, scale=0.01)
+    bias = torch.full((N,), 50.0, device=DEV)
+    h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    kw = dict(epilogue=K.EPI_BIAS_RELU_DROP, bias=bias, p_drop=0.3, seed=(7 << 32) + 1234)
+    words = K.gemm_relu_mask_words(X, W, h, M, N, Kd, **kw)
+    assert words > 0  # the ring kernel (the path with a relu_mask layout) runs this shape
+    mask = torch.zeros(words, dtype=torch.int64, device=DEV)
+    K.gemm(X, W, h, M, N, Kd, relu_mask=mask, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal((h != 0).cpu(), torch.from_numpy(_keep_pattern_np((7 << 32) + 1234, M, N, 0.3)))
+
+
 @pytest.mark.parametrize("M,N", [(1024, 2048), (1000, 4096)])
 def test_gemm_relu_mask_roundtrip(M, N):
     """relu_mask: the ReLU-dropout forward epilogue's keep&positive bits drive the
