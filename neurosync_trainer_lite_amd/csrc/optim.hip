@@ -60,6 +60,20 @@ struct AdamParams {
 // NT: the f32 master, gradient and moments stream through once per step with
 // nontemporal loads / stores (their next use is a whole step later), leaving the
 // caches to the bf16 shadow the next forward's GEMMs read
+// The update of one element (m, v in place; returns the new parameter), shared
+// by every Adam kernel.  Contraction is off and the FMAs are explicit, so the
+// rounding is fixed by the source: an element rounds the same whether a kernel
+// reaches it in an unrolled pass or a tail loop (left to the compiler, the
+// unrolled form differed by 1 ulp on 12 of 10^6 elements).
+NSTL_DEV float adam_math(const AdamParams& a, float coef, float pv, float g, float& m, float& v) {
+#pragma clang fp contract(off)
+  const float gc = fmaf(a.wd, pv, g * coef);               // clip, then L2 (coupled)
+  m = fmaf(1.f - a.b1, gc - m, m);                         // torch lerp form
+  v = fmaf(v, a.b2, ((1.f - a.b2) * gc) * gc);
+  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+  return fmaf(-a.step_size, m / denom, pv);
+}
+
 template <bool NT_ = false>
 NSTL_DEV void adam_elem(const AdamParams& a, float coef, int64_t i) {
   auto ld = [](const float* q) { return NT_ ? __builtin_nontemporal_load(q) : *q; };
@@ -68,14 +82,10 @@ NSTL_DEV void adam_elem(const AdamParams& a, float coef, int64_t i) {
     else *q = x;
   };
   const float pv = ld(a.p + i);
-  float g = ld(a.g + i) * coef;
-  g = g + a.wd * pv;
+  const float g = ld(a.g + i);
   float m = ld(a.m + i);
-  m = m + (1.f - a.b1) * (g - m);
   float v = ld(a.v + i);
-  v = v * a.b2 + (1.f - a.b2) * g * g;
-  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
-  const float np = pv + (-a.step_size) * (m / denom);
+  const float np = adam_math(a, coef, pv, g, m, v);
   st(a.p + i, np);
   st(a.m + i, m);
   st(a.v + i, v);
@@ -148,11 +158,44 @@ __global__ __launch_bounds__(1024) void clip_coef_many_kernel(const float* part,
 // Adam with the coefficient read from device memory: no LDS, so its workgroups
 // fit on a CU beside a 160 KB ring-GEMM workgroup (the range updates that run
 // under the next forward, FusedAdam.overlap_next_forward)
-template <bool NT_>
+template <bool NT_, int U = 1>
 __global__ __launch_bounds__(NT) void adam_gcoef_kernel(AdamParams a) {
   const float coef = *a.coef;
   const int64_t stride = (int64_t)gridDim.x * NT;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < a.n; i += stride) adam_elem<NT_>(a, coef, i);
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if constexpr (U > 1) {
+    // U elements per pass, every load issued before the first store (the
+    // compiler cannot hoist loads above stores to possibly aliasing arrays):
+    // U x 4 loads in flight per lane
+    auto ld = [](const float* q) { return NT_ ? __builtin_nontemporal_load(q) : *q; };
+    auto st = [](float* q, float x) {
+      if (NT_) __builtin_nontemporal_store(x, q);
+      else *q = x;
+    };
+    for (; i + (U - 1) * stride < a.n; i += U * stride) {
+      float pv[U], g[U], m[U], v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pv[u] = ld(a.p + i + u * stride);
+        g[u] = ld(a.g + i + u * stride);
+        m[u] = ld(a.m + i + u * stride);
+        v[u] = ld(a.v + i + u * stride);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float np = adam_math(a, coef, pv[u], g[u], m[u], v[u]);
+        const int64_t k = i + u * stride;
+        st(a.p + k, np);
+        st(a.m + k, m[u]);
+        st(a.v + k, v[u]);
+        if (a.lowp) {
+          if (a.lowp_bf16) ((bf16*)a.lowp)[k] = (bf16)np;
+          else ((float*)a.lowp)[k] = np;
+        }
+      }
+    }
+  }
+  for (; i < a.n; i += stride) adam_elem<NT_>(a, coef, i);
 }
 
 __global__ void cast_kernel(int src_bf16, const void* src, int dst_bf16, void* dst, int64_t n) {
@@ -308,8 +351,8 @@ extern "C" int nstl_adam_step(const nstl_adam_args* a, void* stream) {
   p.bc2_sqrt = (float)std::sqrt(bc2);
   p.part = a->sumsq_partial; p.n_part = a->n_partial; p.max_norm = a->max_norm; p.norm_out = a->norm_out;
   p.coef = a->coef;
-  // scalar, one element per thread and step: measured faster than 16-byte
-  // vectorised forms (x1: +4 %, x2 unrolled: +4-8 %, tools/bench_adam.py)
+  // scalar elements (16-byte vectorised forms measured slower: x1 +4 %, x2
+  // unrolled +4-8 %, tools/bench_adam.py), strided by the grid
   if (a->coef) {
     NSTL_CHECK_ARG(!a->sumsq_partial, "nstl_adam_step: coef and sumsq_partial are exclusive");
     // NSTL_ADAM_GRID: cap on its workgroups (how many CUs a range update shares)
@@ -320,7 +363,19 @@ extern "C" int nstl_adam_step(const nstl_adam_args* a, void* stream) {
     // NSTL_ADAM_NT=0: plain loads / stores (A/B; read per call).  Nontemporal is the
     // default: +0.4 % step rate same-box (586.7k vs 584.3k frames/s, 3 reps)
     const char* ne = getenv("NSTL_ADAM_NT");
-    if (!(ne && ne[0] == '0'))
+    // two elements per lane and pass with all 8 loads in flight (default: +0.35 %
+    // step same-box, 586.6-587.6k vs 584.7-585.9k); NSTL_ADAM_U=1 | 4 for A/B
+    static const int unroll = [] {
+      const char* e = getenv("NSTL_ADAM_U");
+      return e ? atoi(e) : 2;
+    }();
+    if (!(ne && ne[0] == '0') && unroll == 2)
+      hipLaunchKernelGGL((adam_gcoef_kernel<true, 2>), dim3(std::min(grid_for(a->n, 4), cap)), dim3(NT), 0,
+                         (hipStream_t)stream, p);
+    else if (!(ne && ne[0] == '0') && unroll == 4)
+      hipLaunchKernelGGL((adam_gcoef_kernel<true, 4>), dim3(std::min(grid_for(a->n, 4), cap)), dim3(NT), 0,
+                         (hipStream_t)stream, p);
+    else if (!(ne && ne[0] == '0'))
       hipLaunchKernelGGL(adam_gcoef_kernel<true>, dim3(std::min(grid_for(a->n, 4), cap)), dim3(NT), 0,
                          (hipStream_t)stream, p);
     else

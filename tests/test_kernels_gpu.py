@@ -814,6 +814,37 @@ def test_adam_clip_matches_oracle():
     torch.testing.assert_close(p16.cpu(), p.cpu().to(torch.bfloat16))
 
 
+def test_adam_coef_path_matches_sumsq_path():
+    """The engine's path (nstl_clip_coef, then nstl_adam_step reading `coef`:
+    adam_gcoef_kernel, whichever NSTL_ADAM_NT / NSTL_ADAM_U variant the process
+    runs) is bit-identical to the one-launch sumsq path (adam_kernel)."""
+    n = 1_000_003
+    g = rnd(n, scale=0.01, seed=63)
+    part = torch.empty(1024, device=DEV)
+    K.sumsq(g, n, part, 1024)
+    coef, norm = torch.empty(1, device=DEV), torch.empty(1, device=DEV)
+    K.clip_coef(part, 1024, 2.0, coef, norm)
+    outs = []
+    for use_coef in (False, True):
+        p = rnd(n, seed=62)
+        m, v = rnd(n, scale=0.01, seed=64), rnd(n, scale=1e-4, seed=65).abs()
+        p16 = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        a = K.AdamArgs()
+        a.p, a.g, a.m, a.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+        a.p_lowp, a.lowp_dtype, a.n = p16.data_ptr(), K.BF16, n
+        a.lr, a.beta1, a.beta2, a.eps, a.weight_decay = 1e-3, 0.9, 0.999, 1e-8, 1e-2
+        a.step, a.max_norm = 3, 2.0
+        if use_coef:
+            a.coef = coef.data_ptr()
+        else:
+            a.sumsq_partial, a.n_partial = part.data_ptr(), 1024
+        K.adam_step(a)
+        outs.append((p, m, v, p16))
+    torch.cuda.synchronize()
+    for name, x, y in zip(("p", "m", "v", "p16"), *outs):
+        assert torch.equal(x, y), (name, (x.float() - y.float()).abs().max().item(), (x != y).sum().item())
+
+
 def test_small_kernels():
     rows, cols = 600, 200
     x = rnd(rows, cols, dtype=torch.bfloat16, seed=70)
