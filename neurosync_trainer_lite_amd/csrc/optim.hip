@@ -248,7 +248,21 @@ __global__ __launch_bounds__(NT) void colsum_vec_kernel(const T* x, int64_t ld, 
 #pragma unroll
   for (int j = 0; j < EPV; ++j) acc[j] = 0.f;
   if (c0 < cols) {
-    for (int r = r0 + rg; r < r1; r += RG) {
+    // 4 rows' loads in flight, then their adds in row order (the sums of the
+    // one-row-at-a-time loop, which waited a memory latency per row)
+    int r = r0 + rg;
+    for (; r + 3 * RG < r1; r += 4 * RG) {
+      uint4 u[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) u[q] = *(const uint4*)(x + (int64_t)(r + q * RG) * ld + c0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const T* e = (const T*)&u[q];
+#pragma unroll
+        for (int j = 0; j < EPV; ++j) acc[j] += to_f32(e[j]);
+      }
+    }
+    for (; r < r1; r += RG) {
       const uint4 u = *(const uint4*)(x + (int64_t)r * ld + c0);
       const T* e = (const T*)&u;
 #pragma unroll
