@@ -47,58 +47,91 @@ def frames_flops(W, T, D, n_attn=24):
     return 6 * W + 12 * T * D * n_attn
 
 
-def _pmc_per_dispatch(d, counter):
-    """{dispatch id: summed counter} over the bf16 GEMM-family dispatches of a
-    rocprofv3 --output-format csv counter run."""
+def _is_bf16_gemm(name):
+    return "gemm" in name and "splitk" not in name and "f8" not in name
+
+
+def _pmc_dispatches(d):
+    """{dispatch id: (kernel name, ns, {counter: summed value})} of a rocprofv3
+    --output-format csv counter run."""
     import csv
     import glob
-    vals = {}
+    out = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"]
-            if r["Counter_Name"] != counter or "gemm" not in name or "splitk" in name or "f8" in name:
-                continue
             k = int(r["Dispatch_Id"])
-            vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
-    return vals
+            if k not in out:
+                out[k] = (r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), {})
+            c = out[k][2]
+            c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return out
 
 
-def measure_gemm_traffic(args):
-    """HBM bytes per GEMM-family launch, measured on this box in this run: two
-    rocprofv3 counter passes (FETCH_SIZE, WRITE_SIZE: separate passes, as
-    MI355X_MICROARCH.md prescribes) over a child run of this same bench (1
-    warm-up + 1 step of the same workload), started before this process touches
-    the GPU.  bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950 FETCH_SIZE
-    counts streaming reads at half their bytes).  Returns (bytes, note)."""
+def measure_gemm_counters(args):
+    """PMC figures of the GEMM family, measured on this box in this run by three
+    rocprofv3 counter passes over a child run of this same bench (1 warm-up + 1
+    step of the same workload), started before this process touches the GPU:
+      - FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md): HBM
+        bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950
+        FETCH_SIZE counts streaming reads at half their bytes);
+      - SQ_VALU_MFMA_BUSY_CYCLES with GRBM_GUI_ACTIVE: the share of the clock
+        cycles the matrix pipes were busy, MFMA / (GRBM_GUI_ACTIVE / 8 XCDs x 1024
+        SIMDs), and the clock the kernel ran at (GRBM_GUI_ACTIVE / 8 / wall).
+    Returns {"traffic": bytes|None, "note": str, "mfma_busy": {...}|None}."""
     import shutil
     import subprocess
     import tempfile
+    res = {"traffic": None, "mfma_busy": None}
     exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
-        return None, "rocprofv3 absent: traffic not measured"
-    kib = {}
+        res["note"] = "rocprofv3 absent: counters not measured"
+        return res
+    runs = {}
     t0 = time.perf_counter()
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+    for tag, counters in (("FETCH_SIZE", ["FETCH_SIZE"]), ("WRITE_SIZE", ["WRITE_SIZE"]),
+                          ("MFMA", ["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"])):
         d = tempfile.mkdtemp(prefix="nstl_pmc_", dir="/tmp")
-        cmd = ["timeout", "-s", "KILL", "240", exe, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv",
+        cmd = ["timeout", "-s", "KILL", "240", exe, "--pmc"] + counters + [
+               "-d", d, "-o", "run", "--output-format", "csv",
                "--", sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
                "--no-parity", "--feature-steps", "0", "--feed-steps", "0", "--no-traffic",
-               "--batch", str(args.batch), "--seq", str(args.seq)]
+               "--batch", str(args.batch), "--seq", str(args.seq)] + (["--fp8"] if args.fp8 else [])
         env = dict(os.environ, TMPDIR="/tmp")
-        log("traffic: rocprofv3 --pmc %s pass (child bench, 1+1 steps)" % counter)
+        log("counters: rocprofv3 --pmc %s pass (child bench, 1+1 steps)" % " ".join(counters))
         r = subprocess.run(cmd, env=env, cwd="/tmp", stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
         if r.returncode != 0:
-            log("traffic: %s pass failed (rc %d): %s" % (counter, r.returncode, r.stderr[-400:]))
-            return None, "rocprofv3 %s pass failed (rc %d): traffic not measured" % (counter, r.returncode)
-        v = _pmc_per_dispatch(d, counter)
+            log("counters: %s pass failed (rc %d): %s" % (tag, r.returncode, r.stderr[-400:]))
+            res["note"] = "rocprofv3 %s pass failed (rc %d): counters not measured" % (tag, r.returncode)
+            return res
+        runs[tag] = _pmc_dispatches(d)
         shutil.rmtree(d, ignore_errors=True)
+    log("counters: three passes in %.1fs" % (time.perf_counter() - t0))
+    kib = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        v = [x[2][c] for x in runs[c].values() if _is_bf16_gemm(x[0]) and c in x[2]]
         if not v:
-            return None, "rocprofv3 %s pass recorded no GEMM dispatch: traffic not measured" % counter
-        kib[counter] = sum(v.values()) / len(v)
-    log("traffic: both passes in %.1fs" % (time.perf_counter() - t0))
-    return (round((2.0 * kib["FETCH_SIZE"] + kib["WRITE_SIZE"]) * 1024.0),
-            "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 1+1-step child run of "
-            "this workload, mean over its bf16 GEMM-family dispatches")
+            res["note"] = "rocprofv3 %s pass recorded no GEMM dispatch: traffic not measured" % c
+            return res
+        kib[c] = sum(v) / len(v)
+    res["traffic"] = round((2.0 * kib["FETCH_SIZE"] + kib["WRITE_SIZE"]) * 1024.0)
+    res["note"] = ("measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 1+1-step child run of "
+                   "this workload, mean over its bf16 GEMM-family dispatches")
+
+    def busy(sel):
+        xs = [x for x in runs["MFMA"].values() if sel(x[0]) and "GRBM_GUI_ACTIVE" in x[2]]
+        if not xs:
+            return None
+        grbm = sum(x[2]["GRBM_GUI_ACTIVE"] for x in xs)
+        mfma = sum(x[2].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for x in xs)
+        ns = sum(x[1] for x in xs)
+        return {"mfma_busy": round(mfma / (grbm / 8 * 1024), 4), "clock_ghz": round(grbm / 8 / ns, 3),
+                "dispatches": len(xs)}
+    res["mfma_busy"] = {"gemm_family": busy(_is_bf16_gemm),
+                        "grouped_dw": busy(lambda n: "group_kernel" in n and _is_bf16_gemm(n)),
+                        "source": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, child run (1+1 steps); "
+                                  "busy = MFMA cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); profiled runs "
+                                  "clock a few % below un-profiled ones"}
+    return res
 
 
 def cpu_baseline(cfg, T, budget_s=20.0):
@@ -329,9 +362,10 @@ def main():
     from neurosync_trainer_lite_amd.utils.model_utils import build_model, prepare_training_components
 
     # PMC traffic passes first: child processes, started before this one touches the GPU
-    traffic, traffic_src = None, "skipped (--no-traffic or n>1)"
+    traffic, traffic_src, mfma_busy = None, "skipped (--no-traffic or n>1)", None
     if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_traffic:
-        traffic, traffic_src = measure_gemm_traffic(args)
+        ctr = measure_gemm_counters(args)
+        traffic, traffic_src, mfma_busy = ctr["traffic"], ctr["note"], ctr["mfma_busy"]
     rank, world, local = parallel.init_from_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -353,9 +387,12 @@ def main():
     src = torch.randn(B, T, cfg["input_dim"], device=dev, generator=g)
     trg = torch.randn(B, T, cfg["output_dim"], device=dev, generator=g) * 20
 
-    # as train_one_epoch sets it: the loop's next use of the parameters is its
-    # forward, so FusedAdam runs its update under that forward (same results)
-    opt.overlap_next_forward = world == 1
+    # as train_one_epoch sets it: nothing writes the gradients between backward
+    # and step, so the clip norm may come from the weight-gradient epilogues'
+    # partials.  (train_one_epoch also sets overlap_next_forward; that overlap only
+    # runs under NSTL_ADAM_OVERLAP=1, off by default, so it is not set here: the
+    # timed update runs on the main stream after backward.)
+    opt.trust_backward_norm = world == 1
 
     def step(x=src, y=trg):
         opt.zero_grad()
@@ -575,13 +612,21 @@ def main():
             "step_mfma_frac": round(step_tf / BF16_DENSE_PEAK_TFLOPS, 4),
             "final_loss": round(loss_v, 4),
         }
+        if mfma_busy is not None:
+            out["roofline"]["mfma_busy"] = mfma_busy["gemm_family"]
         if dom_roof is not None:
+            if mfma_busy is not None:
+                dom_roof["mfma_busy"] = mfma_busy["grouped_dw"]
+                dom_roof["mfma_busy_source"] = mfma_busy["source"]
             out["roofline_dominant"] = dom_roof
         if fp8_roof is not None:
+            scope = eng.fp8_scope_desc() if hasattr(eng, "fp8_scope_desc") else None
+            fp8_roof["scope"] = scope
             out["roofline_fp8"] = fp8_roof
-            out["dtype"] = "bf16 + e4m3 (attention q/k/v + encoder FFN1 forward GEMMs, row-wise scales)"
+            out["dtype"] = "bf16 + e4m3 (%s; row-wise scales)" % (scope["summary"] if scope else "fp8 GEMMs")
             out["config"]["workload"] = ("C5: 228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam), "
-                                         "fp8 attention q/k/v + encoder FFN1 forward, T=%d" % T)
+                                         "fp8 %s, T=%d" % (scope["summary"] if scope else "GEMMs", T))
+            out["config"]["fp8_scope"] = scope
         if feat is not None:
             out["feature_inclusive"] = feat
         if feed is not None:

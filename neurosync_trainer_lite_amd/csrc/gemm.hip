@@ -1159,6 +1159,272 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm256r_group_kernel(GroupParams g
 }
 
 // ===========================================================================
+// Two workgroups per CU (NSTL_GEMM_H): a 128 (M) x 256 (N) tile on 4 waves, one
+// per SIMD, each owning 128 x 64 -- the per-wave work of the 256^2 ring kernel
+// (8 A + 4 B fragments, 32 MFMAs per 32-deep K-step) -- with a ring of three
+// 24 KB LDS-DMA stages (A 128 x 32 + B 256 x 32 bf16: 72 KB), so two
+// workgroups fit on a CU (144 of 160 KB) and every SIMD runs one wave of each.
+// The workgroups are independent: one workgroup's epilogue, prologue and
+// dispatch gap run beside the other's K loop on the same CU, where the
+// one-workgroup 256^2 kernel leaves the matrix pipes idle for ~10 us per round
+// ("Where a GEMM round's fixed cost goes"), and the partner
+// wave on a SIMD fills the barrier and fragment-read gaps of this one (the role
+// the stagger plays inside the 8-wave kernel).
+// Step s: wait for this wave's share of stage s; barrier (stage s has landed for
+// every wave, and every wave has its fragments of stage s-1 in registers, so
+// its slot is free); stage s+2 into that slot; fragment reads of stage s; 32
+// MFMAs.  One barrier per K-step, two stages in flight.
+#ifndef NSTL_GEMMH_MODE
+#define NSTL_GEMMH_MODE 2
+#endif
+constexpr int H_BM = 128, H_NT = 256, H_SLOT = 24576, H_STAGES = 3, H_A = 8192;
+constexpr int H_SMEM = H_STAGES * H_SLOT;
+static_assert(4 * RING_EPI_WAVE <= H_SMEM, "epilogue scratch must fit in the ring");
+
+// per-lane LDS-DMA sources of wave-instructions q0 .. q0+NQ-1 of one operand image
+// (the glds_src32 layouts: K-major 64-byte rows with kswz, or ImgMN<512>)
+template <bool KMAJ, int NQ>
+NSTL_DEV void glds_src_q(const char* (&src)[NQ], const char* base, int64_t ld, int row0, int rows_total, int q0,
+                         int lane) {
+#pragma unroll
+  for (int s = 0; s < NQ; ++s) {
+    const int q = q0 + s;
+    if (KMAJ) {
+      const int row = 16 * q + (lane >> 2), ch = (lane & 3) ^ kswz(row);
+      const int gi = min(row0 + row, rows_total - 1);
+      src[s] = base + ((int64_t)gi * ld + ch * 8) * 2;
+    } else {
+      const int row = 2 * q + (lane >> 5), pc = lane & 31;
+      const int x = (row & 3) | (((row >> 3) & 1) << 2);
+      const int lc = pc ^ (x << 1);
+      const int gi = min(row0 + lc * 8, ((rows_total - 1) / 8) * 8);
+      src[s] = base + ((int64_t)row * ld + gi) * 2;
+    }
+  }
+}
+
+template <int NQ>
+NSTL_DEV void glds_issue_q(char* img, const char* const (&src)[NQ], int64_t off, int q0) {
+#pragma unroll
+  for (int s = 0; s < NQ; ++s)
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src[s] + off),
+                                     (void __attribute__((address_space(3)))*)(img + (q0 + s) * 1024), 16, 0, 0);
+}
+
+// One 128 x 256 tile of p over K range [kz0, kz1) (`id` already XCD-remapped).
+// flags (RT_*): RT_SAVE parks the f32 accumulators in the workgroup's private
+// slot `part` instead of an epilogue; RT_RESTORE adds the parked piece before it
+// (register g of thread t at part[g * 256 + t]).
+template <bool BKM, int EM>
+NSTL_DEV void h_tile(const GemmParams& p, int id, int kz0, int kz1, char* smem, int flags = 0,
+                     f32x4* part = nullptr) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nt_n = (p.N + BIG - 1) / BIG, nt_m = (p.M + H_BM - 1) / H_BM;
+  // grouped order over XCD-contiguous id ranges: an XCD's 64 co-resident
+  // workgroups cover ~8 x 8 tiles (8 A panels of 128 rows, 8 B panels of 256 columns)
+  constexpr int GROUP_M = 8;
+  const int per_group = GROUP_M * nt_n;
+  const int first_m = (id / per_group) * GROUP_M;
+  const int gm = min(nt_m - first_m, GROUP_M);
+  const int in_g = id % per_group;
+  const int tm = first_m + in_g % gm, tn = in_g / gm;
+  const int m0 = tm * H_BM, n0 = tn * BIG;
+  const int nk = (kz1 - kz0) / R_BK;
+  const uint32_t smem_u32 = lds_u32(smem);
+  const char* sa[2];
+  const char* sb[4];
+  glds_src_q<true, 2>(sa, p.A, p.lda, m0, p.M, wave * 2, lane);
+  glds_src_q<BKM, 4>(sb, p.B, p.ldb, n0, p.N, wave * 4, lane);
+  const int64_t b_kb = BKM ? 2 : 2 * p.ldb;
+  auto stage = [&](int slot, int k0) {
+    char* img = smem + slot * H_SLOT;
+    glds_issue_q<2>(img, sa, (int64_t)k0 * 2, wave * 2);
+    glds_issue_q<4>(img + H_A, sb, (int64_t)k0 * b_kb, wave * 4);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  __amdgpu_buffer_rsrc_t prs;
+  if (flags) prs = __builtin_amdgcn_make_buffer_rsrc(part, 0, H_BM * BIG * 4, 0x00020000);
+
+  // NSTL_GEMMH_MODE (compile time, experiments): bit 0 progressive fragment waits
+  // (the MFMAs of A fragment a start once it has landed), bit 1 (default) the
+  // stage's six LDS-DMA pieces issued between the MFMA groups instead of ahead of
+  // the fragment reads, bit 2 static priority by the workgroup's slot on its CU
+  // (HW_ID TG_ID parity).  Measured (profiles/r3_gemmh_modes.txt): 2 is the
+  // fastest; 1 and 4 do not help.
+  constexpr int HM = NSTL_GEMMH_MODE;
+  bool prio_hi = false;
+  if (HM & 4) prio_hi = ((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 16) & 1) != 0;
+  if (prio_hi) __builtin_amdgcn_s_setprio(2);
+  stage(0, kz0);
+  if (nk > 1) stage(1, kz0 + R_BK);
+  int slot = 0;
+  // last: no stage is in flight behind this one (wait for all)
+  auto step = [&](int kt, bool stage2, bool last) {
+    if (last) NSTL_VMCNT(0);
+    else NSTL_VMCNT(6);
+    __builtin_amdgcn_s_barrier();
+    int s2 = slot + 2;
+    if (s2 >= H_STAGES) s2 -= H_STAGES;
+    char* const img2 = smem + s2 * H_SLOT;
+    const int64_t k2 = (int64_t)kz0 + (kt + 2) * R_BK;
+    if (stage2 && !(HM & 2)) stage(s2, (int)k2);
+    const uint32_t Ai = smem_u32 + slot * H_SLOT;
+    const uint32_t Bi = Ai + H_A;
+    bf16x8 fb[4], fa[8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (BKM) asm_frag_k64(fb[t], Bi, wave * 64 + t * 16 + (lane & 15), 8 * (lane >> 4));
+      else asm_frag_mn512(fb[t], Bi, wave * 64 + t * 16, lane);
+    }
+#pragma unroll
+    for (int a = 0; a < 8; ++a) asm_frag_k64(fa[a], Ai, a * 16 + (lane & 15), 8 * (lane >> 4));
+    if (!(HM & 1)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (prio_hi) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      if (HM & 1) {
+        // LDS reads return in order: fragment a has landed once at most 7 - a
+        // (B: one ds_read_b128 per fragment, or two transpose reads, all issued
+        // before the A reads) are outstanding
+        if (a == 0) asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+        else if (a == 1) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+        else if (a == 2) asm volatile("s_waitcnt lgkmcnt(5)" ::: "memory");
+        else if (a == 3) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+        else if (a == 4) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+        else if (a == 5) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        else if (a == 6) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mma16(acc[a][b], fb[b], fa[a]);
+      if ((HM & 2) && stage2 && a < 6) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (a < 2) glds_issue_q<1>(img2, *(const char* const(*)[1]) & sa[a], k2 * 2, wave * 2 + a);
+        else glds_issue_q<1>(img2 + H_A, *(const char* const(*)[1]) & sb[a - 2], k2 * b_kb, wave * 4 + a - 2);
+      }
+      if (HM & 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (prio_hi) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
+    slot = slot + 1 == H_STAGES ? 0 : slot + 1;
+  };
+  if (nk >= 2) {
+    for (int kt = 0; kt + 2 < nk; ++kt) step(kt, true, false);
+    step(nk - 2, false, false);
+    step(nk - 1, false, true);
+  } else if (nk == 1) {
+    step(0, false, true);
+  }
+  if (flags & RT_RESTORE) {
+    // the parked first piece, loaded one 16-VGPR group ahead (acc = second + first)
+    f32x4 nx[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      nx[b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, tid * 16, b * H_NT * 16, 0));
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      f32x4 cur[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) cur[b] = nx[b];
+      if (a + 1 < 8) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          nx[b] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, tid * 16, ((a + 1) * 4 + b) * H_NT * 16, 0));
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] += cur[b];
+    }
+  }
+  const int col0 = n0 + wave * 64;
+  if (flags & RT_SAVE) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, acc[a][b]), prs, tid * 16,
+                                               (a * 4 + b) * H_NT * 16, 0);
+  } else if (p.debug_skip_epilogue == 1) {  // timing experiments only (NSTL_GEMM_DEBUG=skip_epi)
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(acc[a][b]));
+  } else if (EM == EM_BF16 && p.direct_epi && m0 + H_BM <= p.M && n0 + BIG <= p.N) {
+    ring_epi_bf16_direct(p, acc, m0, col0, lane);
+  } else {
+    __syncthreads();  // every wave is done with the ring: it becomes scratch
+    char* scr = smem + wave * RING_EPI_WAVE;
+    if (EM == EM_GENERIC) ring_epi_generic(p, acc, m0, col0, lane, scr);
+    else ring_epi<EM, false>(p, acc, m0, col0, lane, scr, 0);
+  }
+}
+
+template <bool BKM, int EM>
+__global__ __launch_bounds__(H_NT, 2) void gemmh_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[H_SMEM];
+  const int nt = ((p.M + H_BM - 1) / H_BM) * ((p.N + BIG - 1) / BIG);
+  h_tile<BKM, EM>(p, xcd_remap(blockIdx.x, nt), 0, p.K, smem);
+}
+
+// Persistent form (tiles = rounds x gridDim.x, grid = two workgroups per CU):
+// workgroup w runs the tiles of blocks w, w + G, ... of the one-shot grid.  Two
+// co-resident workgroups that start together run their tiles in lockstep, so
+// their epilogues and prologues coincide and nothing hides them (measured: the
+// one-shot grid hides no per-round cost).  One of the pair (HW_ID TG_ID odd:
+// its slot on the CU; placement only affects speed) therefore cuts its first
+// tile at half its K range: the first piece is parked in the workgroup's f32
+// slot and finished last, so its tile boundaries fall half a tile after its
+// partner's and each one's epilogue runs beside the other's K loop.
+template <bool BKM, int EM>
+__global__ __launch_bounds__(H_NT, 2) void gemmhp_kernel(GemmParams p, int rounds, f32x4* parts) {
+  __shared__ __attribute__((aligned(16))) char smem[H_SMEM];
+  const int G = gridDim.x, w = blockIdx.x;
+  const int nt = rounds * G;
+  const int nk = p.K / R_BK;
+  const bool odd = ((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 16) & 1) != 0 && p.debug_skip_epilogue != 3;
+  const int cut = odd ? (nk >> 1) * R_BK : 0;  // K index of the cut (0: none)
+  f32x4* part = parts + (int64_t)w * (H_BM * BIG / 4);
+  // segments: [tile 0 to the cut, parked] tiles 1..rounds-1 [tile 0 from the cut]
+  // (one h_tile call site: inlining it per segment kind spills registers)
+  const int nseg = rounds + (cut > 0 ? 1 : 0);
+  for (int sg = 0; sg < nseg; ++sg) {
+    const int j = sg < rounds ? sg : 0;
+    int kb = 0, ke = p.K, flags = 0;
+    if (cut > 0 && sg == 0) { ke = cut; flags = RT_SAVE; }
+    if (cut > 0 && sg == rounds) { kb = cut; flags = RT_RESTORE; }
+    if (sg > 0) __syncthreads();  // the previous tile's epilogue scratch / ring is free
+    h_tile<BKM, EM>(p, xcd_remap(w + j * G, nt), kb, ke, smem, flags, part);
+  }
+}
+
+template <bool BKM>
+void launch_h_em(int em, dim3 grid, hipStream_t st, const GemmParams& p, int rounds = 0, f32x4* parts = nullptr) {
+  dim3 block(H_NT);
+#define NSTL_H_LAUNCH(EMv)                                                                        \
+  if (rounds > 0) hipLaunchKernelGGL((gemmhp_kernel<BKM, EMv>), grid, block, 0, st, p, rounds, parts); \
+  else hipLaunchKernelGGL((gemmh_kernel<BKM, EMv>), grid, block, 0, st, p);
+  switch (em) {
+    case EM_BF16: NSTL_H_LAUNCH(EM_BF16) break;
+    case EM_RELU_DROP: NSTL_H_LAUNCH(EM_RELU_DROP) break;
+    case EM_ROPE: NSTL_H_LAUNCH(EM_ROPE) break;
+    case EM_DRELU: NSTL_H_LAUNCH(EM_DRELU) break;
+    case EM_F32: NSTL_H_LAUNCH(EM_F32) break;
+    default: hipLaunchKernelGGL((gemmh_kernel<BKM, EM_GENERIC>), grid, block, 0, st, p); break;
+  }
+#undef NSTL_H_LAUNCH
+}
+
+// ===========================================================================
 // FP8 forward GEMM (BASELINE config C5: fp8 QKV/FFN projections):
 //   C[i][j] = sa[i] * sb[j] * sum_r qa[i][r] qb[j][r]  (+ epilogue)
 // with A [M][K], B [N][K] OCP e4m3 bytes (K-major) and f32 row scales sa (per
@@ -1434,11 +1700,43 @@ void launch_persist_em(int em, int G, int rounds, hipStream_t st, const GemmPara
   }
 }
 
+// NSTL_GEMM_H: 1 runs K-major-A problems without split-K on the two-workgroups-
+// per-CU 128 x 256 kernel (gemmh_kernel); 0 keeps the 256^2 ring kernel
+int getenv_gemm_h() {
+  static const int v = [] {
+    const char* e = getenv("NSTL_GEMM_H");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t st) {
   const int nt = ((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
   dim3 grid(nt, splits), block(BIG_NT);
   if (getenv_ring()) {
     const int em = ring_epi_mode(a, p);
+    const int hmode = getenv_gemm_h();
+    if (hmode && splits == 1 && a->a_kmajor) {
+      const int nth = ((a->M + H_BM - 1) / H_BM) * ((a->N + BIG - 1) / BIG);
+      const int G = 2 * device_cus();
+      const bool multi = em != EM_GENERIC && em != EM_WS && G > 0 && nth % G == 0 && nth / G >= 2 &&
+                         a->K % (4 * R_BK) == 0;
+      if (hmode == 1 || multi) {
+        f32x4* parts = nullptr;
+        if (hmode == 2) {
+          parts = persist_slots(st, G);  // 256 KB slots: the 128 x 256 tile needs half
+          NSTL_CHECK_ARG(parts != nullptr, "nstl_gemm: persistent slot allocation failed");
+        }
+        const dim3 grid(hmode == 2 ? G : nth);
+        const int rounds = hmode == 2 ? nth / G : 0;
+        if (a->b_kmajor) launch_h_em<true>(em, grid, st, p, rounds, parts);
+        else launch_h_em<false>(em, grid, st, p, rounds, parts);
+        NSTL_LAUNCH_CHECK("nstl_gemm (128x256 two per CU)");
+        nstl::count(NSTL_K_GEMM_RING);
+        nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt);
+        return 0;
+      }
+    }
     // multi-round problems with a lean epilogue: the persistent XCD-phased kernel
     const int G = device_cus();
     const bool lean = em == EM_BF16 || em == EM_RELU_DROP || em == EM_ROPE || em == EM_DRELU || em == EM_F32;

@@ -8,6 +8,7 @@ without an ``audio_features.csv`` cache are extracted on the GPU
 (utils/audio/extraction/extract_features.py).
 """
 import os
+import subprocess
 
 import numpy as np
 import pandas as pd
@@ -61,13 +62,28 @@ def process_folder(folder_path, sr, apply_smoothing=False, apply_over_scale=Fals
                    include_slow=False):
     """data_processing.py:44-78.  A video clip (mov preferred over mp4, as the
     reference's ``mov_path or mp4_path``) is decoded by ffmpeg inside
-    load_audio rather than first written to an audio.wav beside it."""
+    load_audio rather than first written to an audio.wav beside it; an existing
+    audio.wav beside the video is used instead, as the reference's extract_audio
+    does (utils/video/mov_extraction.py:44-47).  When ffmpeg fails, the clip falls
+    back to its audio_features.csv cache, or is skipped without one (the
+    reference's extract_audio returns None there, :60-62)."""
     found, audio_features_csv_path = clip_files(folder_path)
     facial_csv_path = found.get('facial')
-    audio_path = found.get('mov') or found.get('mp4') or found.get('wav')
+    video_path = found.get('mov') or found.get('mp4')
+    audio_path = video_path or found.get('wav')
+    extracted = os.path.join(folder_path, 'audio.wav')
+    if video_path and os.path.exists(extracted):
+        print(f"Audio already exists at {extracted}")
+        audio_path = extracted
     if facial_csv_path and (audio_path or os.path.exists(audio_features_csv_path)):
-        audio_features, facial_data = collect_features(audio_path, audio_features_csv_path, facial_csv_path, sr,
-                                                       include_fast=include_fast, include_slow=include_slow)
+        try:
+            audio_features, facial_data = collect_features(audio_path, audio_features_csv_path, facial_csv_path, sr,
+                                                           include_fast=include_fast, include_slow=include_slow)
+        except (subprocess.CalledProcessError, FileNotFoundError) as e:
+            if audio_path != video_path:
+                raise
+            print(f"Failed to extract audio from {video_path}: {e}")
+            return None, None
         if apply_over_scale:
             facial_data = scale_facial_data(facial_data)
         facial_data[:, :61] *= 100

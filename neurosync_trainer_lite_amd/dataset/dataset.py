@@ -153,10 +153,15 @@ class AudioFacialDataset(Dataset):
                 for s, t in window_plan(len(audio_features), len(facial_data), w)]
 
 
-class _Batch:
-    """(src [B, T, 256], trg [B, T, 61]) as fetched by __getitems__."""
+class _Batch(list):
+    """(src [B, T, 256], trg [B, T, 61]) as fetched by __getitems__.  It is also
+    the list of per-window (src_i, trg_i) pairs (views of the pinned batch), so a
+    DataLoader with torch's default_collate (or any collate that takes a list of
+    samples) still works; AudioFacialDataset.collate_fn takes the pinned tensors
+    whole."""
 
     def __init__(self, src, trg):
+        super().__init__(zip(src.unbind(0), trg.unbind(0)))
         self.src, self.trg = src, trg
 
 

@@ -557,6 +557,21 @@ class Seq2SeqEngine:
                 out += [(pre + "ffn.linear1.weight", 1), (pre + "ffn.linear2.weight", 1)]
         return out
 
+    def fp8_scope_desc(self):
+        """What runs in fp8 (bench.py reports it with the C5 line, so lines of
+        different scopes are not compared as if they were one configuration)."""
+        fwd = {"attn+enc_ffn1": "attention q/k/v (self and cross) + encoder FFN linear1 forward GEMMs",
+               "all": "attention q/k/v + every FFN linear1/linear2 forward GEMM"}[self.fp8_scope]
+        groups = sorted({n.split(".", 3)[-1] if n.startswith(("encoder", "decoder")) else n
+                         for n, _ in self.fp8_groups()})
+        enc = sorted({n.split(".", 3)[-1] for n, _ in self.fp8_groups() if n.startswith("encoder")})
+        dec = sorted({n.split(".", 3)[-1] for n, _ in self.fp8_groups() if n.startswith("decoder")})
+        bwd = getattr(self, "fp8_bwd", False)
+        return {"scope": self.fp8_scope, "forward": fwd,
+                "backward": "dX/dW on e4m3 weights/activations and e5m2 output gradients" if bwd else "bf16",
+                "encoder_groups": enc, "decoder_groups": dec, "launches_per_forward": len(self.fp8_groups()),
+                "summary": fwd + ("; fp8 backward" if bwd else "; bf16 backward")} if groups else None
+
     def set_fp8(self, on, scope=None):
         if on and self.dt != torch.bfloat16:
             raise ValueError("fp8 projections need the bf16 compute dtype (use_amp=True)")
@@ -1075,13 +1090,23 @@ class Seq2SeqEngine:
             self.sq_state = (self.g32._version, self._sq_used)
 
     def take_sq_partials(self):
-        """The grouped dW launches' sums of squares of the last backward, if the
-        gradient arena is still what that backward left (torch bumps g32's version
-        on any in-place write through a p.grad view); consumed once."""
+        """The grouped dW launches' sums of squares of the last backward; consumed
+        once.  Only valid when nothing wrote the gradient arena since that
+        backward.  The version check catches in-place writes through a p.grad
+        view, but NOT writers outside autograd's version counter (c10d
+        collectives, ``.data`` aliases, kernels given g32 pointers): callers use
+        this only when their own loop guarantees that (FusedAdam.
+        trust_backward_norm), and every writer in this package calls
+        invalidate_sq()."""
         st, self.sq_state = self.sq_state, None
         if st is None or st[0] != self.g32._version:
             return None
         return self._sq_buf[:st[1]]
+
+    def invalidate_sq(self):
+        """The gradient arena was written after backward: the epilogue partials no
+        longer describe it (the next clip norm re-reads the arena)."""
+        self.sq_state = None
 
     def _ready(self, red, upto):
         """Gradient arena prefix final: its all-reduce is ordered after both streams

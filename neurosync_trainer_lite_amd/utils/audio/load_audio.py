@@ -8,9 +8,9 @@ rates are resampled with a windowed-sinc polyphase filter
 (``scipy.signal.resample_poly``).  That resampler is not soxr: for 88.2 kHz input
 (the reference's own capture rate, and every benchmark input) there is no
 resampling and the samples are identical; for other rates parity is unpinned
-(DESIGN.md).  Other containers (mov/mp4) are decoded by ffmpeg straight to
-mono f32 PCM at 88.2 kHz on a pipe (the reference first writes an audio.wav
-with ffmpeg, utils/video/mov_extraction.py:39-62).
+(DESIGN.md).  Other containers (mov/mp4) are decoded by ffmpeg to mono 16-bit
+PCM at 88.2 kHz on a pipe, the same samples as the audio.wav the reference
+first writes with ffmpeg (utils/video/mov_extraction.py:39-62).
 """
 import io
 import os
@@ -80,13 +80,16 @@ def peak_normalise(y):
 
 
 def _decode_container(path, sr):
-    """Any container ffmpeg reads -> mono f32 at ``sr`` (ffmpeg resamples)."""
+    """Any container ffmpeg reads -> mono samples at ``sr`` (ffmpeg resamples).
+    Decoded as 16-bit PCM and scaled by 1/32768, the samples the reference's
+    audio.wav round trip gives (ffmpeg's default WAV codec is pcm_s16le,
+    utils/video/mov_extraction.py:39-62, read back by librosa)."""
     from ...config import training_config
     sr = sr or TARGET_SR
     cmd = [training_config['ffmpeg_path'], '-v', 'error', '-i', path, '-vn', '-ac', '1', '-ar', str(sr),
-           '-f', 'f32le', '-']
+           '-f', 's16le', '-acodec', 'pcm_s16le', '-']
     pcm = subprocess.run(cmd, check=True, stdout=subprocess.PIPE).stdout
-    return np.frombuffer(pcm, '<f4').astype(np.float32), sr
+    return np.frombuffer(pcm, '<i2').astype(np.float32) / 32768.0, sr
 
 
 def load_audio(audio_path, sr=TARGET_SR):

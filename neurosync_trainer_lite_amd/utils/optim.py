@@ -44,6 +44,13 @@ class FusedAdam(torch.optim.Optimizer):
         # (562.0k vs 561.3k frames/s): the ring GEMMs lose ~5 % to any kernel that
         # holds CUs beside them, about what the update saves
         self.overlap_next_forward = False
+        # The caller guarantees nothing writes the gradients between backward and
+        # step() (train_one_epoch's own loop sets this): the clip norm may then
+        # come from the weight-gradient GEMM epilogues' sums of squares.  Off by
+        # default: drop-in code that averages or rescales p.grad in between (the
+        # reference's multi-GPU path copies into p.grad.data,
+        # utils/training_utils.py:235) gets the norm re-read from the arena.
+        self.trust_backward_norm = False
         self._overlap_allowed = os.environ.get("NSTL_ADAM_OVERLAP", "0") == "1"
         self._upd_stream = None
 
@@ -170,7 +177,8 @@ class FusedAdam(torch.optim.Optimizer):
             return loss
         if self._comm is None:
             eng.sync_pending()
-            sq = eng.take_sq_partials() if max_norm is not None else None
+            sq = eng.take_sq_partials() if max_norm is not None and self.trust_backward_norm else None
+            eng.invalidate_sq()
             if sq is not None:
                 # the weight gradients' sums of squares came from the grouped dW
                 # epilogues; nstl_sumsq covers the rest of the arena (head, embedding,

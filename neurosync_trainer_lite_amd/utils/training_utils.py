@@ -93,9 +93,12 @@ def train_one_epoch(epoch, model, dataloader, criterion, optimizer, device, clip
     pending = _Pending()
     # the next use of the parameters is this loop's forward: the fused optimizer
     # may run its update under that forward (FusedAdam.overlap_next_forward)
+    # and nothing in this loop writes the gradients between backward and step, so
+    # the clip norm may come from the backward's own epilogue partials
     fused = isinstance(optimizer, FusedAdam) and optimizer._comm is None
     if fused:
         optimizer.overlap_next_forward = True
+        optimizer.trust_backward_norm = True
 
     def report(done):
         nonlocal epoch_loss
@@ -126,6 +129,7 @@ def train_one_epoch(epoch, model, dataloader, criterion, optimizer, device, clip
     report(pending.flush())
     if fused:
         optimizer.overlap_next_forward = False
+        optimizer.trust_backward_norm = False
         optimizer._sync()
     print_epoch_summary(epoch, total_epochs, epoch_loss, n_batches, time.time() - start_time)
     save_loss_plot(epoch, train_steps, train_losses, val_steps, val_losses, save_dir="dataset/validation_plots/loss")
@@ -315,6 +319,7 @@ def _average_into_primary(models, devices):
     e0 = _engine_of(models[0])
     with torch.no_grad():
         if e0 is not None and all(_engine_of(m) is not None for m in models):
+            e0.invalidate_sq()
             for m in models[1:]:
                 e0.g32.add_(_engine_of(m).g32.to(e0.device, non_blocking=True))
             e0.g32.div_(len(models))

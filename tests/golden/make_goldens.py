@@ -317,16 +317,49 @@ def gen_formats():
     save("formats.npz", **out)
 
 
+def gen_stats():
+    """The per-epoch comparison statistics file (utils/validation.py:45-137,
+    save_comparison_stats) written by the reference from seeded generated and
+    ground-truth CSVs: generated longer and shorter than the ground truth, a
+    68-column generated file (emotion columns after the 61 used ones), constant
+    columns (NaN correlation) and exact zeros in the ground truth (the MAPE
+    guard).  Inputs are kept as the CSV bytes the reference reads."""
+    import pandas as pd
+    from utils.csv.save_csv import save_generated_data_as_csv
+    from utils.validation import save_comparison_stats
+    out = {}
+    rng = np.random.default_rng(77)
+    names = ["Timecode", "BlendshapeCount"] + ["bs%d" % i for i in range(61)]
+    cases = {"long_gen": (140, 120, False), "short_gen": (90, 120, False), "emotions": (100, 100, True)}
+    with tempfile.TemporaryDirectory() as td:
+        for tag, (ng, nt, emo) in cases.items():
+            gt = rng.random((nt, 61))
+            gt[:, 5] = 0.25                  # constant ground-truth column
+            gt[rng.random((nt, 61)) < 0.05] = 0.0
+            gen = gt[np.arange(ng) % nt] + 0.05 * rng.standard_normal((ng, 61))
+            gen[:, 9] = 0.5                  # constant generated column
+            if emo:
+                gen = np.hstack([gen, rng.random((ng, 7))])
+            gpath, tpath, spath = (os.path.join(td, tag + x) for x in ("_gen.csv", "_gt.csv", "_stats.txt"))
+            save_generated_data_as_csv(gen, gpath, include_emotion_dimensions=emo)
+            pd.DataFrame(np.hstack([np.arange(nt)[:, None] / 60.0, np.full((nt, 1), 61), gt]), columns=names).to_csv(
+                tpath, index=False)
+            save_comparison_stats(gpath, tpath, spath)
+            for k, pth in (("gen", gpath), ("gt", tpath), ("stats", spath)):
+                out["%s_%s" % (k, tag)] = np.frombuffer(open(pth, "rb").read(), np.uint8)
+    save("stats.npz", **out)
+
+
+GENERATORS = {
+    "loss": gen_loss, "rope": gen_rope,
+    "model_tiny": lambda: gen_model("tiny", D=128, H=2, L=2, B=2, T=32, seed=21),
+    "model_mid": lambda: gen_model("mid", D=256, H=4, L=1, B=2, T=128, seed=22, steps=1),
+    "layers_full": gen_full_layers, "autocorr": gen_autocorr, "windows": gen_windows, "augment": gen_augment,
+    "lr": gen_lr, "inference": gen_inference, "formats": gen_formats, "stats": gen_stats,
+}
+
 if __name__ == "__main__":
+    # python tests/golden/make_goldens.py [generator ...]  (default: all)
     torch.set_num_threads(8)
-    gen_loss()
-    gen_rope()
-    gen_model("tiny", D=128, H=2, L=2, B=2, T=32, seed=21)
-    gen_model("mid", D=256, H=4, L=1, B=2, T=128, seed=22, steps=1)
-    gen_full_layers()
-    gen_autocorr()
-    gen_windows()
-    gen_augment()
-    gen_lr()
-    gen_inference()
-    gen_formats()
+    for name in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[name]()

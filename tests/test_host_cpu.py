@@ -197,14 +197,22 @@ def test_lr_lambda_matches_reference(golden):
         np.testing.assert_allclose([f(e) for e in range(len(g[key]))], g[key], rtol=0, atol=1e-15)
 
 
-def test_comparison_stats():
-    from neurosync_trainer_lite_amd.utils.validation import comparison_stats
-    rng = np.random.default_rng(3)
-    gt = rng.random((50, 61))
-    gen = gt[:48] + 0.01 * rng.standard_normal((48, 61))
-    overall, per_dim = comparison_stats(gen, gt)
-    assert overall['Mean Squared Error (MSE)'] == pytest.approx(np.mean((gt[:48] - gen) ** 2))
-    assert len(per_dim) == 61 and per_dim['JawOpen']['MAE'] > 0
+@pytest.mark.parametrize("tag", ["long_gen", "short_gen", "emotions"])
+def test_comparison_stats_file_matches_reference(golden, tag, tmp_path):
+    """The per-epoch statistics file (utils/validation.py:45-137) byte for byte
+    against the reference's own output on the same generated / ground-truth CSVs
+    (tests/golden/stats.npz, make_goldens.py gen_stats): MAE/MAPE/MSE/RMSE/r
+    overall and per dimension, length alignment, NaN correlations of constant
+    columns, the zero-ground-truth MAPE guard."""
+    from neurosync_trainer_lite_amd.utils.validation import comparison_stats, save_comparison_stats
+    g = golden("stats.npz")
+    gpath, tpath, spath = tmp_path / "gen.csv", tmp_path / "gt.csv", tmp_path / "stats.txt"
+    gpath.write_bytes(g["gen_" + tag].tobytes())
+    tpath.write_bytes(g["gt_" + tag].tobytes())
+    save_comparison_stats(str(gpath), str(tpath), str(spath))
+    assert spath.read_bytes() == g["stats_" + tag].tobytes()
+    overall, per_dim = comparison_stats(np.zeros((3, 61)), np.ones((4, 61)))
+    assert overall['Mean Squared Error (MSE)'] == 1.0 and len(per_dim) == 61
 
 
 def test_batched_fetch_equals_per_window(golden):
@@ -226,3 +234,8 @@ def test_batched_fetch_equals_per_window(golden):
     s0, t0 = next(iter(dl))
     want = [ds[train.indices[i]] for i in range(32)]
     assert torch.equal(s0, torch.stack([w[0] for w in want])) and torch.equal(t0, torch.stack([w[1] for w in want]))
+    # torch's default_collate (no collate_fn), over the Subset and the dataset itself
+    for loader_ds, ids in ((train, [train.indices[i] for i in range(32)]), (ds, list(range(32)))):
+        s1, t1 = next(iter(DataLoader(loader_ds, batch_size=32, shuffle=False)))
+        want = [ds[i] for i in ids]
+        assert torch.equal(s1, torch.stack([w[0] for w in want])) and torch.equal(t1, torch.stack([w[1] for w in want]))

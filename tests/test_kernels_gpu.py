@@ -973,10 +973,11 @@ def _cus():
     return torch.cuda.get_device_properties(0).multi_processor_count
 
 
-# the persistent kernel is opt-in (NSTL_GEMM_PERSIST=1, read once per process):
-# tools/run_persist.sh runs these tests with it on
-persistent = pytest.mark.skipif(os.environ.get("NSTL_GEMM_PERSIST") != "1",
-                                reason="persistent GEMM off (NSTL_GEMM_PERSIST=1 enables it)")
+# the persistent kernels are opt-in (NSTL_GEMM_PERSIST=1: the 256^2 XCD-phased
+# grid; NSTL_GEMM_H=2: the two-per-CU 128 x 256 grid; read once per process):
+# tools/run_persist.sh and tools/run_gemm_h.sh run these tests with them on
+persistent = pytest.mark.skipif(os.environ.get("NSTL_GEMM_PERSIST") != "1" and os.environ.get("NSTL_GEMM_H") != "2",
+                                reason="persistent GEMM off (NSTL_GEMM_PERSIST=1 / NSTL_GEMM_H=2 enable it)")
 
 
 def _halves(run, M):

@@ -414,6 +414,7 @@ def test_fused_clip_norm_matches_arena_sumsq(monkeypatch, steps):
     for fused in ("1", "0"):
         monkeypatch.setenv("NSTL_FUSED_NORM", fused)
         cfg, model, crit, opt, params = make(256, 4, 2, 11, amp=True, dropout=0.0)
+        opt.trust_backward_norm = True  # as train_one_epoch's own loop sets it
         g = torch.Generator().manual_seed(6)
         src = torch.randn(4, 128, 256, generator=g).to(DEV)
         trg = (torch.randn(4, 128, 61, generator=g) * 20).to(DEV)
@@ -436,6 +437,7 @@ def test_fused_clip_norm_matches_arena_sumsq(monkeypatch, steps):
     # an in-place edit of a gradient after backward: the step re-reads the arena
     monkeypatch.setenv("NSTL_FUSED_NORM", "1")
     cfg, model, crit, opt, params = make(256, 4, 2, 11, amp=True, dropout=0.0)
+    opt.trust_backward_norm = True
     opt.zero_grad()
     crit(model(src), trg).backward()
     eng = opt._bind()
@@ -445,3 +447,52 @@ def test_fused_clip_norm_matches_arena_sumsq(monkeypatch, steps):
     ref = torch.cat([p.grad.detach().double().flatten().cpu() for p in model.parameters()]).norm().item()
     opt.step(max_norm=0.5)
     assert abs(opt.last_norm.item() - ref) <= 1e-5 * ref
+
+
+@pytest.mark.parametrize("writer", ["grad_data", "all_reduce"])
+def test_clip_norm_sees_gradient_writes_outside_autograd(monkeypatch, writer):
+    """Drop-in code that rescales or averages p.grad between backward and step --
+    through ``p.grad.data`` (the reference's multi-GPU path, utils/training_utils.py
+    :235) or a c10d collective -- writes the arena without bumping g32's version.
+    FusedAdam does not trust the backward's epilogue partials unless its caller
+    says so (trust_backward_norm, off by default), so the clip norm is the one of
+    the gradients as they stand at step()."""
+    import torch.distributed as dist
+    monkeypatch.setenv("NSTL_FUSED_NORM", "1")
+    cfg, model, crit, opt, params = make(256, 4, 2, 11, amp=True, dropout=0.0)
+    g = torch.Generator().manual_seed(6)
+    src = torch.randn(4, 128, 256, generator=g).to(DEV)
+    trg = (torch.randn(4, 128, 61, generator=g) * 20).to(DEV)
+    opt.zero_grad()
+    crit(model(src), trg).backward()
+    eng = opt._bind()
+    assert eng.sq_state is not None  # the backward left its partials
+    before = torch.cat([p.grad.detach().double().flatten().cpu() for p in model.parameters()]).norm().item()
+    if writer == "grad_data":
+        for p in model.parameters():
+            p.grad.data.mul_(0.25)
+    else:
+        init = not dist.is_initialized()
+        if init:
+            dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1)
+        try:
+            for p in model.parameters():
+                t = p.grad.detach().cpu()
+                dist.all_reduce(t)
+                p.grad.data.copy_(t * 0.25)
+        finally:
+            if init:
+                dist.destroy_process_group()
+    ref = torch.cat([p.grad.detach().double().flatten().cpu() for p in model.parameters()]).norm().item()
+    assert abs(ref - 0.25 * before) <= 1e-5 * ref
+    opt.step(max_norm=0.5)
+    torch.cuda.synchronize()
+    assert abs(opt.last_norm.item() - ref) <= 1e-5 * ref, (opt.last_norm.item(), ref, before)
+    assert eng.sq_state is None
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
