@@ -95,7 +95,8 @@ def measure_gemm_counters(args):
                "-d", d, "-o", "run", "--output-format", "csv",
                "--", sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
                "--no-parity", "--feature-steps", "0", "--feed-steps", "0", "--no-traffic",
-               "--batch", str(args.batch), "--seq", str(args.seq)] + (["--fp8"] if args.fp8 else [])
+               "--batch", str(args.batch), "--seq", str(args.seq)] + (["--fp8"] if args.fp8 else []) + \
+              (["--fp8-bwd"] if args.fp8_bwd else [])
         env = dict(os.environ, TMPDIR="/tmp")
         log("counters: rocprofv3 --pmc %s pass (child bench, 1+1 steps)" % " ".join(counters))
         r = subprocess.run(cmd, env=env, cwd="/tmp", stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
@@ -354,6 +355,8 @@ def main():
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE config C5: q/k/v + FFN forward GEMMs on e4m3 operands (row-wise scales); "
                          "C5 also doubles the clip length: --seq 256 --batch 64")
+    ap.add_argument("--fp8-bwd", action="store_true",
+                    help="with --fp8: every FFN linear2 input-gradient GEMM on e4m3 operands too")
     args = ap.parse_args()
 
     from neurosync_trainer_lite_amd import _hip as K
@@ -371,7 +374,7 @@ def main():
     dev = torch.device("cuda", local)
     cfg = dict(training_config)
     B, T = args.batch, args.seq
-    cfg.update(micro_batch_size=T, frame_size=T, batch_size=B, use_fp8=args.fp8)
+    cfg.update(micro_batch_size=T, frame_size=T, batch_size=B, use_fp8=args.fp8, fp8_backward=args.fp8_bwd)
     torch.manual_seed(1234)  # identical init on every rank
     model = build_model(cfg, dev)
     model.train()
@@ -498,7 +501,7 @@ def main():
     if ev8:
         ms8 = sum(a.elapsed_time(b) for a, b, _, _, _, _ in ev8)
         tf8 = sum(f for _, _, f, _, _, _ in ev8) / (ms8 * 1e-3) / 1e12
-        fp8_roof = {"bound": "mfma", "kernel": "gemm256f8_kernel (e4m3 attention q/k/v + encoder FFN1 forward, row scales)",
+        fp8_roof = {"bound": "mfma", "kernel": "gemm256f8_kernel (e4m3 operands, row scales; which GEMMs: config.fp8_scope)",
                     "achieved": round(tf8, 1), "peak": FP8_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(tf8 / FP8_DENSE_PEAK_TFLOPS, 4), "launches": len(ev8),
                     "avg_launch_us": round(ms8 * 1e3 / len(ev8), 2),

@@ -112,6 +112,14 @@ typedef struct nstl_fp8_job {
   int rows, cols;
 } nstl_fp8_job;
 int nstl_fp8_quant_rows(int x_dtype, const nstl_fp8_job* jobs, int n, void* stream);
+/* The transposed form: job (x [rows][ldx], cols) writes Q [cols][ldq] and scale
+ * [cols] = nstl_fp8_quant_rows of X^T, i.e. per-column scales.  The weight operand
+ * of the fp8 input-gradient GEMM (dX = dY W, contraction over W's rows): the
+ * transposed weights, K-major over the output channels, one scale per input
+ * channel.  rows % 64 == 0, cols % 64 == 0, ldq % 16 == 0 and ldq >= rows.
+ * Replaces nothing in the reference (fp8 is BASELINE config C5's precision
+ * choice; the reference's backward of utils/model.py:153-158 runs under autocast). */
+int nstl_fp8_quant_cols(int x_dtype, const nstl_fp8_job* jobs, int n, void* stream);
 
 /* Non-causal multi-head attention with per-head RoPE already applied to q,k
  * (by the projection epilogue), softmax scale 1/sqrt(dh), attention-probability
@@ -175,9 +183,10 @@ typedef struct nstl_ln_args {
   const void* dout2;       /* optional dtype [rows][D], added to dout: the input gradient
                               of a Linear fed by this LN's output, kept in dtype as the
                               reference's autocast casts it (utils/model.py Linears) */
-  /* forward, optional (bf16 only): the row-wise e4m3 copy of `out` [rows][ldq8] and
-     its row scales, exactly nstl_fp8_quant_rows(out) (the fp8 q/k/v / FFN GEMM
-     operand of BASELINE config C5) */
+  /* optional (bf16 only): the row-wise e4m3 copy [rows][ldq8] and its row scales,
+     exactly nstl_fp8_quant_rows of the stored values (BASELINE config C5): in the
+     forward of `out` (the fp8 q/k/v / FFN GEMM operand), in the backward of
+     `dbranch` (the A operand of the fp8 FFN linear2 input-gradient GEMM) */
   void* q8; int64_t ldq8; float* q8_scale;
 } nstl_ln_args;
 int nstl_ln_fwd(const nstl_ln_args* args, void* stream);

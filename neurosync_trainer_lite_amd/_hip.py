@@ -110,7 +110,7 @@ EXPORTS = [
     "nstl_colsum", "nstl_rope",
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_clip_coef", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
     "nstl_features", "nstl_stft_mel", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
-    "nstl_version", "nstl_fp8_quant_rows", "nstl_kernel_counts", "nstl_kernel_counts_reset",
+    "nstl_version", "nstl_fp8_quant_rows", "nstl_fp8_quant_cols", "nstl_kernel_counts", "nstl_kernel_counts_reset",
     "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs",
 ]
 
@@ -135,6 +135,7 @@ def lib():
         L.nstl_gemm.argtypes = [P(GemmArgs), _vp]
         L.nstl_gemm_grouped.argtypes = [P(GemmArgs), _i32, _vp]
         L.nstl_fp8_quant_rows.argtypes = [_i32, P(Fp8Job), _i32, _vp]
+        L.nstl_fp8_quant_cols.argtypes = [_i32, P(Fp8Job), _i32, _vp]
         L.nstl_gemm_colsum_rows.argtypes = [P(GemmArgs)]
         L.nstl_gemm_colsum_rows.restype = _i32
         L.nstl_gemm_relu_mask_words.argtypes = [P(GemmArgs)]
@@ -297,10 +298,7 @@ def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=N
     return a
 
 
-def fp8_quant_rows(jobs, stream=None):
-    """Row-wise e4m3 quantization (nstl_fp8_quant_rows): `jobs` is a list of
-    (x, rows, cols, q, scale) with x f32/bf16 [rows, >= cols], q float8_e4m3fn
-    [rows, >= cols] and scale f32 [rows]; all jobs share x's dtype."""
+def _fp8_jobs(fn, jobs, stream, what):
     if not jobs:
         return
     dt = jobs[0][0].dtype
@@ -309,10 +307,23 @@ def fp8_quant_rows(jobs, stream=None):
         arr = (Fp8Job * len(chunk))()
         for i, (x, rows, cols, q, scale) in enumerate(chunk):
             if x.dtype != dt or q.dtype != torch.float8_e4m3fn or scale.dtype != torch.float32:
-                raise TypeError("fp8_quant_rows: x of one dtype, q float8_e4m3fn, scale float32")
+                raise TypeError("%s: x of one dtype, q float8_e4m3fn, scale float32" % what)
             arr[i] = Fp8Job(x.data_ptr(), x.stride(0), q.data_ptr(), q.stride(0), scale.data_ptr(), rows, cols)
-        check(lib().nstl_fp8_quant_rows(dtype_code(dt), arr, len(chunk), stream if stream is not None else stream_of()),
-              "nstl_fp8_quant_rows")
+        check(fn(dtype_code(dt), arr, len(chunk), stream if stream is not None else stream_of()), what)
+
+
+def fp8_quant_rows(jobs, stream=None):
+    """Row-wise e4m3 quantization (nstl_fp8_quant_rows): `jobs` is a list of
+    (x, rows, cols, q, scale) with x f32/bf16 [rows, >= cols], q float8_e4m3fn
+    [rows, >= cols] and scale f32 [rows]; all jobs share x's dtype."""
+    _fp8_jobs(lib().nstl_fp8_quant_rows, jobs, stream, "nstl_fp8_quant_rows")
+
+
+def fp8_quant_cols(jobs, stream=None):
+    """Column-wise (transposed) e4m3 quantization (nstl_fp8_quant_cols): jobs
+    (x, rows, cols, q, scale) with x [rows, >= cols], q float8_e4m3fn [cols, >= rows]
+    = quant_rows(x^T), scale f32 [cols]."""
+    _fp8_jobs(lib().nstl_fp8_quant_cols, jobs, stream, "nstl_fp8_quant_cols")
 
 
 def attn_args(dtype, B, T, H, q, q_ld, k, k_ld, v, v_ld, o, o_ld, lse, p_drop, seed, dh=64):

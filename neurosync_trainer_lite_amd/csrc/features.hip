@@ -100,20 +100,28 @@ __global__ __launch_bounds__(NT) void autocorr_kernel(const float* y, int64_t n,
 // w[k+l0..k+l0+30] from LDS (16-byte reads) for 256 f64 FMAs -- no register
 // shifting (the sliding window above moves 7 registers per 8 FMAs).  12 lag
 // groups x 20 chunks = 240 threads; chunk partials summed in LDS in chunk order.
+// r3: the partials overwrite the frame image once every thread is done with it
+// (one barrier), so a workgroup holds max(frame, partials) = 31 KB of LDS instead
+// of 46 KB (5 workgroups per CU instead of 3), and every thread forms lag 0 from
+// the same partials in the same order, so the normalisation is one pass over
+// registers instead of a second read-modify-write of the output.
 constexpr int AC2_LG = 16, AC2_GROUPS = 12, AC2_CHUNKS = 20;
 constexpr int AC2_NT = 256;
 
 size_t ac2_chunk(int L) { return ((size_t)(L + AC2_CHUNKS - 1) / AC2_CHUNKS + AC2_LG - 1) / AC2_LG * AC2_LG; }
 size_t ac2_wlen(int L) { return ac2_chunk(L) * AC2_CHUNKS + AC2_LG * AC2_GROUPS + 2 * AC2_LG; }
-size_t ac2_lds(int L) { return (ac2_wlen(L) + (size_t)AC2_CHUNKS * AC2_LG * AC2_GROUPS + 8) * sizeof(double); }
+size_t ac2_lds(int L) {
+  return (std::max(ac2_wlen(L), (size_t)AC2_CHUNKS * AC2_LG * AC2_GROUPS) + 8) * sizeof(double);
+}
 
 __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64_t n, int L, int hop, int n_lags,
                                                             const double* __restrict__ hann, double* out, int chunk,
                                                             int wlen) {
   extern __shared__ __attribute__((aligned(16))) double ac2_smem[];
   double* w = ac2_smem;                  // [wlen]: the windowed frame, zero tail
-  double* part = w + wlen;               // [AC2_CHUNKS][AC2_LG * AC2_GROUPS]
-  double* red = part + AC2_CHUNKS * AC2_LG * AC2_GROUPS;  // [4] wave sums, [4] lag 0
+  double* part = ac2_smem;               // [AC2_CHUNKS][AC2_LG * AC2_GROUPS], over w after the products
+  const int wpart = std::max(wlen, AC2_CHUNKS * AC2_LG * AC2_GROUPS);
+  double* red = ac2_smem + wpart;        // [4] wave sums
   const int f = blockIdx.x, tid = threadIdx.x;
   const int64_t start = (int64_t)f * hop - L / 2;
   double s = 0.0;
@@ -138,13 +146,14 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
     w[k] = (double)c * hann[k];
   }
   __syncthreads();
-  if (tid < AC2_GROUPS * AC2_CHUNKS) {
-    const int g = tid % AC2_GROUPS, c = tid / AC2_GROUPS;
-    const int l0 = g * AC2_LG;
-    const int k0 = c * chunk, k1 = min(L, k0 + chunk);
-    double acc[AC2_LG];
+  const bool worker = tid < AC2_GROUPS * AC2_CHUNKS;
+  const int g = tid % AC2_GROUPS, c = tid / AC2_GROUPS;
+  const int l0 = g * AC2_LG;
+  double acc[AC2_LG];
 #pragma unroll
-    for (int r = 0; r < AC2_LG; ++r) acc[r] = 0.0;
+  for (int r = 0; r < AC2_LG; ++r) acc[r] = 0.0;
+  if (worker) {
+    const int k0 = c * chunk, k1 = min(L, k0 + chunk);
     for (int kb = k0; kb < k1; kb += AC2_LG) {
       double a[AC2_LG], b[2 * AC2_LG];
 #pragma unroll
@@ -164,21 +173,24 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
 #pragma unroll
         for (int r = 0; r < AC2_LG; ++r) acc[r] = fma(a[j], b[j + r], acc[r]);
     }
+  }
+  __syncthreads();  // every thread is done with w: the partials take its place
+  if (worker) {
 #pragma unroll
-    for (int r = 0; r < AC2_LG; ++r) part[c * AC2_LG * AC2_GROUPS + l0 + r] = acc[r];
+    for (int r = 0; r < AC2_LG; r += 2)
+      *(double2*)(part + c * AC2_LG * AC2_GROUPS + l0 + r) = make_double2(acc[r], acc[r + 1]);
   }
   __syncthreads();
-  double* ac0 = red + 4;
-  for (int lag = tid; lag <= n_lags; lag += AC2_NT) {
-    double acc = 0.0;
+  // lag 0, summed by every thread in chunk order (the value the lag loop forms for lag 0)
+  double ac0 = 0.0;
 #pragma unroll
-    for (int c = 0; c < AC2_CHUNKS; ++c) acc += part[c * AC2_LG * AC2_GROUPS + lag];
-    if (lag == 0) *ac0 = acc;
-    if (lag > 0) out[(int64_t)f * n_lags + (lag - 1)] = acc;
+  for (int cc = 0; cc < AC2_CHUNKS; ++cc) ac0 += part[cc * AC2_LG * AC2_GROUPS];
+  for (int lag = 1 + tid; lag <= n_lags; lag += AC2_NT) {
+    double v = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < AC2_CHUNKS; ++cc) v += part[cc * AC2_LG * AC2_GROUPS + lag];
+    out[(int64_t)f * n_lags + (lag - 1)] = ac0 != 0.0 ? v / ac0 : v;
   }
-  __syncthreads();
-  if (*ac0 != 0.0)
-    for (int lag = tid; lag < n_lags; lag += AC2_NT) out[(int64_t)f * n_lags + lag] /= *ac0;
 }
 
 // np.hanning(L) (symmetric), computed on the host in f64 once per (device, L)

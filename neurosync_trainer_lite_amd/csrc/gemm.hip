@@ -1595,7 +1595,7 @@ int ring_epi_mode(const nstl_gemm_args* a, const GemmParams& p) {
     case NSTL_EPI_BIAS: return EM_BF16;
     case NSTL_EPI_BIAS_RELU_DROP: return (a->N % 2 == 0) ? EM_RELU_DROP : EM_GENERIC;
     case NSTL_EPI_BIAS_ROPE: return EM_ROPE;
-    case NSTL_EPI_DRELU_DROP: return a->dtype == NSTL_BF16 ? EM_DRELU : EM_GENERIC;
+    case NSTL_EPI_DRELU_DROP: return a->dtype == NSTL_BF16 || a->dtype == NSTL_FP8 ? EM_DRELU : EM_GENERIC;
   }
   return EM_GENERIC;
 }
@@ -1882,18 +1882,21 @@ int gemm_f8(const nstl_gemm_args* a, GemmParams& p, hipStream_t st) {
   NSTL_CHECK_ARG(a->a_kmajor && a->b_kmajor, "nstl_gemm: FP8 needs K-major A and B (Y = X W^T)");
   NSTL_CHECK_ARG(a->K % 64 == 0, "nstl_gemm: FP8 needs K %% 64 == 0 (got %d)", a->K);
   NSTL_CHECK_ARG(a->a_scale && a->b_scale, "nstl_gemm: FP8 needs the row scales a_scale [M] and b_scale [N]");
-  NSTL_CHECK_ARG(a->split_k <= 1 && !a->colsum_part, "nstl_gemm: FP8: no split-K, no colsum_part");
+  NSTL_CHECK_ARG(a->split_k <= 1, "nstl_gemm: FP8: no split-K");
   const int em = ring_epi_mode(a, p);
-  NSTL_CHECK_ARG(em == EM_BF16 || em == EM_RELU_DROP || em == EM_ROPE || em == EM_F32,
-                 "nstl_gemm: FP8 supports the NONE / BIAS / BIAS_RELU_DROP / BIAS_ROPE epilogues "
+  NSTL_CHECK_ARG(em == EM_BF16 || em == EM_RELU_DROP || em == EM_ROPE || em == EM_DRELU || em == EM_F32,
+                 "nstl_gemm: FP8 supports the NONE / BIAS / BIAS_RELU_DROP / BIAS_ROPE / DRELU_DROP epilogues "
                  "(bf16 out without beta, or f32 out without epilogue)");
-  NSTL_CHECK_ARG(!a->relu_mask || em == EM_RELU_DROP, "nstl_gemm: relu_mask needs the ReLU-dropout epilogue");
+  NSTL_CHECK_ARG(!a->relu_mask || em == EM_RELU_DROP || em == EM_DRELU,
+                 "nstl_gemm: relu_mask needs the ReLU-dropout / dReLU epilogue");
+  NSTL_CHECK_ARG(!a->colsum_part || em == EM_DRELU, "nstl_gemm: FP8: colsum_part needs the dReLU epilogue");
   const int nt = ((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
   dim3 grid(nt), block(BIG_NT);
   switch (em) {
     case EM_BF16: hipLaunchKernelGGL((gemm256f8_kernel<EM_BF16>), grid, block, 0, st, p); break;
     case EM_RELU_DROP: hipLaunchKernelGGL((gemm256f8_kernel<EM_RELU_DROP>), grid, block, 0, st, p); break;
     case EM_ROPE: hipLaunchKernelGGL((gemm256f8_kernel<EM_ROPE>), grid, block, 0, st, p); break;
+    case EM_DRELU: hipLaunchKernelGGL((gemm256f8_kernel<EM_DRELU>), grid, block, 0, st, p); break;
     default: hipLaunchKernelGGL((gemm256f8_kernel<EM_F32>), grid, block, 0, st, p); break;
   }
   NSTL_LAUNCH_CHECK("nstl_gemm (FP8)");
@@ -1999,6 +2002,9 @@ extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream
 extern "C" int nstl_gemm_colsum_rows(const nstl_gemm_args* a) {
   GemmParams p;
   if (a == nullptr || make_params(a, p) != 0) return 0;
+  if (a->dtype == NSTL_FP8)  // the fp8 ring kernel's dReLU epilogue (same 128-row partial layout)
+    return a->epilogue == NSTL_EPI_DRELU_DROP && a->split_k <= 1 && a->c_dtype == NSTL_BF16 &&
+                   ring_epi_mode(a, p) == EM_DRELU ? (a->M + 127) / 128 : 0;
   if (!big_ok(a) || a->epilogue != NSTL_EPI_DRELU_DROP || a->split_k > 1 || !getenv_ring()) return 0;
   if (ring_epi_mode(a, p) != EM_DRELU) return 0;
   return (a->M + 127) / 128;
@@ -2008,7 +2014,8 @@ extern "C" int64_t nstl_gemm_relu_mask_words(const nstl_gemm_args* a) {
   GemmParams p;
   if (a == nullptr || make_params(a, p) != 0) return 0;
   if (a->dtype == NSTL_FP8) {
-    if (a->split_k > 1 || a->c_dtype != NSTL_BF16 || ring_epi_mode(a, p) != EM_RELU_DROP) return 0;
+    const int em = ring_epi_mode(a, p);
+    if (a->split_k > 1 || a->c_dtype != NSTL_BF16 || (em != EM_RELU_DROP && em != EM_DRELU)) return 0;
     return (int64_t)((a->M + 63) / 64) * 8 * ((a->N + 7) / 8);
   }
   if (!big_ok(a) || a->split_k > 1 || !getenv_ring() || a->dtype != NSTL_BF16 || a->c_dtype != NSTL_BF16) return 0;

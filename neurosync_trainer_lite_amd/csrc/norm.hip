@@ -286,6 +286,35 @@ NSTL_DEV void store4(T* p, const float* v) {
   }
 }
 
+// The row-wise e4m3 copy of a stored row v (already rounded to the storage type),
+// the same arithmetic as nstl_fp8_quant_rows: the forward's LN output (the next fp8
+// projection's operand) or, in the backward, dbranch (the fp8 input-gradient GEMM's
+// A operand).  Interleaved column map: lane l owns columns k*64G + G*l .. +G-1.
+template <int VPL, int G>
+NSTL_DEV void q8_row(const LnParams& p, int row, int lane, const float (&v)[VPL]) {
+  constexpr int NK = VPL / G, SPAN = 64 * G;
+  float am = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) am = fmaxf(am, fabsf(v[j]));
+  am = wave_max(am);
+  const float inv = am > 0.f ? 448.f / am : 1.f;
+  if (lane == 0) p.q8_scale[row] = am > 0.f ? am / 448.f : 1.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    float x[G];
+#pragma unroll
+    for (int e = 0; e < G; ++e) x[e] = fminf(fmaxf(v[G * k + e] * inv, -448.f), 448.f);
+    uint32_t b[G / 4];
+#pragma unroll
+    for (int h = 0; h < G / 4; ++h)
+      b[h] = ((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h], x[4 * h + 1], 0, false) & 0xffffu) |
+             (((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h + 2], x[4 * h + 3], 0, false) & 0xffffu) << 16);
+    uint8_t* q = p.q8 + (int64_t)row * p.ldq8 + k * SPAN + G * lane;
+    if constexpr (G == 8) *(uint2*)q = make_uint2(b[0], b[1]);
+    else *(uint32_t*)q = b[0];
+  }
+}
+
 template <typename T, int VPL, int G>
 __global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
   constexpr int NK = VPL / G;  // G-column groups per lane
@@ -363,6 +392,7 @@ __global__ __launch_bounds__(NTB) void ln_bwd_kernel_il(LnParams p) {
       for (int k = 0; k < NK; ++k) storeG<T, G>((T*)p.dbranch + base + k * SPAN, d + G * k);
 #pragma unroll
       for (int j = 0; j < VPL; ++j) dyb[j] += d[j];
+      if (p.q8) q8_row<VPL, G>(p, row, lane, d);  // fp8 backward: the e4m3 copy of dbranch
     }
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
@@ -463,28 +493,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel_il(LnParams p) {
     p.mean[row] = mean;
     p.rstd[row] = rstd;
   }
-  if (p.q8) {  // the same arithmetic as nstl_fp8_quant_rows on the stored row
-    float am = 0.f;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) am = fmaxf(am, fabsf(o[j]));
-    am = wave_max(am);
-    const float inv = am > 0.f ? 448.f / am : 1.f;
-    if (lane == 0) p.q8_scale[row] = am > 0.f ? am / 448.f : 1.f;
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-      float v[G];
-#pragma unroll
-      for (int e = 0; e < G; ++e) v[e] = fminf(fmaxf(o[G * k + e] * inv, -448.f), 448.f);
-      uint32_t b[G / 4];
-#pragma unroll
-      for (int h = 0; h < G / 4; ++h)
-        b[h] = ((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h], v[4 * h + 1], 0, false) & 0xffffu) |
-               (((uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h + 2], v[4 * h + 3], 0, false) & 0xffffu) << 16);
-      uint8_t* q = p.q8 + (int64_t)row * p.ldq8 + k * SPAN + G * lane;
-      if constexpr (G == 8) *(uint2*)q = make_uint2(b[0], b[1]);
-      else *(uint32_t*)q = b[0];
-    }
-  }
+  if (p.q8) q8_row<VPL, G>(p, row, lane, o);
   if (p.rot_out) {
     const int t = row % p.rope_T, half = p.D >> 1;
 #pragma unroll
@@ -585,6 +594,9 @@ extern "C" int nstl_ln_bwd(const nstl_ln_args* a, void* stream) {
   if (rc) return rc;
   NSTL_CHECK_ARG(a->s_in && a->dout && a->ds && a->mean && a->rstd, "nstl_ln_bwd: null tensor");
   NSTL_CHECK_ARG(a->dgamma_part && a->dbeta_part && a->n_part > 0, "nstl_ln_bwd: partials");
+  NSTL_CHECK_ARG(!a->q8 || (a->dbranch && a->dtype == NSTL_BF16 && a->q8_scale && a->D % 256 == 0 &&
+                            a->ldq8 >= a->D && a->ldq8 % 16 == 0 && ((uintptr_t)a->q8 % 16) == 0),
+                 "nstl_ln_bwd: q8 needs dbranch, bf16, D %% 256 == 0, q8_scale and a 16-byte aligned ldq8 >= D");
   // n_part blocks; each needs at least one row per wave (4 waves; 8 when D % 256 == 0)
   const int nw = (a->D % 256 == 0) ? NTB / 64 : NT / 64;
   const int grid = std::min(a->n_part, (a->rows + nw - 1) / nw);

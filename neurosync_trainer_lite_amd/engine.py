@@ -234,6 +234,13 @@ class Seq2SeqEngine:
         self._fp8_w = None         # (weight name, rows) -> (e4m3 [rows*N, K], f32 scales [rows*N])
         self._fp8_act = {}         # M -> (e4m3 scratch [M, max(D, Fd)], scales [M], e4m3 mem, mem scales)
         self._xq = {}              # data_ptr of an activation -> its live e4m3 copy (q, scales)
+        # fp8 backward (C5, set_fp8(..., backward=True) / config key 'fp8_backward'):
+        # the FFN linear2 input gradient dh = dy W2 (dReLU epilogue) on e4m3 operands
+        # -- dy row-quantized by the LayerNorm backward that writes it, W2^T
+        # column-quantized once per forward.  Every other backward GEMM stays bf16.
+        self.fp8_bwd = False
+        self._fp8_wt = None        # weight name -> (e4m3 W^T [in, out], f32 scales [in])
+        self._fp8_dy = {}          # M -> (e4m3 [M, D], scales [M])
         # NSTL_FUSED_NORM=0: the clip norm re-reads the whole gradient arena
         # (nstl_sumsq) instead of taking the grouped weight-gradient GEMMs' per-tile
         # sums of squares (their epilogue, nstl_gemm_args.sq_part) plus nstl_sumsq
@@ -566,13 +573,23 @@ class Seq2SeqEngine:
                          for n, _ in self.fp8_groups()})
         enc = sorted({n.split(".", 3)[-1] for n, _ in self.fp8_groups() if n.startswith("encoder")})
         dec = sorted({n.split(".", 3)[-1] for n, _ in self.fp8_groups() if n.startswith("decoder")})
-        bwd = getattr(self, "fp8_bwd", False)
+        bwd = self.fp8_bwd
         return {"scope": self.fp8_scope, "forward": fwd,
-                "backward": "dX/dW on e4m3 weights/activations and e5m2 output gradients" if bwd else "bf16",
+                "backward": ("FFN linear2 input-gradient GEMMs (every layer) on e4m3 dy (row scales, from the "
+                             "LayerNorm backward) and e4m3 W2^T (input-channel scales); other backward GEMMs bf16")
+                if bwd else "bf16",
+                "backward_launches": len(self.fp8_bwd_groups()) if bwd else 0,
                 "encoder_groups": enc, "decoder_groups": dec, "launches_per_forward": len(self.fp8_groups()),
                 "summary": fwd + ("; fp8 backward" if bwd else "; bf16 backward")} if groups else None
 
-    def set_fp8(self, on, scope=None):
+    def fp8_bwd_groups(self):
+        """Weights whose input-gradient GEMM runs in fp8 when fp8_bwd is on: every
+        FFN linear2 (encoder and decoder).  The forward's MSE gate does not apply to
+        the backward; the gradient bound is tests/test_fp8_gpu.py's."""
+        return ["%s.%d.ffn.linear2.weight" % (st, l) for st in ("encoder.transformer_encoder",
+                                                               "decoder.transformer_decoder") for l in range(self.L)]
+
+    def set_fp8(self, on, scope=None, backward=None):
         if on and self.dt != torch.bfloat16:
             raise ValueError("fp8 projections need the bf16 compute dtype (use_amp=True)")
         if scope is not None:
@@ -581,6 +598,8 @@ class Seq2SeqEngine:
             if scope != self.fp8_scope:
                 self._fp8_w = None  # re-quantize the new set
             self.fp8_scope = scope
+        if backward is not None:
+            self.fp8_bwd = bool(backward)
         self.fp8 = bool(on)
 
     def _fp8_on(self, name, rows=1):
@@ -601,6 +620,22 @@ class Seq2SeqEngine:
             W = self.w(name, rows)
             jobs.append((W, W.shape[0], W.shape[1], q, sc))
         K.fp8_quant_rows(jobs, stream=self.st)
+        if self.fp8_bwd:
+            if self._fp8_wt is None:
+                self._fp8_wt = {}
+                for name in self.fp8_bwd_groups():
+                    n, k = self.w(name).shape
+                    self._fp8_wt[name] = (torch.empty(k, n, dtype=torch.float8_e4m3fn, device=self.device),
+                                          torch.empty(k, dtype=torch.float32, device=self.device))
+            K.fp8_quant_cols([(self.w(name), self.w(name).shape[0], self.w(name).shape[1], q, sc)
+                              for name, (q, sc) in self._fp8_wt.items()], stream=self.st)
+
+    def _fp8_dy_bufs(self, M):
+        """e4m3 copy of the LayerNorm backward's dbranch [M, D] and its row scales."""
+        if M not in self._fp8_dy:
+            self._fp8_dy = {M: (torch.empty(M, self.D, dtype=torch.float8_e4m3fn, device=self.device),
+                                torch.empty(M, dtype=torch.float32, device=self.device))}
+        return self._fp8_dy[M]
 
     def _fp8_bufs(self, M):
         if M not in self._fp8_act:
@@ -736,15 +771,21 @@ class Seq2SeqEngine:
             self._main.wait_stream(self._side)
             self._side_reads = []
 
-    def _dx(self, dy, wname, rows, out, beta, epi=K.EPI_NONE, aux=None, p_drop=0.0, colsum=None, relu_mask=None):
+    def _dx(self, dy, wname, rows, out, beta, epi=K.EPI_NONE, aux=None, p_drop=0.0, colsum=None, relu_mask=None,
+            dyq=None):
         """out (+)= dy W  (W: [N][K] read as [r][j]).  colsum = (partials, grad(b), beta):
         the bias gradient of the Linear whose input gradient `out` is, from the
-        epilogue's column sums; returns False when the kernel cannot produce them."""
+        epilogue's column sums; returns False when the kernel cannot produce them.
+        `dyq` = (e4m3 dy, row scales): the fp8 form, on W^T's e4m3 copy."""
         W = self.w(wname, rows)
         n, k = W.shape
         self._guard(out)
         kw = dict(a_kmajor=True, b_kmajor=False, beta=beta, epilogue=epi, aux=aux,
                   ld_aux=aux.stride(0) if aux is not None else 0, p_drop=p_drop)
+        if dyq is not None:
+            qt, st = self._fp8_wt[wname]
+            dy, W = dyq[0], qt
+            kw.update(b_kmajor=True, a_scale=dyq[1], b_scale=st)
         if relu_mask is not None and 0 < K.gemm_relu_mask_words(dy, W, out, dy.shape[0], k, n, **kw) \
                 <= relu_mask.numel():
             kw["relu_mask"] = relu_mask
@@ -790,9 +831,10 @@ class Seq2SeqEngine:
         if self.fp8 and q8 is not None:
             self._xq[out.data_ptr()] = (q, sc)
 
-    def _ln_bwd(self, s_in, stats, prefix, dres_in, dres_out, dbranch, n_masks, seeds, bf, bias_of=None):
+    def _ln_bwd(self, s_in, stats, prefix, dres_in, dres_out, dbranch, n_masks, seeds, bf, bias_of=None, q8=None):
         """LayerNorm(+dropout+residual) backward; with `bias_of`, the column sums of
-        dbranch become grad(bias) of that Linear (its output was the LN branch)."""
+        dbranch become grad(bias) of that Linear (its output was the LN branch);
+        `q8` = (e4m3 [rows, D], scales [rows]): also the row-wise e4m3 copy of dbranch."""
         bb = self.cur
         a = K.LnArgs()
         a.dtype = K.dtype_code(self.dt)
@@ -813,6 +855,8 @@ class Seq2SeqEngine:
         a.dgamma_part, a.dbeta_part, a.n_part = part[0].data_ptr(), part[1].data_ptr(), bb.n_part
         if bias_of is not None:
             a.dbranch_part = part[2].data_ptr()
+        if q8 is not None:
+            a.q8, a.ldq8, a.q8_scale = q8[0].data_ptr(), q8[0].stride(0), q8[1].data_ptr()
         K.ln_bwd(a, stream=self.st)
         outs = [self.gb(prefix + ".weight"), self.gb(prefix + ".bias")]
         if bias_of is not None:
@@ -1139,11 +1183,14 @@ class Seq2SeqEngine:
         ws = self.cur.ws
         dy = bb.dy if dy is None else dy
         dh = bb.dh if dh is None else dh
+        w2 = pre + "ffn.linear2.weight"
+        dyq = self._fp8_dy_bufs(dy.shape[0]) if self.fp8 and self.fp8_bwd and self._fp8_wt \
+            and w2 in self._fp8_wt else None
         self._ln_bwd(s_out, st, pre + norm, bb.dres, bb.dres, dy, 1, (seed_drop, 0), bf,
-                     bias_of=pre + "ffn.linear2.bias")
-        self._dw(dy, h, pre + "ffn.linear2.weight", 1, bf, ws, bias=False)
-        fused = self._dx(dy, pre + "ffn.linear2.weight", 1, dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p,
-                         colsum=(bb.hpart, self.gb(pre + "ffn.linear1.bias"), bf), relu_mask=rmask)
+                     bias_of=pre + "ffn.linear2.bias", q8=dyq)
+        self._dw(dy, h, w2, 1, bf, ws, bias=False)
+        fused = self._dx(dy, w2, 1, dh, 0.0, epi=K.EPI_DRELU_DROP, aux=h, p_drop=self.p,
+                         colsum=(bb.hpart, self.gb(pre + "ffn.linear1.bias"), bf), relu_mask=rmask, dyq=dyq)
         self._dw(dh, x_in, pre + "ffn.linear1.weight", 1, bf, ws, bias=not fused)
         self._dx_res(dh, pre + "ffn.linear1.weight", 1)
 

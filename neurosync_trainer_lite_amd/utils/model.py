@@ -306,6 +306,7 @@ class Seq2Seq(nn.Module):
         self.compute_dtype = torch.bfloat16
         self.fp8 = False
         self.fp8_scope = "attn+enc_ffn1"
+        self.fp8_backward = False
         self.dropout_p = encoder.transformer_encoder[0].ffn.dropout.p if len(encoder.transformer_encoder) else 0.0
         self._engine = None
         self._anchor = torch.zeros((), requires_grad=True)
@@ -333,7 +334,7 @@ class Seq2Seq(nn.Module):
             if dev.type != "cuda":
                 raise RuntimeError("Seq2Seq runs only on the MI355X HIP path (device %s)" % dev)
             self._engine = Seq2SeqEngine(self, dev, self.compute_dtype)
-            self._engine.set_fp8(self.fp8, self.fp8_scope)
+            self._engine.set_fp8(self.fp8, self.fp8_scope, self.fp8_backward)
         return self._engine
 
     def set_compute_dtype(self, dtype):
@@ -344,18 +345,22 @@ class Seq2Seq(nn.Module):
             raise RuntimeError("set the compute dtype before the first forward")
         self.compute_dtype = dtype
 
-    def set_fp8(self, on=True, scope=None):
+    def set_fp8(self, on=True, scope=None, backward=None):
         """BASELINE config C5: run projections' forward GEMMs on e4m3 operands
         with row-wise scales (bf16 compute dtype only).  scope: "attn+enc_ffn1"
         (default: every attention q/k/v projection and the encoder FFN linear1,
-        within the 1e-3 forward-MSE gate) or "all" (every q/k/v and FFN GEMM)."""
+        within the 1e-3 forward-MSE gate) or "all" (every q/k/v and FFN GEMM).
+        backward=True: also every FFN linear2 input-gradient GEMM (e4m3 dy from the
+        LayerNorm backward, e4m3 W2^T)."""
         if on and self.compute_dtype != torch.bfloat16:
             raise ValueError("fp8 projections need the bf16 compute dtype (use_amp=True)")
         self.fp8 = bool(on)
         if scope is not None:
             self.fp8_scope = scope
+        if backward is not None:
+            self.fp8_backward = bool(backward)
         if self._engine is not None:
-            self._engine.set_fp8(self.fp8, self.fp8_scope)
+            self._engine.set_fp8(self.fp8, self.fp8_scope, self.fp8_backward)
 
     def forward(self, src):
         _require_gpu(src, "Seq2Seq")

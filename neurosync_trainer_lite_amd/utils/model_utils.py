@@ -33,7 +33,7 @@ def build_model(config, device):
     model = Seq2Seq(encoder, decoder, device).to(device)
     model.set_compute_dtype(torch.bfloat16 if config.get('use_amp', True) else torch.float32)
     if config.get('use_fp8', False):  # BASELINE config C5 (not a reference key): fp8 forward projections
-        model.set_fp8(True, config.get('fp8_scope', 'attn+enc_ffn1'))
+        model.set_fp8(True, config.get('fp8_scope', 'attn+enc_ffn1'), config.get('fp8_backward', False))
     if torch.device(device).type == 'cuda':
         model.engine(device)
     return model
