@@ -108,6 +108,17 @@ __global__ __launch_bounds__(NT) void autocorr_kernel(const float* y, int64_t n,
 constexpr int AC2_LG = 16, AC2_GROUPS = 12, AC2_CHUNKS = 20;
 constexpr int AC2_NT = 256;
 
+// LDS bank swizzle of the frame image (r3).  Every product read is a 16-byte
+// double pair at a 16-sample-aligned base + j: logical slot s = 8m + j/2 with
+// m = (chunk * 80 + lag group * 16 + block) / 16, so the 16 lanes of a
+// ds_read_b128 group -- distinct (chunk, lag group), i.e. distinct m -- all land on
+// slots 8m + const, two of the 16 bank slots: up to 8-way conflicts.  Slot s is
+// stored at s ^ ((s >> 3) & 7): distinct m now spread over the 16 bank slots.
+NSTL_DEV int ac2_sw(int k) {
+  const int s = k >> 1;
+  return ((s ^ ((s >> 3) & 7)) << 1) | (k & 1);
+}
+
 size_t ac2_chunk(int L) { return ((size_t)(L + AC2_CHUNKS - 1) / AC2_CHUNKS + AC2_LG - 1) / AC2_LG * AC2_LG; }
 size_t ac2_wlen(int L) { return ac2_chunk(L) * AC2_CHUNKS + AC2_LG * AC2_GROUPS + 2 * AC2_LG; }
 size_t ac2_lds(int L) {
@@ -130,10 +141,10 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
     if (i < 0) i = -i;                   // numpy 'reflect' (edge not repeated)
     if (i >= n) i = 2 * (n - 1) - i;
     const double v = (double)y[i];
-    w[k] = v;
+    w[ac2_sw(k)] = v;
     s += v;
   }
-  for (int k = L + tid; k < wlen; k += AC2_NT) w[k] = 0.0;
+  for (int k = L + tid; k < wlen; k += AC2_NT) w[ac2_sw(k)] = 0.0;
   s = wave_sum_d(s);
   if ((tid & 63) == 0) red[tid >> 6] = s;
   __syncthreads();
@@ -142,8 +153,8 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
   // float64 window multiplies them)
   const float mean_f = (float)mean;
   for (int k = tid; k < L; k += AC2_NT) {
-    const float c = (float)w[k] - mean_f;
-    w[k] = (double)c * hann[k];
+    const float c = (float)w[ac2_sw(k)] - mean_f;
+    w[ac2_sw(k)] = (double)c * hann[k];
   }
   __syncthreads();
   const bool worker = tid < AC2_GROUPS * AC2_CHUNKS;
@@ -153,25 +164,45 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
 #pragma unroll
   for (int r = 0; r < AC2_LG; ++r) acc[r] = 0.0;
   if (worker) {
+    // Block kb needs b = w[kb + l0 .. kb + l0 + 31]; its upper half is the next
+    // block's lower half, so the window slides by 16 values per block: two blocks per
+    // iteration with the halves in named registers (lo | mid | hi), 16 new b values
+    // per block instead of 32 (LDS reads per 256 FMAs: 16 instead of 24).  Same
+    // products in the same order per accumulator as the one-block form.
     const int k0 = c * chunk, k1 = min(L, k0 + chunk);
-    for (int kb = k0; kb < k1; kb += AC2_LG) {
-      double a[AC2_LG], b[2 * AC2_LG];
+    auto ld16 = [&](double (&v)[AC2_LG], int at) {  // at % 16 == 0
 #pragma unroll
       for (int j = 0; j < AC2_LG; j += 2) {
-        const double2 t = *(const double2*)(w + kb + j);
-        a[j] = t.x;
-        a[j + 1] = t.y;
+        const double2 t = *(const double2*)(w + ac2_sw(at + j));
+        v[j] = t.x;
+        v[j + 1] = t.y;
       }
-#pragma unroll
-      for (int j = 0; j < 2 * AC2_LG; j += 2) {
-        const double2 t = *(const double2*)(w + kb + l0 + j);
-        b[j] = t.x;
-        b[j + 1] = t.y;
-      }
+    };
+    auto block = [&](const double (&a)[AC2_LG], const double (&lo)[AC2_LG], const double (&hi)[AC2_LG]) {
 #pragma unroll
       for (int j = 0; j < AC2_LG; ++j)
 #pragma unroll
-        for (int r = 0; r < AC2_LG; ++r) acc[r] = fma(a[j], b[j + r], acc[r]);
+        for (int r = 0; r < AC2_LG; ++r) acc[r] = fma(a[j], j + r < AC2_LG ? lo[j + r] : hi[j + r - AC2_LG], acc[r]);
+    };
+    double lo[AC2_LG];
+    ld16(lo, k0 + l0);
+    int kb = k0;
+    for (; kb + AC2_LG < k1; kb += 2 * AC2_LG) {
+      double a[AC2_LG], mid[AC2_LG], hi[AC2_LG];
+      ld16(a, kb);
+      ld16(mid, kb + l0 + AC2_LG);
+      block(a, lo, mid);
+      ld16(a, kb + AC2_LG);
+      ld16(hi, kb + l0 + 2 * AC2_LG);
+      block(a, mid, hi);
+#pragma unroll
+      for (int j = 0; j < AC2_LG; ++j) lo[j] = hi[j];
+    }
+    if (kb < k1) {
+      double a[AC2_LG], mid[AC2_LG];
+      ld16(a, kb);
+      ld16(mid, kb + l0 + AC2_LG);
+      block(a, lo, mid);
     }
   }
   __syncthreads();  // every thread is done with w: the partials take its place
@@ -552,14 +583,22 @@ __global__ __launch_bounds__(FFT_NT) void stft_mel_kernel(const float* __restric
   for (int k = tid; k < nnz; k += FFT_NT) bw[k] = bw_g[k];
   float vmax = 0.f;
   const int nb = n / 2 + 1;
-  for (int fi = 0; fi < FFT_FPB; ++fi) {
-    const int f = blockIdx.x * FFT_FPB + fi;
-    if (f >= F) break;  // uniform over the workgroup
-    __syncthreads();    // tables loaded / the previous frame's mel reads are done
-    const int64_t start = (int64_t)f * hop - n / 2;  // center=True, zero padding
+  // Two real frames per complex FFT (r3): frame f0 in the real part, f0 + 1 in the
+  // imaginary part, Z = X0 + i X1; X0[k] = (Z[k] + conj Z[n-k]) / 2 and
+  // X1[k] = (Z[k] - conj Z[n-k]) / 2i, so |X0|^2 = ((zr + zr')^2 + (zi - zi')^2) / 4
+  // and |X1|^2 = ((zr - zr')^2 + (zi + zi')^2) / 4 with z' = Z[(n - k) % n]: half the
+  // FFT passes (and barriers) per frame.
+  for (int fi = 0; fi < FFT_FPB; fi += 2) {
+    const int f0 = blockIdx.x * FFT_FPB + fi;
+    if (f0 >= F) break;  // uniform over the workgroup
+    const bool two = f0 + 1 < F;
+    __syncthreads();    // tables loaded / the previous pair's mel reads are done
+    const int64_t start = (int64_t)f0 * hop - n / 2;  // center=True, zero padding
     for (int k = tid; k < n; k += FFT_NT) {
-      const int64_t i = start + k;
-      buf0[k] = make_float2(i >= 0 && i < n_samples ? y[i] * win[k] : 0.f, 0.f);
+      const int64_t i0 = start + k, i1 = i0 + hop;
+      const float a = i0 >= 0 && i0 < n_samples ? y[i0] * win[k] : 0.f;
+      const float b = two && i1 >= 0 && i1 < n_samples ? y[i1] * win[k] : 0.f;
+      buf0[k] = make_float2(a, b);
     }
     __syncthreads();
     float2* src = buf0;
@@ -580,20 +619,27 @@ __global__ __launch_bounds__(FFT_NT) void stft_mel_kernel(const float* __restric
       dst = t;
       __syncthreads();
     }
-    float* pw = (float*)dst;  // |X|^2 of bins 0..nb-1 into the free buffer
-    for (int b = tid; b < nb; b += FFT_NT) pw[b] = src[b].x * src[b].x + src[b].y * src[b].y;
+    float* pw = (float*)dst;  // |X0|^2 of bins 0..nb-1, then |X1|^2, into the free buffer
+    for (int b = tid; b < nb; b += FFT_NT) {
+      const float2 z = src[b], zc = src[b == 0 ? 0 : n - b];
+      const float ar = z.x + zc.x, ai = z.y - zc.y, br = z.x - zc.x, bi = z.y + zc.y;
+      pw[b] = 0.25f * (ar * ar + ai * ai);
+      pw[nb + b] = 0.25f * (br * br + bi * bi);
+    }
     __syncthreads();
-    if (tid < N_MELS) {
-      const int lo = band[3 * tid], cnt = band[3 * tid + 1], off = band[3 * tid + 2];
+    const int which = tid / N_MELS, m = tid % N_MELS;  // 2 x 128 threads: frame f0 + which, filter m
+    if (which < 2 && (which == 0 || two)) {
+      const int lo = band[3 * m], cnt = band[3 * m + 1], off = band[3 * m + 2];
+      const float* pwf = pw + which * nb;
       float acc = 0.f;
-      for (int t = 0; t < cnt; ++t) acc = fmaf(bw[off + t], pw[lo + t], acc);
-      mel[(int64_t)f * N_MELS + tid] = acc;
+      for (int t = 0; t < cnt; ++t) acc = fmaf(bw[off + t], pwf[lo + t], acc);
+      mel[(int64_t)(f0 + which) * N_MELS + m] = acc;
       vmax = fmaxf(vmax, acc);
     }
   }
   if (key != nullptr) {
     vmax = wave_max(vmax);
-    if ((tid & 63) == 0 && tid < N_MELS) atomicMax(key, __float_as_int(vmax));
+    if ((tid & 63) == 0) atomicMax(key, __float_as_int(vmax));
   }
 }
 

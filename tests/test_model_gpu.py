@@ -8,6 +8,10 @@ within 1e-3 (north-star gate; achieved ~1e-6), every parameter gradient within
 is ~0 can legitimately flip).  bf16 mode is checked against the same oracle with
 bf16-appropriate bounds.
 """
+import json
+import os
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -496,3 +500,21 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def test_short_training_validation_mse_tracks_reference():
+    """SURVEY 8(d)(ii) mechanics (tools/short_train_mse.py): the build (fp32 mode)
+    and the reference step's fp32 restatement train from the same seeded weights on
+    the same 20 batches of a learnable synthetic corpus (dropout 0), then go through
+    the drop-in validation pipeline (features -> process_audio_features ->
+    LiveLink CSV -> save_comparison_stats).  The two stay together: predictions
+    within 1e-6 MSE of each other (blendshape units / 100), the validation MSE
+    within 1 % relative, and training lowered the loss."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import short_train_mse
+    res = short_train_mse.run(steps=20, modes=("fp32",), log=lambda m: None)
+    ref, got = res["reference_fp32_cpu"], res["build_fp32"]
+    print(json.dumps(res))
+    assert got["pred_mse_vs_reference"] < 1e-6, got
+    assert abs(got["Mean Squared Error"] - ref["Mean Squared Error"]) <= 0.01 * ref["Mean Squared Error"], (got, ref)
+    assert got["last_loss"] < got["first_loss"] and ref["last_loss"] < ref["first_loss"]
