@@ -108,17 +108,6 @@ __global__ __launch_bounds__(NT) void autocorr_kernel(const float* y, int64_t n,
 constexpr int AC2_LG = 16, AC2_GROUPS = 12, AC2_CHUNKS = 20;
 constexpr int AC2_NT = 256;
 
-// LDS bank swizzle of the frame image (r3).  Every product read is a 16-byte
-// double pair at a 16-sample-aligned base + j: logical slot s = 8m + j/2 with
-// m = (chunk * 80 + lag group * 16 + block) / 16, so the 16 lanes of a
-// ds_read_b128 group -- distinct (chunk, lag group), i.e. distinct m -- all land on
-// slots 8m + const, two of the 16 bank slots: up to 8-way conflicts.  Slot s is
-// stored at s ^ ((s >> 3) & 7): distinct m now spread over the 16 bank slots.
-NSTL_DEV int ac2_sw(int k) {
-  const int s = k >> 1;
-  return ((s ^ ((s >> 3) & 7)) << 1) | (k & 1);
-}
-
 size_t ac2_chunk(int L) { return ((size_t)(L + AC2_CHUNKS - 1) / AC2_CHUNKS + AC2_LG - 1) / AC2_LG * AC2_LG; }
 size_t ac2_wlen(int L) { return ac2_chunk(L) * AC2_CHUNKS + AC2_LG * AC2_GROUPS + 2 * AC2_LG; }
 size_t ac2_lds(int L) {
@@ -141,10 +130,10 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
     if (i < 0) i = -i;                   // numpy 'reflect' (edge not repeated)
     if (i >= n) i = 2 * (n - 1) - i;
     const double v = (double)y[i];
-    w[ac2_sw(k)] = v;
+    w[k] = v;
     s += v;
   }
-  for (int k = L + tid; k < wlen; k += AC2_NT) w[ac2_sw(k)] = 0.0;
+  for (int k = L + tid; k < wlen; k += AC2_NT) w[k] = 0.0;
   s = wave_sum_d(s);
   if ((tid & 63) == 0) red[tid >> 6] = s;
   __syncthreads();
@@ -153,8 +142,8 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
   // float64 window multiplies them)
   const float mean_f = (float)mean;
   for (int k = tid; k < L; k += AC2_NT) {
-    const float c = (float)w[ac2_sw(k)] - mean_f;
-    w[ac2_sw(k)] = (double)c * hann[k];
+    const float c = (float)w[k] - mean_f;
+    w[k] = (double)c * hann[k];
   }
   __syncthreads();
   const bool worker = tid < AC2_GROUPS * AC2_CHUNKS;
@@ -173,7 +162,7 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
     auto ld16 = [&](double (&v)[AC2_LG], int at) {  // at % 16 == 0
 #pragma unroll
       for (int j = 0; j < AC2_LG; j += 2) {
-        const double2 t = *(const double2*)(w + ac2_sw(at + j));
+        const double2 t = *(const double2*)(w + at + j);
         v[j] = t.x;
         v[j + 1] = t.y;
       }
