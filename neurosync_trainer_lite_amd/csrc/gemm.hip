@@ -17,6 +17,7 @@
 #include "../../include/nstl.h"
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <string>
 
 #include "common.h"
@@ -879,14 +880,24 @@ NSTL_DEV uint32_t pack_bf16x2(float lo, float hi) {
   const bf16 a = (bf16)lo, b = (bf16)hi;
   return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
 }
-NSTL_DEV void ring_epi_bf16_direct(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, int col0, int lane) {
-  const int g = lane >> 4, c = lane & 15, odd = g & 1;
-  const float alpha = p.alpha;
-  float bias[4][4];
+NSTL_DEV void load_bias16(float (&bias)[4][4], const GemmParams& p, int col0, int lane) {
+  const int g = lane >> 4;
 #pragma unroll
   for (int b = 0; b < 4; ++b)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[b][e] = p.bias != nullptr ? p.bias[col0 + 16 * b + 4 * g + e] : 0.f;
+}
+NSTL_DEV void ring_epi_bf16_direct_b(const GemmParams& p, const f32x4 (&acc)[8][4], const float (&bias)[4][4],
+                                     int row0, int col0, int lane);
+NSTL_DEV void ring_epi_bf16_direct(const GemmParams& p, const f32x4 (&acc)[8][4], int row0, int col0, int lane) {
+  float bias[4][4];
+  load_bias16(bias, p, col0, lane);
+  ring_epi_bf16_direct_b(p, acc, bias, row0, col0, lane);
+}
+NSTL_DEV void ring_epi_bf16_direct_b(const GemmParams& p, const f32x4 (&acc)[8][4], const float (&bias)[4][4],
+                                     int row0, int col0, int lane) {
+  const int g = lane >> 4, c = lane & 15, odd = g & 1;
+  const float alpha = p.alpha;
   bf16* const cbase = (bf16*)p.C + (int64_t)(row0 + c) * p.ldc + col0;
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
@@ -1136,6 +1147,131 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm256p_kernel(GemmParams p, int r
     if (sg > 0) __syncthreads();  // the previous tile's epilogue scratch is free
     ring_tile<AK, BKM, EM>(p, xcd_remap(w + j * G, nt), kb, ke, smem, flags, part);
   }
+}
+
+// Persistent, cross-tile pipelined form (r3, NSTL_GEMM_PQ=1; bf16 output without
+// beta on full tiles, the register-direct epilogue).  One workgroup per CU runs
+// its tiles (w, w + G, ...: the one-shot grid's XCD-aware order) as ONE
+// continuous stream of K-steps: the last three K-steps of tile i stage tile
+// i + 1's first three, so the ring never drains and there is no prologue or
+// workgroup dispatch between tiles.  The epilogue writes straight from the
+// accumulators (no LDS, no barrier), so each wave group does it between its own
+// M(last) and R(first) of the next tile; its 16 stores per wave sit in vmcnt
+// between the next tile's stages 2 and 3, and the first two K-steps of the next
+// tile count them (vmcnt(24) instead of 8): the stores retire under those
+// K-steps instead of holding the next loads.  The first K-step of a tile starts
+// its accumulators from the MFMA's zero operand.
+constexpr int PQ_ST = 16;  // global stores per wave of ring_epi_bf16_direct_b (checked in the ISA)
+
+NSTL_DEV void pq_tile(const GemmParams& p, int id, int& m0, int& n0) {
+  const int nt_n = (p.N + BIG - 1) / BIG, nt_m = (p.M + BIG - 1) / BIG;
+  constexpr int GROUP_M = 4;
+  const int per_group = GROUP_M * nt_n;
+  const int first_m = (id / per_group) * GROUP_M;
+  const int gm = min(nt_m - first_m, GROUP_M);
+  const int in_g = id % per_group;
+  m0 = (first_m + in_g % gm) * BIG;
+  n0 = (in_g / gm) * BIG;
+}
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(BIG_NT, 1) void gemm256q_kernel(GemmParams p, int rounds) {
+  __shared__ __attribute__((aligned(16))) char smem[R_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int G = gridDim.x, w = blockIdx.x;
+  const int nt = rounds * G;
+  const int nk = p.K / R_BK;
+  const uint32_t smem_u32 = lds_u32(smem);
+  int m0, n0, nm0 = 0, nn0 = 0;
+  pq_tile(p, xcd_remap(w, nt), m0, n0);
+  RingSrc rs = ring_src<AK, BKM>(p, m0, n0, wave, lane), rn = rs;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) ring_stage(smem + s * R_SLOT, rs, s * R_BK, wave);
+  NSTL_VMCNT(0);  // all three landed: the head steps' vmcnt(24) then holds for tile 0 too
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // the stagger (kept across tiles)
+  int slot = 0;
+  // stage: 0 none, 1 this tile's K-step kt + 3, 2 the next tile's K-step kt + 3 - nk.
+  // W: the wait count (a compile-time constant at each call site: a runtime
+  // choice between s_waitcnt immediates costs taken branches every K-step).
+  auto step = [&](int kt, int stage, auto W) {
+    constexpr int wait = decltype(W)::value;
+    const uint32_t Ai = smem_u32 + slot * R_SLOT;
+    const uint32_t Bi = Ai + R_SLOT / 2;
+    bf16x8 fb[4], fa[8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (BKM) asm_frag_k64(fb[t], Bi, wn * 64 + t * 16 + (lane & 15), 8 * (lane >> 4));
+      else asm_frag_mn512(fb[t], Bi, wn * 64 + t * 16, lane);
+    }
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      if (AK) asm_frag_k64(fa[a], Ai, wm * 128 + a * 16 + (lane & 15), 8 * (lane >> 4));
+      else asm_frag_mn512(fa[a], Ai, wm * 128 + a * 16, lane);
+    }
+    if (stage) {
+      int s3 = slot + 3;
+      if (s3 >= R_STAGES) s3 -= R_STAGES;
+      if (stage == 1) ring_stage(smem + s3 * R_SLOT, rs, (kt + 3) * R_BK, wave);
+      else ring_stage(smem + s3 * R_SLOT, rn, (kt + 3 - nk) * R_BK, wave);
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) mma16(acc[a][b], fb[b], fa[a]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait) : "memory");
+    __builtin_amdgcn_s_barrier();
+    slot = slot + 1 == R_STAGES ? 0 : slot + 1;
+  };
+  using W8 = std::integral_constant<int, 8>;
+  using W24 = std::integral_constant<int, PQ_ST + 8>;
+  // three loops per tile (three step call sites, as the one-shot kernel's four:
+  // more sites gave the accumulators different registers per site and spilled)
+  for (int i = 0; i < rounds; ++i) {
+    const bool last = i + 1 == rounds;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // K-steps 0, 1: the previous tile's 16 stores may still fly (counted: S(k+1)
+    // is retired with S(k+2), the stores and S(k+3) younger)
+    for (int kt = 0; kt < 2; ++kt) step(kt, 1, W24());
+    for (int kt = 2; kt < nk - 3; ++kt) step(kt, 1, W8());
+    // the next tile's sources (live for three K-steps); the last tile stages its
+    // own first three K-steps again into slots nobody reads (no drain variant of
+    // the step, so the accumulators keep one register assignment), retired by
+    // the vmcnt(0) before the workgroup ends
+    pq_tile(p, xcd_remap(w + (last ? i : i + 1) * G, nt), nm0, nn0);
+    rn = ring_src<AK, BKM>(p, nm0, nn0, wave, lane);
+    for (int kt = nk - 3; kt < nk; ++kt) step(kt, 2, W8());
+    // the epilogue from registers: the bias loads, then every older operation
+    // (the next tile's three staged K-steps) and the bias retire, then the 16
+    // stores go out behind them (no bias: no loads, and no wait at all)
+    if (p.bias != nullptr) {
+      float bs[4][4];
+      load_bias16(bs, p, n0 + wn * 64, lane);
+      NSTL_VMCNT(0);
+      ring_epi_bf16_direct_b(p, acc, bs, m0 + wm * 128, n0 + wn * 64, lane);
+    } else {  // a separate path: a merge with the loads above makes the compiler wait vmcnt(0)
+      const float bs[4][4] = {};
+      ring_epi_bf16_direct_b(p, acc, bs, m0 + wm * 128, n0 + wn * 64, lane);
+    }
+    m0 = nm0;
+    n0 = nn0;
+    rs = rn;
+  }
+  NSTL_VMCNT(0);  // the last tile's re-staged K-steps land before the workgroup ends
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger
 }
 
 // Grouped launch: independent problems of one kind back to back in one grid
@@ -1655,6 +1791,16 @@ bool getenv_persist() {
   return v != 0;
 }
 
+// NSTL_GEMM_PQ=1: the persistent cross-tile pipelined kernel (gemm256q_kernel)
+// (2: also single-round problems -- a diagnostic of the per-K-step cost)
+int getenv_pq() {
+  static const int v = [] {
+    const char* e = getenv("NSTL_GEMM_PQ");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // CUs of the current device (the persistent grid: one workgroup per CU)
 int device_cus() {
   static int cus[64] = {0};
@@ -1732,6 +1878,22 @@ int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t s
         if (a->b_kmajor) launch_h_em<true>(em, grid, st, p, rounds, parts);
         else launch_h_em<false>(em, grid, st, p, rounds, parts);
         NSTL_LAUNCH_CHECK("nstl_gemm (128x256 two per CU)");
+        nstl::count(NSTL_K_GEMM_RING);
+        nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt);
+        return 0;
+      }
+    }
+    // NSTL_GEMM_PQ=1: multi-round bf16 problems with the plain (bias) epilogue on
+    // full tiles run on the persistent cross-tile pipelined kernel
+    {
+      const int G = device_cus();
+      if (getenv_pq() && splits == 1 && em == EM_BF16 && p.direct_epi && a->M % BIG == 0 && a->N % BIG == 0 &&
+          G > 0 && nt % G == 0 && nt / G >= (getenv_pq() == 2 ? 1 : 2) && a->K % R_BK == 0 && a->K / R_BK >= 6 &&
+          a->a_kmajor && p.debug_skip_epilogue == 0) {
+        dim3 g(G), b(BIG_NT);
+        if (a->a_kmajor && a->b_kmajor) hipLaunchKernelGGL((gemm256q_kernel<true, true>), g, b, 0, st, p, nt / G);
+        else hipLaunchKernelGGL((gemm256q_kernel<true, false>), g, b, 0, st, p, nt / G);
+        NSTL_LAUNCH_CHECK("nstl_gemm (256 cross-tile persistent)");
         nstl::count(NSTL_K_GEMM_RING);
         nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt);
         return 0;

@@ -976,8 +976,9 @@ def _cus():
 # the persistent kernels are opt-in (NSTL_GEMM_PERSIST=1: the 256^2 XCD-phased
 # grid; NSTL_GEMM_H=2: the two-per-CU 128 x 256 grid; read once per process):
 # tools/run_persist.sh and tools/run_gemm_h.sh run these tests with them on
-persistent = pytest.mark.skipif(os.environ.get("NSTL_GEMM_PERSIST") != "1" and os.environ.get("NSTL_GEMM_H") != "2",
-                                reason="persistent GEMM off (NSTL_GEMM_PERSIST=1 / NSTL_GEMM_H=2 enable it)")
+persistent = pytest.mark.skipif(os.environ.get("NSTL_GEMM_PERSIST") != "1" and os.environ.get("NSTL_GEMM_H") != "2"
+                                and os.environ.get("NSTL_GEMM_PQ") != "1",
+                                reason="persistent GEMM off (NSTL_GEMM_PERSIST=1 / NSTL_GEMM_H=2 / NSTL_GEMM_PQ=1 enable it)")
 
 
 def _halves(run, M):
@@ -1036,6 +1037,39 @@ def test_gemm256_persistent_forward_matches_one_shot(epi):
     y = f64(X) @ f64(W).T + f64(b)
     if epi == "bias":
         check(full, y, 1e-2, "persistent fwd")
+
+
+@persistent
+@pytest.mark.parametrize("layout", ["fwd", "dx"])
+def test_gemm256_persistent_four_rounds(layout):
+    """Four rounds of 256-tiles per workgroup (the FFN shapes' depth): every
+    quarter of the persistent result equals the one-shot kernel's result for
+    those rows (one round each), and the whole matches the f64 product to bf16."""
+    dt, N, Kd = torch.bfloat16, 2048, 1024
+    M = 2 * _persist_rows()
+    b = rnd(N, seed=412)
+    if layout == "fwd":
+        X, W = rnd(M, Kd, dtype=dt, seed=410), rnd(N, Kd, dtype=dt, scale=0.05, seed=411)
+        kw = dict(epilogue=K.EPI_BIAS, bias=b)
+        ref = f64(X) @ f64(W).T + f64(b)
+    else:
+        X, W = rnd(M, Kd, dtype=dt, seed=413), rnd(Kd, N, dtype=dt, scale=0.05, seed=414)
+        kw = dict(a_kmajor=True, b_kmajor=False)
+        ref = f64(X) @ f64(W)
+
+    def run(i0, rows):
+        C = torch.empty(rows, N, dtype=dt, device=DEV)
+        K.gemm(X[i0:i0 + rows], W, C, rows, N, Kd, **kw)
+        return C
+
+    full = run(0, M)
+    q = M // 4
+    parts = [run(i * q, q) for i in range(4)]
+    torch.cuda.synchronize()
+    for i, part in enumerate(parts):
+        _same(full[i * q:(i + 1) * q], part, "quarter %d" % i)
+    err = (f64(full) - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
 
 
 @persistent
