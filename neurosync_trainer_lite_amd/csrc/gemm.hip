@@ -2074,11 +2074,20 @@ bool big_ok(const nstl_gemm_args* a) {
 
 }  // namespace
 
+namespace nstl {
+int lt_gemm(const nstl_gemm_args* a, hipStream_t st, int* handled);  // lt.hip
+}
+
 extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   GemmParams p;
   if (int rc = make_params(a, p)) return rc;
   NSTL_CHECK_ARG(!a->sq_part, "nstl_gemm: sq_part is produced by nstl_gemm_grouped only");
   if (a->dtype == NSTL_FP8) return gemm_f8(a, p, (hipStream_t)stream);
+  {  // plain bf16 GEMMs (no fused epilogue beyond a bias) on hipBLASLt
+    int handled = 0;
+    if (int rc = nstl::lt_gemm(a, (hipStream_t)stream, &handled)) return rc;
+    if (handled) return 0;
+  }
   const int esz = a->dtype == NSTL_F32 ? 4 : 2;
 
   // the 256x256 LDS-DMA kernel: bf16, K a multiple of its 64-deep K tile, and at

@@ -135,6 +135,44 @@ def test_gemm_relu_dropout_and_backward(dt):
     check(dH, refd, 1e-5, "drelu")
 
 
+@pytest.mark.parametrize("case", ["fwd_bias", "dx_bf16", "dx_f32_beta1", "fwd_f32"])
+def test_gemm_plain_on_hipblaslt(case):
+    """Plain bf16-output GEMMs (no fused epilogue beyond a bias, beta 0) run on
+    hipBLASLt through nstl_gemm (NSTL_GEMM_LT, default on): the launch counter sees
+    them, and the results match the f64 product in both layouts nstl_gemm maps onto
+    the library's column-major convention (K-major B with bias; MN-major B).  f32
+    output (beta 0 or 1) stays on the ring kernel (the library measured slower)."""
+    if os.environ.get("NSTL_GEMM_LT") == "0":
+        pytest.skip("hipBLASLt path off")
+    dt, M, N, Kd = torch.bfloat16, 4096, 1024 + 256, 1024 + 64
+    b = rnd(N, seed=503)
+    K.kernel_counts_reset()
+    if case in ("fwd_bias", "fwd_f32"):
+        X, W = rnd(M, Kd, dtype=dt, seed=501), rnd(N, Kd, dtype=dt, scale=0.05, seed=502)
+        C = torch.empty(M, N, dtype=dt if case == "fwd_bias" else torch.float32, device=DEV)
+        kw = dict(epilogue=K.EPI_BIAS, bias=b) if case == "fwd_bias" else {}
+        K.gemm(X, W, C, M, N, Kd, **kw)
+        ref = f64(X) @ f64(W).T + (f64(b) if case == "fwd_bias" else 0)
+    else:
+        dY, W = rnd(M, Kd, dtype=dt, seed=504), rnd(Kd, N, dtype=dt, scale=0.05, seed=505)
+        if case == "dx_bf16":
+            C = torch.empty(M, N, dtype=dt, device=DEV)
+            K.gemm(dY, W, C, M, N, Kd, a_kmajor=True, b_kmajor=False)
+            ref = f64(dY) @ f64(W)
+        else:
+            C0 = rnd(M, N, seed=506)
+            C = C0.clone()
+            K.gemm(dY, W, C, M, N, Kd, a_kmajor=True, b_kmajor=False, beta=1.0)
+            ref = f64(C0) + f64(dY) @ f64(W)
+    torch.cuda.synchronize()
+    c = K.kernel_counts()
+    if C.dtype == dt:
+        assert c["gemm_lt"] == 1 and c["gemm_ring"] == 0, c
+    else:
+        assert c["gemm_lt"] == 0 and c["gemm_ring"] == 1, c
+    check(C, ref, 1e-2 if C.dtype == dt else 1e-4, "hipBLASLt " + case)
+
+
 def test_gemm_rejects_bad_args():
     A = torch.zeros(16, 12, device=DEV)
     C = torch.zeros(16, 16, device=DEV)

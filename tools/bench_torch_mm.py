@@ -20,6 +20,7 @@ def t(fn, reps=20):
 
 
 for name, m, n, k in (("fwd out", M, D, D), ("fwd ffn2", M, D, F), ("fwd ffn1", M, F, D), ("fwd qkv", M, 3 * D, D),
+                      ("dX ffn1", M, D, F), ("dX qkv", M, D, 3 * D), ("dX ffn2", M, F, D),
                       ("dW ffn1", F, D, M), ("dW out", D, D, M), ("big 8192^3", 8192, 8192, 8192)):
     a = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
     b = torch.randn(k, n, device=dev, dtype=torch.bfloat16)
