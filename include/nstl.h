@@ -267,6 +267,22 @@ int nstl_clip_coef(const float* partial, int n_partial, float max_norm, float* c
 int nstl_copy2d(int src_dtype, const void* src, int64_t src_ld, int dst_dtype, void* dst, int64_t dst_ld,
                 int rows, int cols, int dst_cols, const float* scale, void* stream);
 
+/* Batched bf16 transpose: job k writes y[j][i] = x[i][j] for x [rows][ldx] ->
+ * y [cols][ldy].  The input-gradient GEMMs' weight operand (dX = dY W contracts
+ * over W's rows): the transposed bf16 copy W^T [in][out] is K-major, the layout
+ * the GEMM kernels read fastest, refreshed once per backward from the bf16
+ * shadow.  rows % 64 == 0, cols % 64 == 0, ldx / ldy multiples of 8, 16-byte
+ * aligned; up to NSTL_TRANSPOSE_BATCH_MAX jobs per launch.  Replaces nothing in
+ * the reference (a layout choice; autograd's mm backward of utils/model.py's
+ * Linears reads W in place). */
+#define NSTL_TRANSPOSE_BATCH_MAX 64
+typedef struct nstl_transpose_job {
+  const void* x; int64_t ldx;
+  void* y; int64_t ldy;
+  int rows, cols;
+} nstl_transpose_job;
+int nstl_transpose_bf16(const nstl_transpose_job* jobs, int n, void* stream);
+
 /* dtype conversion (f32 <-> bf16), n elements. */
 int nstl_cast(int src_dtype, const void* src, int dst_dtype, void* dst, int64_t n, void* stream);
 

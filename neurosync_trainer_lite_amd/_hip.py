@@ -48,6 +48,13 @@ class Fp8Job(ctypes.Structure):
 FP8_BATCH_MAX = 64
 
 
+class TransposeJob(ctypes.Structure):
+    _fields_ = [("x", _vp), ("ldx", _i64), ("y", _vp), ("ldy", _i64), ("rows", _i32), ("cols", _i32)]
+
+
+TRANSPOSE_BATCH_MAX = 64
+
+
 class AttnArgs(ctypes.Structure):
     _fields_ = [
         ("dtype", _i32), ("B", _i32), ("T", _i32), ("H", _i32), ("dh", _i32),
@@ -111,7 +118,7 @@ EXPORTS = [
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_clip_coef", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
     "nstl_features", "nstl_stft_mel", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
     "nstl_version", "nstl_fp8_quant_rows", "nstl_fp8_quant_cols", "nstl_kernel_counts", "nstl_kernel_counts_reset",
-    "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs",
+    "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs", "nstl_transpose_bf16",
 ]
 
 # nstl_kernel_counts order (NSTL_K_* in include/nstl.h)
@@ -136,6 +143,7 @@ def lib():
         L.nstl_gemm_grouped.argtypes = [P(GemmArgs), _i32, _vp]
         L.nstl_fp8_quant_rows.argtypes = [_i32, P(Fp8Job), _i32, _vp]
         L.nstl_fp8_quant_cols.argtypes = [_i32, P(Fp8Job), _i32, _vp]
+        L.nstl_transpose_bf16.argtypes = [P(TransposeJob), _i32, _vp]
         L.nstl_gemm_colsum_rows.argtypes = [P(GemmArgs)]
         L.nstl_gemm_colsum_rows.restype = _i32
         L.nstl_gemm_relu_mask_words.argtypes = [P(GemmArgs)]
@@ -324,6 +332,20 @@ def fp8_quant_cols(jobs, stream=None):
     (x, rows, cols, q, scale) with x [rows, >= cols], q float8_e4m3fn [cols, >= rows]
     = quant_rows(x^T), scale f32 [cols]."""
     _fp8_jobs(lib().nstl_fp8_quant_cols, jobs, stream, "nstl_fp8_quant_cols")
+
+
+def transpose_bf16(jobs, stream=None):
+    """Batched bf16 transpose (nstl_transpose_bf16): jobs (x, y) with x bf16
+    [rows, cols] (row stride >= cols) and y bf16 [cols, rows] (row stride >= rows)."""
+    for lo in range(0, len(jobs), TRANSPOSE_BATCH_MAX):
+        chunk = jobs[lo:lo + TRANSPOSE_BATCH_MAX]
+        arr = (TransposeJob * len(chunk))()
+        for i, (x, y) in enumerate(chunk):
+            if x.dtype != torch.bfloat16 or y.dtype != torch.bfloat16 or y.shape != (x.shape[1], x.shape[0]):
+                raise TypeError("nstl_transpose_bf16: x bf16 [r, c] and y bf16 [c, r]")
+            arr[i] = TransposeJob(x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), x.shape[0], x.shape[1])
+        check(lib().nstl_transpose_bf16(arr, len(chunk), stream if stream is not None else stream_of()),
+              "nstl_transpose_bf16")
 
 
 def attn_args(dtype, B, T, H, q, q_ld, k, k_ld, v, v_ld, o, o_ld, lse, p_drop, seed, dh=64):

@@ -344,6 +344,42 @@ __global__ void rope_kernel(const TI* in, int64_t in_ld, TO* out, int64_t out_ld
   }
 }
 
+// Batched bf16 transpose, one 64 x 64 tile per workgroup: 16-byte row loads into
+// a padded LDS tile, 16-byte row stores of the transposed tile (both sides
+// coalesced; HBM-bound at 4 B per element).
+struct TpBatch {
+  nstl_transpose_job j[NSTL_TRANSPOSE_BATCH_MAX];
+};
+__global__ __launch_bounds__(NT) void transpose_bf16_kernel(TpBatch b) {
+  const nstl_transpose_job& J = b.j[blockIdx.z];
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  if (c0 >= J.cols || r0 >= J.rows) return;
+  __shared__ uint32_t tile[64][33];  // 64 source rows of 64 bf16 (pairs), one dword of padding
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = h * 32 + (t >> 3), c = (t & 7) * 8;
+    const uint4 v = *(const uint4*)((const bf16*)J.x + (int64_t)(r0 + r) * J.ldx + c0 + c);
+    tile[r][c / 2] = v.x;
+    tile[r][c / 2 + 1] = v.y;
+    tile[r][c / 2 + 2] = v.z;
+    tile[r][c / 2 + 3] = v.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    // output row c0 + oc (a source column), 8 source rows ob .. ob + 7
+    const int q = h * NT + t, oc = q >> 3, ob = (q & 7) * 8;
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t lo = tile[ob + 2 * e][oc >> 1], hi = tile[ob + 2 * e + 1][oc >> 1];
+      o[e] = (oc & 1) ? ((lo >> 16) | (hi & 0xFFFF0000u)) : ((lo & 0xFFFFu) | (hi << 16));
+    }
+    *(uint4*)((bf16*)J.y + (int64_t)(c0 + oc) * J.ldy + r0 + ob) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 int grid_for(int64_t n, int per_thread = 1) {
   int64_t g = (n + (int64_t)NT * per_thread - 1) / ((int64_t)NT * per_thread);
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, 8192));
@@ -431,6 +467,30 @@ extern "C" int nstl_cast(int src_dtype, const void* src, int dst_dtype, void* ds
   hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n, 4)), dim3(NT), 0, (hipStream_t)stream,
                      src_dtype == NSTL_BF16, src, dst_dtype == NSTL_BF16, dst, n);
   NSTL_LAUNCH_CHECK("nstl_cast");
+  return 0;
+}
+
+extern "C" int nstl_transpose_bf16(const nstl_transpose_job* jobs, int n, void* stream) {
+  NSTL_CHECK_ARG(jobs != nullptr && n >= 1 && n <= NSTL_TRANSPOSE_BATCH_MAX, "nstl_transpose_bf16: 1..%d jobs (got %d)",
+                 NSTL_TRANSPOSE_BATCH_MAX, n);
+  TpBatch b;
+  int wide = 0, tall = 0;
+  for (int k = 0; k < n; ++k) {
+    const nstl_transpose_job& J = jobs[k];
+    NSTL_CHECK_ARG(J.x && J.y, "nstl_transpose_bf16: job %d: null pointer", k);
+    NSTL_CHECK_ARG(J.rows > 0 && J.cols > 0 && J.rows % 64 == 0 && J.cols % 64 == 0,
+                   "nstl_transpose_bf16: job %d: rows and cols must be positive multiples of 64 (got %d x %d)", k,
+                   J.rows, J.cols);
+    NSTL_CHECK_ARG(J.ldx >= J.cols && J.ldy >= J.rows && J.ldx % 8 == 0 && J.ldy % 8 == 0 &&
+                       ((uintptr_t)J.x | (uintptr_t)J.y) % 16 == 0,
+                   "nstl_transpose_bf16: job %d: leading dimensions (multiples of 8, >= the row length) and "
+                   "16-byte aligned pointers", k);
+    b.j[k] = J;
+    wide = std::max(wide, J.cols);
+    tall = std::max(tall, J.rows);
+  }
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(wide / 64, tall / 64, n), dim3(NT), 0, (hipStream_t)stream, b);
+  NSTL_LAUNCH_CHECK("nstl_transpose_bf16");
   return 0;
 }
 

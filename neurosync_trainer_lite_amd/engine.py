@@ -241,6 +241,14 @@ class Seq2SeqEngine:
         self.fp8_bwd = False
         self._fp8_wt = None        # weight name -> (e4m3 W^T [in, out], f32 scales [in])
         self._fp8_dy = {}          # M -> (e4m3 [M, D], scales [M])
+        # NSTL_WT=1: the input-gradient GEMMs (dX = dY W) read a transposed bf16 copy
+        # W^T [in, out] (K-major, the layout both the ring kernel and hipBLASLt run
+        # fastest), refreshed by one batched transpose at the start of every backward,
+        # instead of W in place as an MN-major operand.  Off: the GEMMs gain what the
+        # transpose costs (587.3k vs 587.4k frames/s same-box, profiles/r3_wt_ab.txt)
+        self.wt_on = os.environ.get("NSTL_WT", "0") == "1"
+        self._wt = None            # (weight name, rows) -> bf16 W^T [in, rows * out]
+        self._wt_ok = False        # _wt holds this backward's weights
         # NSTL_FUSED_NORM=0: the clip norm re-reads the whole gradient arena
         # (nstl_sumsq) instead of taking the grouped weight-gradient GEMMs' per-tile
         # sums of squares (their epilogue, nstl_gemm_args.sq_part) plus nstl_sumsq
@@ -589,6 +597,48 @@ class Seq2SeqEngine:
         return ["%s.%d.ffn.linear2.weight" % (st, l) for st in ("encoder.transformer_encoder",
                                                                "decoder.transformer_decoder") for l in range(self.L)]
 
+    def wt_groups(self):
+        """(weight name, rows) of the input-gradient GEMMs that read the transposed
+        bf16 copy (every layer projection; the FFN linear2 not when its dX runs in
+        fp8), plus ("kv", 0): the stacked cross-attention k|v slab of the
+        concatenated memory-gradient GEMM."""
+        out = []
+        fp8_w2 = self.fp8 and self.fp8_bwd
+        for l in range(self.L):
+            for pre, names in (("encoder.transformer_encoder.%d." % l, ("self_attn",)),
+                               ("decoder.transformer_decoder.%d." % l, ("self_attn", "multihead_attn"))):
+                for a in names:
+                    if a == "self_attn":
+                        out.append((pre + a + ".q_linear.weight", 3))
+                    else:
+                        out.append((pre + a + ".q_linear.weight", 1))
+                        if not self.dmem_concat:
+                            out.append((pre + a + ".k_linear.weight", 2))
+                    out.append((pre + a + ".out_linear.weight", 1))
+                out.append((pre + "ffn.linear1.weight", 1))
+                if not fp8_w2:
+                    out.append((pre + "ffn.linear2.weight", 1))
+        if self.dmem_concat:
+            out.append(("kv", 0))
+        return out
+
+    def _refresh_wt(self):
+        """W^T copies of this backward's weights (one batched transpose launch)."""
+        self._wt_ok = False
+        if not (self.wt_on and self.dt == torch.bfloat16):
+            return
+        groups = self.wt_groups()
+        if self._wt is None or set(self._wt) != set(groups):
+            src = {g: (self._kv_weights() if g[0] == "kv" else self.w(*g)) for g in groups}
+            if any(x.shape[0] % 64 or x.shape[1] % 64 for x in src.values()):
+                self.wt_on = False
+                return
+            self._wt = {g: torch.empty(x.shape[1], x.shape[0], dtype=self.dt, device=self.device)
+                        for g, x in src.items()}
+        K.transpose_bf16([(self._kv_weights() if g[0] == "kv" else self.w(*g), y) for g, y in self._wt.items()],
+                         stream=self.st)
+        self._wt_ok = True
+
     def set_fp8(self, on, scope=None, backward=None):
         if on and self.dt != torch.bfloat16:
             raise ValueError("fp8 projections need the bf16 compute dtype (use_amp=True)")
@@ -786,6 +836,9 @@ class Seq2SeqEngine:
             qt, st = self._fp8_wt[wname]
             dy, W = dyq[0], qt
             kw.update(b_kmajor=True, a_scale=dyq[1], b_scale=st)
+        elif self._wt_ok and (wname, rows) in self._wt:
+            W = self._wt[(wname, rows)]
+            kw["b_kmajor"] = True
         if relu_mask is not None and 0 < K.gemm_relu_mask_words(dy, W, out, dy.shape[0], k, n, **kw) \
                 <= relu_mask.numel():
             kw["relu_mask"] = relu_mask
@@ -1069,6 +1122,7 @@ class Seq2SeqEngine:
         self.p, self.base_seed = sv["p"], sv["seed"]
         self._dadd_pending = False
         self._red = None
+        self._refresh_wt()
         bf = 0.0 if self.grads_fresh else 1.0
         self.sq_state = None
         self._sq_ok = self.fused_norm_on and self.dt == torch.bfloat16 and self.grad_reducer is None
@@ -1101,9 +1155,14 @@ class Seq2SeqEngine:
             # dmem = sum_l dkv_l W_kv_l = [dkv_0 | ... | dkv_{L-1}] [W_kv_0; ...; W_kv_{L-1}]:
             # one single-round GEMM with K = L * 2D (L accumulating K = 2D GEMMs each
             # read and wrote the f32 dmem, 128 MB per launch at the 228M shape)
-            W = self._kv_weights()
-            K.gemm(bb.dkv_all, W, bb.dmem, M, D, W.shape[0], a_kmajor=True, b_kmajor=False, beta=0.0,
-                   stream=self.st)
+            if self._wt_ok and ("kv", 0) in self._wt:
+                Wt = self._wt[("kv", 0)]
+                K.gemm(bb.dkv_all, Wt, bb.dmem, M, D, Wt.shape[1], a_kmajor=True, b_kmajor=True, beta=0.0,
+                       stream=self.st)
+            else:
+                W = self._kv_weights()
+                K.gemm(bb.dkv_all, W, bb.dmem, M, D, W.shape[0], a_kmajor=True, b_kmajor=False, beta=0.0,
+                       stream=self.st)
         # decoder input x = GPE(mem): dmem += GPE^T(dres)
         cs, sn = self.rope(T, D)
         K.rope(dres, D, bb.dmem, D, M, D, cs, sn, T, D, inverse=True, accumulate=True, stream=self.st)

@@ -1186,3 +1186,29 @@ def test_gemm256_persistent_dw_matches_one_shot():
     _same(full[:N // 2], lo, "dW lo", f32=True)
     _same(full[N // 2:], hi, "dW hi", f32=True)
     check(full, f64(dY).T @ f64(X), 1e-5, "persistent dW")
+
+
+def test_transpose_bf16_batched_bit_exact():
+    """nstl_transpose_bf16: several jobs of different shapes in one launch, padded
+    leading dimensions on both sides, every element moved exactly."""
+    shapes = [(64, 64), (1024, 3072), (4096, 1024), (192, 640)]
+    xs, ys = [], []
+    for i, (r, c) in enumerate(shapes):
+        full = rnd(r, c + 8 * (i % 2), dtype=torch.bfloat16, seed=40 + i).to(DEV)
+        x = full[:, :c]
+        ybuf = torch.full((c, r + 16 * (i % 2)), 7.0, dtype=torch.bfloat16, device=DEV)
+        xs.append(x)
+        ys.append(ybuf)
+    K.transpose_bf16([(x, y[:, :x.shape[0]]) for x, y in zip(xs, ys)])
+    torch.cuda.synchronize()
+    for x, y in zip(xs, ys):
+        r = x.shape[0]
+        assert torch.equal(y[:, :r].cpu(), x.cpu().t()), x.shape
+        assert (y[:, r:] == 7.0).all(), "wrote past rows"
+
+
+def test_transpose_bf16_rejects_bad_shapes():
+    x = torch.zeros(100, 128, dtype=torch.bfloat16, device=DEV)
+    y = torch.empty(128, 100, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match="multiples of 64"):
+        K.transpose_bf16([(x, y)])

@@ -255,6 +255,33 @@ def test_bf16_concatenated_memory_gradient_matches_per_layer(monkeypatch):
     assert len(enc) > 0 and all(grads[0][k].abs().sum() > 0 for k in enc)
 
 
+def test_bf16_transposed_weight_copies_match_in_place(monkeypatch):
+    """Input-gradient GEMMs on the transposed bf16 weight copies (NSTL_WT=1, the
+    default: W^T refreshed by one batched transpose per backward, K-major operand)
+    equal the in-place MN-major reads of W up to f32 summation order; a second
+    step sees the optimizer's new weights in the copies."""
+    grads = []
+    for wt in ("1", "0"):
+        monkeypatch.setenv("NSTL_WT", wt)
+        cfg, model, crit, opt, params = make(256, 4, 2, 11, amp=True, dropout=0.1)
+        torch.manual_seed(5)
+        g = torch.Generator().manual_seed(6)
+        model.train()
+        for step in range(2):
+            src = torch.randn(4, 128, 256, generator=g).to(DEV)
+            trg = (torch.randn(4, 128, 61, generator=g) * 20).to(DEV)
+            opt.zero_grad()
+            crit(model(src), trg).backward()
+            if step == 0:
+                opt.step()
+        torch.cuda.synchronize()
+        eng = model.engine(torch.device(DEV))
+        assert eng.wt_on == (wt == "1") and eng._wt_ok == (wt == "1")
+        grads.append({k: p.grad.detach().double().cpu().clone() for k, p in model.named_parameters()})
+    worst = max(rel(grads[0][k], grads[1][k]) for k in grads[0])
+    assert worst < 5e-3, worst
+
+
 def test_bf16_batched_reductions_match_per_call(monkeypatch):
     """LayerNorm and bias-gradient partials reduced in one batched launch per backward
     layer (default) equal the per-call reductions: LayerNorm gamma/beta bit-exact
