@@ -644,6 +644,10 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
   const int rhalf = p.rope_dim >> 1;
   // cos/sin of 8 columns = 4 consecutive table entries (16 B) when rope_dim % 8 == 0
   const bool rope_vec = (p.rope_dim & 7) == 0;
+  const int rope_pr = EM == EM_ROPE && rope_col ? (j % p.rope_dim) >> 1 : 0;  // fixed per lane
+  // a pass's rows ib + it * RPI span < 64 rows: with rope_T >= 64 their positions
+  // follow from the pass's first by one conditional wrap (no integer modulo per row)
+  const bool rope_tinc = EM == EM_ROPE && p.rope_T >= 64;
   const int r0 = lane / LPR;
   // dReLU epilogue: column sums of the stored dh (the FFN1 bias gradient)
   const bool csum_on = EM == EM_DRELU && p.colsum_part != nullptr;
@@ -659,6 +663,7 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
    const int ib = row0 + half * 64 + r0;
+   const int tb = EM == EM_ROPE && rope_col ? ib % p.rope_T : 0;
    const int64_t midx = relu_mask_index(p.N, (row0 + half * 64) >> 6, r0, j);
    // dReLU from the forward's mask word (8 B per lane and pass instead of 8 x 16 B of h)
    uint64_t mword = 0;
@@ -677,11 +682,16 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
       if (EM == EM_ROPE) {
         f32x4 cs = {1.f, 1.f, 1.f, 1.f}, sn = {0.f, 0.f, 0.f, 0.f};
         if (ok && rope_col) {
-          const int t = i % p.rope_T;
+          int t;
+          if (rope_tinc) {
+            t = tb + it * RPI;
+            t = t >= p.rope_T ? t - p.rope_T : t;
+          } else {
+            t = i % p.rope_T;
+          }
           if (rope_vec) {
-            const int pr = (j % p.rope_dim) >> 1;
-            cs = *(const f32x4*)(p.rope_cos + t * rhalf + pr);
-            sn = *(const f32x4*)(p.rope_sin + t * rhalf + pr);
+            cs = *(const f32x4*)(p.rope_cos + t * rhalf + rope_pr);
+            sn = *(const f32x4*)(p.rope_sin + t * rhalf + rope_pr);
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
