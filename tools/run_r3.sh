@@ -33,3 +33,8 @@ for arm in bf16 fp8 fp8bwd; do
   grep '^{' $O/${TAG}_c5_$arm.log > $O/${TAG}_c5_$arm.json
 done
 step rccl2 200 python tools/rccl_2rank_probe.py
+# two ranks on the one GPU with gloo carrying the collectives: bench.py's N > 1
+# path (ZeRO-1 reduce-scatter / all-gather on device tensors, barriers, the
+# max-over-ranks clock, rank 0's line) short of RCCL itself
+NSTL_DIST_BACKEND=gloo step dist2_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --no-traffic --no-cpu-baseline --no-parity --feature-steps 0 --feed-steps 0
+grep '^{' $O/${TAG}_dist2_gloo.log > $O/${TAG}_dist2_gloo.json
