@@ -42,7 +42,7 @@ struct AttnParams {
   char* dk; int64_t dk_ld;
   char* dv; int64_t dv_ld;
   const float* rope_cos; const float* rope_sin; int rope_q, rope_k;
-  int rope_fast;  // fused backward: RoPE^T angles recomputed with v_sin / v_cos instead of the tables
+  int rope_fast;  // bf16 backward: RoPE^T angles recomputed with v_sin / v_cos instead of the tables
   int B, T, H, dh;
   float scale;
   uint32_t thresh; float inv_keep; uint64_t seed;
@@ -536,9 +536,13 @@ NSTL_DEV void rope_tab_fast(float (&tc)[4][4], float (&ts)[4][4], int row0, int 
     }
   }
 }
-NSTL_DEV void rope_back_tile(float (&v)[4][4], int row0, int c, const float* cs, const float* sn) {
+// fast: the angles recomputed (rope_tab_fast) instead of per-element table reads
+// from global memory (16 dependent L2 round trips per wave at the end of the split
+// kernels; bf16 only -- the f32 parity mode keeps the tables' exact values)
+NSTL_DEV void rope_back_tile(float (&v)[4][4], int row0, int c, const float* cs, const float* sn, bool fast = false) {
   float tc[4][4], ts[4][4];
-  rope_tab<DH / 2>(tc, ts, row0, c, cs, sn);
+  if (fast) rope_tab_fast(tc, ts, row0, c);
+  else rope_tab<DH / 2>(tc, ts, row0, c, cs, sn);
   rope_apply(v, tc, ts, c);
 }
 
@@ -596,8 +600,11 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
   const int T_ = p.T, nkt = T_ / 16;
   char* Kimg = smem;
   char* Vimg = Kimg + T_ * RBK;
-  char* scratch = Vimg + T_ * RBK;                 // [NW][16][RBK] output staging
-  float* red = (float*)(scratch + NW * 16 * RBK);  // [NW][64] bias partials
+  // T % 128 == 0 (every wave active): the output staging reuses the K image after
+  // a barrier (bwd_lds_bytes), so T = 256 fits two workgroups per CU
+  const bool alias = T_ % BWD_ROWS == 0;
+  char* scratch = alias ? smem : Vimg + T_ * RBK;  // [NW][16][RBK] output staging
+  float* red = (float*)(alias ? Vimg + T_ * RBK : scratch + NW * 16 * RBK);  // [NW][64] bias partials
   unsigned* arrived = (unsigned*)(red + 2 * NW * 64);
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
@@ -698,7 +705,8 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) vq[dt][r] = dq[dt][r] * p.scale;
-  if (p.rope_q) rope_back_tile(vq, q0 + 4 * g, c, p.rope_cos, p.rope_sin);
+  if (p.rope_q) rope_back_tile(vq, q0 + 4 * g, c, p.rope_cos, p.rope_sin, sizeof(T) == 2 && p.rope_fast);
+  if (alias) __syncthreads();  // every wave is done with the K / V images
   store_tile16x64<T>(vq, scratch + w * 16 * RBK, p.dq + ((tok0 + q0) * p.dq_ld + h * DH) * ESZ, p.dq_ld, lane);
   if (bias_row) {
     wave_colsum16x64<T>(vq, red, w, lane);
@@ -719,8 +727,9 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
   char* Dimg = Qimg + T_ * RBK;
   float* lse_s = (float*)(Dimg + T_ * RBK);
   float* dq_s = lse_s + T_;
-  char* scratch = (char*)(dq_s + T_);              // [NW][16][RBK] output staging
-  float* red = (float*)(scratch + NW * 16 * RBK);  // [2][NW][64] bias partials
+  const bool alias = T_ % BWD_ROWS == 0;           // as in attn_bwd_dq_kernel: staging over the Q image
+  char* scratch = alias ? smem : (char*)(dq_s + T_);  // [NW][16][RBK] output staging
+  float* red = alias ? dq_s + T_ : (float*)(scratch + NW * 16 * RBK);  // [2][NW][64] bias partials
   unsigned* arrived = (unsigned*)(red + 2 * NW * 64);
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
@@ -821,7 +830,8 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
       vk[dt][r] = dk[dt][r] * p.scale;
       vv[dt][r] = DM != 0 ? dv[dt][r] * p.inv_keep : dv[dt][r];
     }
-  if (p.rope_k) rope_back_tile(vk, k0 + 4 * g, c, p.rope_cos, p.rope_sin);
+  if (p.rope_k) rope_back_tile(vk, k0 + 4 * g, c, p.rope_cos, p.rope_sin, sizeof(T) == 2 && p.rope_fast);
+  if (alias) __syncthreads();  // every wave is done with the Q / dO images
   char* scr = scratch + w * 16 * RBK;
   store_tile16x64<T>(vk, scr, p.dk + ((tok0 + k0) * p.dk_ld + h * DH) * ESZ, p.dk_ld, lane);
   store_tile16x64<T>(vv, scr, p.dv + ((tok0 + k0) * p.dv_ld + h * DH) * ESZ, p.dv_ld, lane);
@@ -1097,8 +1107,9 @@ size_t fwd_lds_bytes(int T, int esz) {  // K, V images (the output leaves from r
   return (size_t)2 * T * DH * esz;
 }
 size_t bwd_lds_bytes(int T, int esz) {  // either backward kernel (+ 2 x [8][64] f32 bias partials + counter)
-  return (size_t)2 * T * DH * esz + 2 * T * 4 + (BWD_NT / 64) * 16 * DH * (size_t)esz + 2 * (BWD_NT / 64) * 64 * 4 +
-         16;
+  // T % BWD_ROWS == 0: the output staging reuses the first operand image
+  const size_t staging = T % BWD_ROWS == 0 ? 0 : (size_t)(BWD_NT / 64) * 16 * DH * esz;
+  return (size_t)2 * T * DH * esz + 2 * T * 4 + staging + 2 * (BWD_NT / 64) * 64 * 4 + 16;
 }
 
 // ---------------------------------------------------------------------------
@@ -1367,7 +1378,7 @@ int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   p.dv = (char*)a->dv; p.dv_ld = a->dv_ld;
   p.rope_cos = a->rope_cos; p.rope_sin = a->rope_sin;
   p.rope_q = a->rope_q; p.rope_k = a->rope_k;
-  {  // NSTL_ROPE_BWD=table: the fused backward reads the tables (A/B; read per call)
+  {  // NSTL_ROPE_BWD=table: the bf16 backward kernels read the tables (A/B; read per call)
     const char* e = getenv("NSTL_ROPE_BWD");
     p.rope_fast = !(e && e[0] == 't');
   }
