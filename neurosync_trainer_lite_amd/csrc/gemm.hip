@@ -127,7 +127,7 @@ NSTL_DEV void epi_store4(const GemmParams& p, int i, int j, f32x4 v) {
   }
   v = epi_math4(p, i, j, v);
   const int64_t o = (int64_t)i * p.ldc + j;
-  const bool vec = j + 3 < p.N && (p.ldc & 3) == 0;
+  const bool vec = j + 3 < p.N && (p.ldc & 3) == 0 && ((uintptr_t)p.C % (p.c_f32 ? 16 : 8)) == 0;
   if (p.c_f32) {
     float* c = (float*)p.C + o;
     if (vec) {
@@ -626,7 +626,7 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
   const int64_t ldc = EM == EM_WS ? p.N : p.ldc;
   const int c = (lane % LPR) * CW, j = col0 + c;
   const bool colok = j < p.N;
-  const bool vec = j + CW <= p.N && (ldc % CW) == 0;
+  const bool vec = j + CW <= p.N && (ldc % CW) == 0 && ((uintptr_t)C % 16) == 0;
   const bool use_beta = EM == EM_F32 && p.beta != 0.f;
   float bias[CW], csc[CW];
 #pragma unroll

@@ -173,6 +173,28 @@ def test_gemm_plain_on_hipblaslt(case):
     check(C, ref, 1e-2 if C.dtype == dt else 1e-4, "hipBLASLt " + case)
 
 
+@pytest.mark.parametrize("case", ["k_not_64", "few_tiles", "misaligned_c"])
+def test_gemm_plain_outside_hipblaslt_stays_native(case):
+    """A plain bf16 GEMM that hipBLASLt's eligibility rule turns away (K not a
+    multiple of 64, fewer than 32 tiles of 256^2, a C pointer off 16-byte
+    alignment) runs on the hand-written kernels, with the same result."""
+    dt = torch.bfloat16
+    M, N, Kd = {"k_not_64": (4096, 2048, 1000), "few_tiles": (1024, 1024, 1024),
+                "misaligned_c": (4096, 2048, 1024)}[case]
+    X, W = rnd(M, Kd, dtype=dt, seed=511), rnd(N, Kd, dtype=dt, scale=0.05, seed=512)
+    if case == "misaligned_c":
+        buf = torch.empty(M * N + 8, dtype=dt, device=DEV)
+        C = buf[4:4 + M * N].view(M, N)  # 8-byte offset: not 16-byte aligned
+    else:
+        C = torch.empty(M, N, dtype=dt, device=DEV)
+    K.kernel_counts_reset()
+    K.gemm(X, W, C, M, N, Kd)
+    torch.cuda.synchronize()
+    c = K.kernel_counts()
+    assert c["gemm_lt"] == 0 and c["gemm_ring"] + c["gemm128"] == 1, c
+    check(C, f64(X) @ f64(W).T, 1e-2, "native " + case)
+
+
 def test_gemm_rejects_bad_args():
     A = torch.zeros(16, 12, device=DEV)
     C = torch.zeros(16, 16, device=DEV)
