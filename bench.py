@@ -48,7 +48,10 @@ def frames_flops(W, T, D, n_attn=24):
 
 
 def _is_bf16_gemm(name):
-    return "gemm" in name and "splitk" not in name and "f8" not in name
+    # the hand-written kernels, and the hipBLASLt (Tensile "Cijk_...") kernels that
+    # nstl_gemm hands its plain bf16-output GEMMs to (NSTL_GEMM_LT): the same launches
+    # the in-run HIP-event timing of nstl_gemm sees
+    return ("gemm" in name or "Cijk_" in name) and "splitk" not in name and "f8" not in name
 
 
 def _pmc_dispatches(d):
@@ -600,7 +603,7 @@ def main():
             "config": {"workload": "228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam)",
                        "model": "NeuroSync Seq2Seq 228M", "global_batch": B * world, "seq_len": T,
                        "frames_per_step": B * T * world, "parallelism": "dp%d" % world},
-            "roofline": {"bound": "mfma", "kernel": "nstl GEMM family (gemm256r_kernel, its grouped form, gemm_kernel), every launch "
+            "roofline": {"bound": "mfma", "kernel": "nstl GEMM family (gemm256r_kernel, its grouped form, gemm_kernel; the plain bf16-output GEMMs on hipBLASLt), every launch "
                                                     "of the last %d timed steps" % n_sampled,
                          "achieved": round(achieved_tf, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": traffic,
