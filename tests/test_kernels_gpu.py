@@ -248,10 +248,9 @@ def _keep_pattern_np(seed, M, N, p):
 
 @pytest.mark.parametrize("Kd", [256, 1024, 2048])
 def test_gemm_relu_dropout_keep_pattern_matches_hash(Kd):
-    """The ring kernel hashes the ReLU-dropout keep bits inside its K loop (one
-    unit per K-step; units past a short K loop after it): with every
-    pre-activation positive, the zero pattern is exactly the hash's, for K loops
-    shorter than, equal to and longer than the 16 units."""
+    """The ring kernel's ReLU-dropout epilogue keeps element (i, j) by the dropout
+    hash of its pair index (common.h): with every pre-activation positive, the
+    zero pattern is exactly the hash's, at short, medium and long K."""
     M, N = 2048, 1024
     X = rnd(M, Kd, dtype=torch.bfloat16, seed=150)
     W = rnd(N, Kd, dtype=torch.bfloat16, seed=151, scale=0.01)
