@@ -41,7 +41,9 @@ for name, n, k, kw in (
         ("fwd ffn1 BIAS", F, D, dict(epilogue=K.EPI_BIAS)),
         ("fwd ffn1 RELU p0", F, D, dict(epilogue=K.EPI_BIAS_RELU_DROP, p_drop=0.0, seed=5)),
         ("fwd ffn1 RELU_DROP", F, D, dict(epilogue=K.EPI_BIAS_RELU_DROP, p_drop=0.3, seed=5)),
+        ("fwd qkv  BIAS", 3 * D, D, dict(epilogue=K.EPI_BIAS)),
         ("fwd qkv  ROPE", 3 * D, D, dict(epilogue=K.EPI_BIAS_ROPE, rope=(cs, sn, T, 64), rope_cols=2 * D)),
+        ("fwd kvc  BIAS", 2 * D, D, dict(epilogue=K.EPI_BIAS)),
         ("fwd kvc  ROPE", 2 * D, D, dict(epilogue=K.EPI_BIAS_ROPE, rope=(cs, sn, T, 64), rope_cols=D))):
     X = x if k == D else x4
     W, b = r(n, k), torch.zeros(n, device=dev)
