@@ -213,6 +213,139 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
   }
 }
 
+// MFMA form (r3, default): the lag products of one frame as a small f64 GEMM.
+// With n = 16 b + a, r[k] = sum_a P[a][a + k] where P[a][m] = sum_b x[16b + a]
+// x[16b + m] (a < 16, m < 16 AC3_TILES), i.e. P = U^T V over the 16-sample blocks
+// b with U[b][a] = x[16b + a] and V[b][m] = x[16b + m].  On
+// v_mfma_f64_16x16x4_f64 (one f64 of A and of B per lane: A[i = lane & 15][kk =
+// lane >> 4], B[kk][j = lane & 15]; D col = lane & 15, row = (lane >> 4) + 4 v)
+// k-step s covers blocks 4s..4s+3 and both operands are one contiguous LDS read:
+// A = x[64 s + lane], B(tile t) = x[64 s + 16 t + lane].  Every tile runs every
+// step: skipping the ~5 % whose B lies past the frame puts a branch per MFMA and
+// the compiler then serialises each one through an accumulator copy.  The matrix cores run the f64 FMAs the
+// register-tiled kernel above issues on the VALU (same peak rate on gfx950), so the
+// operand reads, loop and address work move off the issue port that bounds it.
+// One wave per frame, four frames per workgroup, no workgroup barrier; P leaves
+// the accumulators one 16 x 16 tile at a time through LDS (over the dead frame
+// image) and its diagonals complete 16 lags per tile.
+constexpr int AC3_TILES = 13;  // P columns 0..207: lags up to 192
+constexpr int AC3_WAVES = 4;
+constexpr int AC3_TW = 48;     // padded tile row (doubles): 16 zeros | 16 values | 16 zeros
+__host__ __device__ inline int ac3_steps(int L) { return (L + 63) / 64; }
+int ac3_xlen(int L) {  // largest B index 64 (S - 1) + 16 (TILES - 1) + 63, and room for the padded tile
+  return std::max(64 * ac3_steps(L) + 16 * (AC3_TILES - 1), 16 * AC3_TW);
+}
+size_t ac3_lds(int L) { return (size_t)AC3_WAVES * ac3_xlen(L) * sizeof(double); }
+
+// orders this wave's LDS accesses across lanes (LDS executes one wave's
+// instructions in order; this keeps the compiler from moving them)
+NSTL_DEV void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64 * AC3_WAVES) void autocorr3_kernel(const float* __restrict__ y, int64_t n, int L,
+                                                                   int hop, int n_lags, int n_frames,
+                                                                   const double* __restrict__ hann,
+                                                                   double* __restrict__ out, int xlen) {
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) double ac3_smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int f = blockIdx.x * AC3_WAVES + wv;
+  if (f >= n_frames) return;  // whole waves only; nothing below synchronises the workgroup
+  double* x = ac3_smem + (size_t)wv * xlen;
+  const int64_t start = (int64_t)f * hop - L / 2;
+  // the frame, 8 loads in flight per lane
+  double s = 0.0;
+  for (int k0 = 0; k0 < L; k0 += 8 * 64) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + 64 * u + lane;
+      int64_t i = start + (k < L ? k : L - 1);
+      if (i < 0) i = -i;  // numpy 'reflect' (edge not repeated)
+      if (i >= n) i = 2 * (n - 1) - i;
+      v[u] = y[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + 64 * u + lane;
+      if (k < L) {
+        x[k] = (double)v[u];
+        s += (double)v[u];
+      }
+    }
+  }
+  for (int k = L + lane; k < xlen; k += 64) x[k] = 0.0;
+  s = wave_sum_d(s);
+  // the reference subtracts the mean in float32 (frames are float32 until the
+  // float64 window multiplies them)
+  const float mean_f = (float)(s / L);
+  for (int k0 = 0; k0 < L; k0 += 8 * 64) {
+    double h[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + 64 * u + lane;
+      h[u] = hann[k < L ? k : L - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + 64 * u + lane;
+      if (k < L) {
+        const float c = (float)x[k] - mean_f;
+        x[k] = (double)c * h[u];
+      }
+    }
+  }
+  wave_lds_order();
+  d4 acc[AC3_TILES];
+#pragma unroll
+  for (int t = 0; t < AC3_TILES; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+  const int S = ac3_steps(L);
+  for (int st = 0; st < S; ++st) {
+    const double* xs = x + 64 * st + lane;
+    double b[AC3_TILES];
+#pragma unroll
+    for (int t = 0; t < AC3_TILES; ++t) b[t] = xs[16 * t];
+#pragma unroll
+    for (int t = 0; t < AC3_TILES; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(b[0], b[t], acc[t], 0, 0, 0);
+  }
+  // Diagonal sums.  The frame image is dead: a zero-padded tile T[16][AC3_TW] with
+  // the accumulator tile in columns 16..31 takes its place.  r[16 t + c] =
+  // D_t(c) + D_{t+1}(c - 16) (D_t(o) = sum_a P_t[a][a + o]): lanes (c, part) read
+  // 8 rows of the upper diagonal c (parts 0, 1) or the lower diagonal c - 16 (parts
+  // 2, 3), branch-free through the padding; lane c carries D_t(c) into the next tile.
+  wave_lds_order();
+  double* T = x;
+  for (int k = lane; k < 16 * AC3_TW; k += 64) T[k] = 0.0;
+  const int c = lane & 15, part = lane >> 4;
+  const int rb = 8 * (part & 1), col0 = part < 2 ? 16 + c : c;
+  double* orow = out + (int64_t)f * n_lags;
+  double carry = 0.0, r0 = 0.0;
+#pragma unroll
+  for (int t = 0; t < AC3_TILES; ++t) {
+    wave_lds_order();
+#pragma unroll
+    for (int v = 0; v < 4; ++v) T[(part + 4 * v) * AC3_TW + 16 + c] = acc[t][v];
+    wave_lds_order();
+    double d = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d += T[(rb + i) * AC3_TW + col0 + rb + i];
+    d += __shfl_xor(d, 16);                  // lanes 0..15: D_t(c); lanes 32..47: D_t(c - 16)
+    const double low = __shfl(d, c + 32);
+    if (t == 0) {
+      r0 = __shfl(d, 0);                     // lag 0 (D_1(-16) is empty)
+    } else {
+      const int k = 16 * (t - 1) + c;
+      if (lane < 16 && k >= 1 && k <= n_lags) {
+        const double v = carry + low;
+        orow[k - 1] = r0 != 0.0 ? v / r0 : v;
+      }
+    }
+    carry = d;
+  }
+}
+
 // np.hanning(L) (symmetric), computed on the host in f64 once per (device, L)
 int get_hann(int L, const double** out) {
   static std::mutex mu;
@@ -274,7 +407,15 @@ extern "C" int nstl_autocorr(const float* y, int64_t n_samples, int frame_length
     const char* e = getenv("NSTL_AUTOCORR_V1");
     return e && e[0] == '1';
   }();
-  if (!v1 && n_lags < AC2_LG * AC2_GROUPS && ac2_lds(frame_length) <= 65536) {
+  static const bool v2 = [] {
+    const char* e = getenv("NSTL_AUTOCORR_V2");
+    return e && e[0] == '1';
+  }();
+  if (!v1 && !v2 && n_lags < 16 * (AC3_TILES - 1) && ac3_lds(frame_length) <= 65536) {
+    hipLaunchKernelGGL(autocorr3_kernel, dim3((n_frames + AC3_WAVES - 1) / AC3_WAVES), dim3(64 * AC3_WAVES),
+                       ac3_lds(frame_length), st, y, n_samples, frame_length, hop_length, n_lags, n_frames, hann, out,
+                       ac3_xlen(frame_length));
+  } else if (!v1 && n_lags < AC2_LG * AC2_GROUPS && ac2_lds(frame_length) <= 65536) {
     hipLaunchKernelGGL(autocorr2_kernel, dim3(n_frames), dim3(AC2_NT), ac2_lds(frame_length), st, y, n_samples,
                        frame_length, hop_length, n_lags, hann, out, (int)ac2_chunk(frame_length),
                        (int)ac2_wlen(frame_length));
