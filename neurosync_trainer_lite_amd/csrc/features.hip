@@ -220,9 +220,11 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
 // v_mfma_f64_16x16x4_f64 (one f64 of A and of B per lane: A[i = lane & 15][kk =
 // lane >> 4], B[kk][j = lane & 15]; D col = lane & 15, row = (lane >> 4) + 4 v)
 // k-step s covers blocks 4s..4s+3 and both operands are one contiguous LDS read:
-// A = x[64 s + lane], B(tile t) = x[64 s + 16 t + lane].  Every tile runs every
-// step: skipping the ~5 % whose B lies past the frame puts a branch per MFMA and
-// the compiler then serialises each one through an accumulator copy.  The matrix cores run the f64 FMAs the
+// A = x[64 s + lane], B(tile t) = x[64 s + 16 t + lane].  A tile whose B lies
+// past the frame (64 s + 16 t >= L, ~5 % of them) is skipped by a scalar branch;
+// with the accumulators in VGPRs (Makefile: -amdgpu-mfma-vgpr-form) that costs
+// no copies (in the default AGPR form the compiler routes every branched MFMA
+// through a copy in and out of the AGPRs).  The matrix cores run the f64 FMAs the
 // register-tiled kernel above issues on the VALU (same peak rate on gfx950), so the
 // operand reads, loop and address work move off the issue port that bounds it.
 // One wave per frame, four frames per workgroup, no workgroup barrier; P leaves
@@ -308,7 +310,8 @@ __global__ __launch_bounds__(64 * AC3_WAVES) void autocorr3_kernel(const float* 
 #pragma unroll
     for (int t = 0; t < AC3_TILES; ++t) b[t] = xs[16 * t];
 #pragma unroll
-    for (int t = 0; t < AC3_TILES; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(b[0], b[t], acc[t], 0, 0, 0);
+    for (int t = 0; t < AC3_TILES; ++t)
+      if (64 * st + 16 * t < L) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(b[0], b[t], acc[t], 0, 0, 0);
   }
   // Diagonal sums.  The frame image is dead: a zero-padded tile T[16][AC3_TW] with
   // the accumulator tile in columns 16..31 takes its place.  r[16 t + c] =
