@@ -255,6 +255,9 @@ def data_feed(cfg, args, step_fn, dev, rank, world):
 
 FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md
 FP64_VECTOR_PEAK_TFLOPS = 78.6   # half the FP32 vector rate (a wave64 f64 FMA takes 4 cycles on SIMD-32)
+# v_mfma_f64_16x16x4_f64 measured alone (tools/micro/mfma_f64_rate.hip,
+# profiles/r3_f64_rate_micro.txt); it shares the f64 unit with the vector FMAs
+FP64_MFMA_MEASURED_TFLOPS = 49.4
 
 
 def feature_rooflines(K, audio, n_samp, sr, dev):
@@ -262,7 +265,8 @@ def feature_rooflines(K, audio, n_samp, sr, dev):
     events, median of 5), against the resource that bounds each:
     - autocorrelation (the dominant one): 2 * n_fft * (n_lags + 1) f64 FLOP per
       120 Hz frame (direct lag products, as the reference's f64 np.correlate)
-      vs the FP64 vector peak;
+      vs the FP64 peak (78.6 TF/s; the kernel runs them on the f64 MFMA, which
+      measured 49.4 TF/s alone: frac_of_mfma_measured);
     - fused STFT/mel: 5 n log2 n FLOP per frame (the radix-agnostic FFT count)
       + |X|^2 + mel bands, vs the FP32 vector peak; its algorithmic bytes (audio
       read once, mel power written) vs HBM."""
@@ -288,10 +292,11 @@ def feature_rooflines(K, audio, n_samp, sr, dev):
     sm_flop = (5.0 * n_fft * math.log2(n_fft) + 3 * (n_fft // 2 + 1) + 2 * 2 * (n_fft // 2 + 1)) * F
     sm_bytes = 4.0 * n_samp + 4.0 * 128 * F
     return {"frames_120hz": F,
-            "roofline": {"kernel": "autocorr2_kernel (f64 lag products, the feature path's longest kernel)",
-                         "bound": "fp64 VALU", "achieved": round(ac_flop / t_ac / 1e12, 2),
+            "roofline": {"kernel": "autocorr3_kernel (f64 MFMA lag products, the feature path's longest kernel)",
+                         "bound": "fp64", "achieved": round(ac_flop / t_ac / 1e12, 2),
                          "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(ac_flop / t_ac / 1e12 / FP64_VECTOR_PEAK_TFLOPS, 4),
+                         "frac_of_mfma_measured": round(ac_flop / t_ac / 1e12 / FP64_MFMA_MEASURED_TFLOPS, 4),
                          "us": round(t_ac * 1e6, 1), "algorithmic_flop": ac_flop},
             "stft_mel": {"kernel": "stft_mel_kernel (fused STFT/mel, mixed-radix f32 FFT in LDS)",
                          "us": round(t_sm * 1e6, 1), "achieved_tflops": round(sm_flop / t_sm / 1e12, 3),
