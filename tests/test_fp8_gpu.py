@@ -167,7 +167,8 @@ def test_fp8_228m_forward_within_metric_gate():
     scope: attention projections + encoder FFN linear1) against the fp32 oracle
     on bench.py's parity batch (2 windows x 128 frames, seeded weights): MSE
     within the metric's 1e-3 gate, and the HIP path runs exactly the scope the
-    oracle simulation (tests/test_fp8_cpu.py) decided."""
+    oracle simulation (tests/test_fp8_cpu.py) decided; the relative RMS error
+    stays under 5 % whatever the output scale."""
     from neurosync_trainer_lite_amd.config import training_config
     from neurosync_trainer_lite_amd.utils.model_utils import build_model
     from oracle import model_ref
@@ -193,7 +194,12 @@ def test_fp8_228m_forward_within_metric_gate():
     assert c["gemm_fp8"] == 5 * L, c  # per layer: enc q|k|v, ffn1; dec q|k|v, cross q, cross k|v
     ref = model_ref.seq2seq_forward(params, src, H).double()
     mse = ((p8 - ref) ** 2).mean().item()
+    # the metric's gate is absolute; the relative RMS error keeps the check
+    # independent of the output scale at this init (measured ~3.5 %)
+    rel = (mse / (ref ** 2).mean().item()) ** 0.5
+    print("C5 fp8 forward: mse %.3e, relative RMS error %.4f" % (mse, rel))
     assert mse < 1e-3, mse
+    assert rel < 0.05, rel
 
 
 def test_fp8_model_forward_and_step():
