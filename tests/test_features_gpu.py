@@ -34,6 +34,33 @@ def test_autocorr_matches_reference_fixture(golden):
         np.testing.assert_allclose(got, want, rtol=2e-6, atol=2e-7)
 
 
+@pytest.mark.parametrize("L,hop,n_lags", [(1470, 735, 187), (800, 400, 187), (1470, 735, 191), (266, 133, 40),
+                                           (64, 32, 10), (1801, 900, 150)])
+def test_autocorr_kernel_matches_oracle_across_frame_lengths(L, hop, n_lags):
+    """nstl_autocorr (the f64 MFMA kernel: 64-sample k-steps, 13 column tiles,
+    tiles past the frame skipped) at other sample rates' frame lengths, lag
+    counts up to its 191 limit, frames shorter than one k-step, and a frame
+    length that is not a multiple of 16, against the oracle's direct products.
+    The frame mean is the exact f32-rounded mean on the GPU and numpy's f32
+    pairwise sum in the reference; at 64-sample frames that DC difference alone
+    moves the normalised lags by up to ~2e-6 (5e-5 relative), so that case is held
+    to 3e-6 absolute; every frame length of a real sample rate (>= 266) to the
+    fixture's rtol 2e-6 / atol 2e-7."""
+    from neurosync_trainer_lite_amd import _hip as K
+    y = synth_audio(0.4, 21)
+    n = len(y)
+    F = (n + 2 * (L // 2) - L) // hop + 1
+    out = torch.empty(F, n_lags, dtype=torch.float64, device="cuda:0")
+    K.autocorr(torch.tensor(y, device="cuda:0"), L, hop, n_lags, out, F)
+    torch.cuda.synchronize()
+    want = data_ref.autocorr_features_120(y, L, hop, n_lags).T
+    assert want.shape == (F, n_lags)
+    if L >= 266:
+        np.testing.assert_allclose(out.cpu().numpy(), want, rtol=2e-6, atol=2e-7)
+    else:
+        np.testing.assert_allclose(out.cpu().numpy(), want, rtol=0, atol=3e-6)
+
+
 @pytest.mark.parametrize("seconds,seed", [(1.0, 3), (0.73, 4), (2.5, 6), (0.09, 7)])
 def test_features_match_oracle(seconds, seed):
     y = synth_audio(seconds, seed)
