@@ -1,4 +1,4 @@
-# autocorr3 tail-tile skip: feature tests, tools/bench_features.py new vs old (HEAD), alternating, then kernel stats of new
+# stft_mel LDS trim (half twiddle table, window read with the samples from global, band bounds in registers: 35 KB, 4 WGs/CU): feature tests, tools/bench_features.py new vs old (HEAD), alternating, then kernel stats of new
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
