@@ -377,9 +377,15 @@ class Seq2SeqEngine:
             p._nstl_engine = me
         self.name_of = {id(p): n for n, p in self._params}
         self._first_ptr = self._params[0][1].data_ptr()
+        self._grad_views = None
 
-    def ensure_bound(self):
-        """Re-pack if someone replaced parameter storage (e.g. model.to())."""
+    def ensure_bound(self, versions=True):
+        """Re-pack if someone replaced parameter storage (e.g. model.to()); keep
+        every p.grad on its arena slice; refresh the compute-dtype shadow after an
+        in-place change of a parameter (versions=False skips that check: the
+        backward uses the weights its forward used).  Runs on the host in front of
+        the backward's first launch, where the GPU waits for it: the common case is
+        one identity test per parameter (~340 in the 228M model)."""
         p0 = self._params[0][1]
         if p0.data_ptr() != self._first_ptr or p0.device != self.device:
             self.sync_pending()
@@ -389,13 +395,21 @@ class Seq2SeqEngine:
                     self.p32[o:o + k].view(shp).copy_(p.detach().to(self.device))
             self._rebind()
             self.refresh_shadow()
-        gbase = self.g32.data_ptr()
-        for n, p in self._params:
-            o, k, shp = self.offsets[n]
-            if p.grad is None or p.grad.data_ptr() != gbase + 4 * o:
-                p.grad = self.g32[o:o + k].view(shp)
-                self.grads_fresh = True
-        if any(p._version != self._versions.get(n, -1) for n, p in self._params):
+        gv = getattr(self, "_grad_views", None)
+        if gv is None:
+            gv = self._grad_views = [None] * len(self._params)
+        gbase = None
+        for i, (n, p) in enumerate(self._params):
+            gp = p.grad
+            if gp is not gv[i]:
+                if gbase is None:
+                    gbase = self.g32.data_ptr()
+                o, k, shp = self.offsets[n]
+                if gp is None or gp.data_ptr() != gbase + 4 * o:
+                    gp = p.grad = self.g32[o:o + k].view(shp)
+                    self.grads_fresh = True
+                gv[i] = gp
+        if versions and any(p._version != v for (n, p), v in zip(self._params, self._version_list)):
             self.refresh_shadow()
 
     def refresh_shadow(self):
@@ -403,6 +417,7 @@ class Seq2SeqEngine:
         if self.p16 is not self.p32:
             K.cast(self.p32, self.p16, stream=K.stream_of(self.device))
         self._versions = {n: p._version for n, p in self._params}
+        self._version_list = [p._version for n, p in self._params]
 
     def zero_grad(self):
         """Next backward overwrites the gradient arena instead of accumulating."""
@@ -1111,7 +1126,7 @@ class Seq2SeqEngine:
         if gen != sv["gen"]:
             raise RuntimeError("Seq2Seq forward was run again before backward of an earlier forward")
         bb, T = sv["bb"], sv["T"]
-        self.ensure_bound()
+        self.ensure_bound(versions=False)
         self.sync_pending()
         self.cur = bb
         self._main = torch.cuda.current_stream(self.device)
