@@ -573,6 +573,46 @@ def main():
             tt_ = torch.tensor([el_f], device=dev)
             torch.distributed.all_reduce(tt_, op=torch.distributed.ReduceOp.MAX)
             el_f = tt_.item()
+        # the same work as a two-stage pipeline: step i+1's features are extracted on
+        # a side stream while step i trains (a prefetching loader's schedule); all
+        # feature_steps extractions run inside the timed region
+        side = torch.cuda.Stream(dev)
+        main = torch.cuda.current_stream(dev)
+
+        def extract_side():
+            with torch.cuda.stream(side):
+                f = extract_audio_features_device(audio, sr, device=dev)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return f, ev
+
+        def pipelined(n):
+            f, ev = extract_side()
+            for i in range(n):
+                main.wait_event(ev)
+                f.record_stream(main)
+                nxt = extract_side() if i + 1 < n else None
+                src_f = f[:B * T].view(B, T, -1)
+                opt.zero_grad()
+                loss_p = crit(model(src_f), trg)
+                loss_p.backward()
+                opt.step(max_norm=2.0)
+                if nxt is not None:
+                    f, ev = nxt
+        pipelined(2)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        t2 = time.perf_counter()
+        pipelined(args.feature_steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el_p = time.perf_counter() - t2
+        if world > 1:
+            tt_ = torch.tensor([el_p], device=dev)
+            torch.distributed.all_reduce(tt_, op=torch.distributed.ReduceOp.MAX)
+            el_p = tt_.item()
         # extraction alone: 5 back-to-back calls (one call alone would time the
         # host's launches into an idle stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -584,10 +624,15 @@ def main():
         feat = {"value": round(B * T * world * args.feature_steps / el_f, 1), "unit": "frames/s",
                 "ms_per_step": round(el_f / args.feature_steps * 1e3, 3), "steps": args.feature_steps,
                 "feature_ms_per_step": round(e0.elapsed_time(e1) / 5, 3),
+                "pipelined_value": round(B * T * world * args.feature_steps / el_p, 1),
+                "pipelined_ms_per_step": round(el_p / args.feature_steps * 1e3, 3),
+                "pipelined": "step i+1's extraction on a side stream under step i (same extractions, same steps)",
                 "workload": "per step: %.1f s of synthetic 88.2 kHz audio per GPU -> GPU MFCC(+d,dd)+autocorr "
                             "features [%d frames x 256] -> the same train step" % (n_samp / sr, B * T)}
         feat.update(feature_rooflines(K, audio, n_samp, sr, dev))
         feat["roofline"]["share_of_features"] = round(feat["roofline"]["us"] * 1e-3 / feat["feature_ms_per_step"], 3)
+        feat["vs_resident"] = round(feat["value"] / value, 4)
+        feat["pipelined_vs_resident"] = round(feat["pipelined_value"] / value, 4)
 
     feed = None
     if args.feed_steps > 0:
