@@ -174,6 +174,44 @@ def test_state_dict_and_optimizer_round_trip(tmp_path):
         assert torch.equal(model(src), model2(src))
 
 
+@pytest.mark.parametrize("amp", [False, True])
+def test_parameter_and_grad_binding_survive_user_edits(amp):
+    """The engine's per-step binding check (one identity test per parameter, no
+    version scan in backward): a p.grad set to None or replaced by the user
+    between forward and backward is re-attached to its arena slice and receives
+    the gradient; an in-place edit of a weight before a forward reaches the
+    compute-dtype shadow (the next forward uses it)."""
+    torch.manual_seed(3)
+    src = torch.randn(2, 32, 256, device=DEV)
+    trg = torch.randn(2, 32, 61, device=DEV)
+    _, ref, crit_r, opt_r, _ = make(128, 2, 1, 6, amp=amp)
+    opt_r.zero_grad()
+    crit_r(ref(src), trg).backward()
+    want = {n: p.grad.detach().clone() for n, p in ref.named_parameters()}
+    _, model, crit, opt, _ = make(128, 2, 1, 6, amp=amp)
+    names = [n for n, _ in model.named_parameters()]
+    pm = dict(model.named_parameters())
+    opt.zero_grad()
+    loss = crit(model(src), trg)
+    pm[names[0]].grad = None
+    pm[names[-1]].grad = torch.zeros_like(pm[names[-1]])
+    loss.backward()
+    for n in (names[0], names[-1], names[len(names) // 2]):
+        g = pm[n].grad
+        assert g is not None and torch.equal(g, want[n]), n
+    # an in-place weight edit before the next forward: same output as a model
+    # loaded with the edited weights
+    _, m2, _, _, _ = make(128, 2, 1, 6, amp=amp)
+    w = "decoder.fc_output.weight"
+    with torch.no_grad():
+        pm[w].mul_(0.5)
+        dict(m2.named_parameters())[w].copy_(pm[w])
+    model.eval()
+    m2.eval()
+    with torch.no_grad():
+        assert torch.equal(model(src), m2(src))
+
+
 @pytest.mark.parametrize("D,H,L,T", [(256, 1, 1, 48), (512, 2, 1, 100)])
 def test_fp32_step_generic_attention_matches_oracle(D, H, L, T):
     """Head dims 256 (BASELINE C1's 1024/4) and ragged T take the generic
