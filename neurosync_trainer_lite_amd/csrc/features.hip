@@ -776,6 +776,150 @@ __global__ __launch_bounds__(FFT_NT) void stft_mel_kernel(const float* __restric
   }
 }
 
+// Wave-per-pair form (r3, default for n_fft <= SW_MAXN): the workgroup shares the
+// tables and nothing else; each wave owns one pair of frames at a time in its own
+// LDS buffer and runs the whole transform with no workgroup barrier.  A pass is
+// in place: every lane reads the R inputs of its n/(R 64) butterflies into
+// registers, the wave's LDS accesses are ordered (in order within a wave), and the
+// outputs go to the same buffer.  The power spectrum is written over the buffer
+// the same way, then the 2 x 128 mel bands come from it.  Same arithmetic per
+// element and same order as stft_mel_kernel.
+constexpr int SW_WAVES = 4, SW_MAXN = 1536, SW_NBIN = (SW_MAXN / 2 + 1 + 63) / 64;
+
+template <int R, int NBL>
+NSTL_DEV void fft_pass_wave(float2* buf, int n, int ns, const float2* tw, int lane) {
+  static_assert(NBL * 64 * R >= SW_MAXN, "butterflies per lane");
+  const int m = n / R, ts = n / (ns * R);
+  float2 W[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) W[k] = tw[k * m];
+  float2 v[NBL][R];
+#pragma unroll
+  for (int i = 0; i < NBL; ++i) {
+    const int j = lane + 64 * i;
+    if (j < m) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[i][r] = buf[j + r * m];
+    }
+  }
+  wave_lds_order();  // every input is in registers before any output lands
+#pragma unroll
+  for (int i = 0; i < NBL; ++i) {
+    const int j = lane + 64 * i;
+    if (j < m) {
+      const int jn = j % ns;
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[i][r] = cmul(v[i][r], tw[r * jn * ts]);  // r jn ts < n
+      const int base = (j - jn) * R + jn;
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        float2 acc = v[i][0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          const float2 w = W[(r * q) % R];
+          acc.x = fmaf(v[i][r].x, w.x, fmaf(-v[i][r].y, w.y, acc.x));
+          acc.y = fmaf(v[i][r].x, w.y, fmaf(v[i][r].y, w.x, acc.y));
+        }
+        buf[base + q * ns] = acc;
+      }
+    }
+  }
+  wave_lds_order();
+}
+
+__host__ __device__ inline size_t stft_wave_tables(int n, int nnz) {
+  return ((size_t)n * 8 + (size_t)n * 4 + 3 * N_MELS * 4 + (size_t)nnz * 4 + 15) / 16 * 16;
+}
+size_t stft_wave_lds(int n, int nnz) { return stft_wave_tables(n, nnz) + (size_t)SW_WAVES * n * 8; }
+
+// pairs of frames: wave w of workgroup b takes pairs (b SW_WAVES + w) ppw .. + ppw - 1
+__global__ __launch_bounds__(64 * SW_WAVES) void stft_mel_wave_kernel(
+    const float* __restrict__ y, int64_t n_samples, int hop, FftPlanArg plan, const float2* __restrict__ tw_g,
+    const float* __restrict__ win_g, const int* __restrict__ band_g, const float* __restrict__ bw_g, int nnz, int F,
+    float* __restrict__ mel, int* __restrict__ key, int ppw) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int n = plan.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float2* tw = (float2*)smem;
+  float* win = (float*)(tw + n);
+  int* band = (int*)(win + n);
+  float* bw = (float*)(band + 3 * N_MELS);
+  float2* buf = (float2*)(smem + stft_wave_tables(n, nnz)) + (size_t)wv * n;
+  for (int k = tid; k < n; k += 64 * SW_WAVES) {
+    tw[k] = tw_g[k];
+    win[k] = win_g[k];
+  }
+  for (int k = tid; k < 3 * N_MELS; k += 64 * SW_WAVES) band[k] = band_g[k];
+  for (int k = tid; k < nnz; k += 64 * SW_WAVES) bw[k] = bw_g[k];
+  __syncthreads();  // the tables: the only workgroup barrier
+  const int nb = n / 2 + 1, npairs = (F + 1) / 2;
+  float vmax = 0.f;
+  for (int pi = 0; pi < ppw; ++pi) {
+    const int pr = (blockIdx.x * SW_WAVES + wv) * ppw + pi;
+    if (pr >= npairs) break;  // uniform over the wave
+    const int f0 = 2 * pr;
+    const bool two = f0 + 1 < F;
+    const int64_t start = (int64_t)f0 * hop - n / 2;  // center=True, zero padding
+    wave_lds_order();  // the previous pair's mel reads are done
+    for (int k = lane; k < n; k += 64) {
+      const int64_t i0 = start + k, i1 = i0 + hop;
+      const float a = i0 >= 0 && i0 < n_samples ? y[i0] * win[k] : 0.f;
+      const float b = two && i1 >= 0 && i1 < n_samples ? y[i1] * win[k] : 0.f;
+      buf[k] = make_float2(a, b);
+    }
+    wave_lds_order();
+    int ns = 1;
+    for (int p = 0; p < plan.nf; ++p) {
+      const int r = plan.radix[p];
+      switch (r) {
+        case 2: fft_pass_wave<2, 12>(buf, n, ns, tw, lane); break;
+        case 3: fft_pass_wave<3, 8>(buf, n, ns, tw, lane); break;
+        case 4: fft_pass_wave<4, 6>(buf, n, ns, tw, lane); break;
+        case 5: fft_pass_wave<5, 5>(buf, n, ns, tw, lane); break;
+        default: fft_pass_wave<7, 4>(buf, n, ns, tw, lane); break;
+      }
+      ns *= r;
+    }
+    // |X0|^2, |X1|^2 of bins 0..nb-1 (see stft_mel_kernel) over the buffer
+    float2 z[SW_NBIN], zc[SW_NBIN];
+#pragma unroll
+    for (int i = 0; i < SW_NBIN; ++i) {
+      const int b = lane + 64 * i;
+      if (b < nb) {
+        z[i] = buf[b];
+        zc[i] = buf[b == 0 ? 0 : n - b];
+      }
+    }
+    wave_lds_order();
+    float* pw = (float*)buf;
+#pragma unroll
+    for (int i = 0; i < SW_NBIN; ++i) {
+      const int b = lane + 64 * i;
+      if (b < nb) {
+        const float ar = z[i].x + zc[i].x, ai = z[i].y - zc[i].y, br = z[i].x - zc[i].x, bi = z[i].y + zc[i].y;
+        pw[b] = 0.25f * (ar * ar + ai * ai);
+        pw[nb + b] = 0.25f * (br * br + bi * bi);
+      }
+    }
+    wave_lds_order();
+#pragma unroll
+    for (int i = 0; i < 2 * N_MELS / 64; ++i) {
+      const int e = lane + 64 * i, which = e / N_MELS, m = e % N_MELS;
+      if (which == 0 || two) {
+        const int lo = band[3 * m], cnt = band[3 * m + 1], off = band[3 * m + 2];
+        const float* pwf = pw + which * nb;
+        float acc = 0.f;
+        for (int t = 0; t < cnt; ++t) acc = fmaf(bw[off + t], pwf[lo + t], acc);
+        mel[(int64_t)(f0 + which) * N_MELS + m] = acc;
+        vmax = fmaxf(vmax, acc);
+      }
+    }
+  }
+  if (key != nullptr) {
+    vmax = wave_max(vmax);
+    if (lane == 0) atomicMax(key, __float_as_int(vmax));
+  }
+}
+
 size_t stft_mel_lds(int n, int nnz) { return (size_t)3 * n * 8 + (size_t)n * 4 + 3 * N_MELS * 4 + (size_t)nnz * 4; }
 
 // |X|^2 for bins 0..nb-1 into rows of nbp (zero tail): the mel GEMM's A operand
@@ -961,6 +1105,27 @@ int launch_stft_mel(const FeatTables* T, const float* y, int64_t n_samples, int 
   plan.n = T->n_fft;
   plan.nf = T->nf;
   for (int i = 0; i < 16; ++i) plan.radix[i] = T->radix[i];
+  static const bool wg_form = [] {
+    const char* e = getenv("NSTL_STFT_WG");
+    return e && e[0] == '1';
+  }();
+  if (!wg_form && T->n_fft <= SW_MAXN) {
+    const size_t lw = stft_wave_lds(T->n_fft, T->nnz);
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipFuncSetAttribute((const void*)stft_mel_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lw) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, stft_mel_wave_kernel, 64 * SW_WAVES, lw) != hipSuccess)
+      return nstl::fail((int)hipErrorInvalidValue, "nstl_features: stft_mel wave kernel setup failed");
+    const int npairs = (F + 1) / 2, waves = cus * std::max(per_cu, 1) * SW_WAVES;
+    const int ppw = std::max(1, (npairs + waves - 1) / waves);
+    const int grid = (npairs + ppw * SW_WAVES - 1) / (ppw * SW_WAVES);
+    hipLaunchKernelGGL(stft_mel_wave_kernel, dim3(grid), dim3(64 * SW_WAVES), lw, st, y, n_samples, hop, plan, T->tw,
+                       T->window, T->band, T->bw, T->nnz, F, mel, key, ppw);
+    NSTL_LAUNCH_CHECK("nstl_features stft_mel (wave)");
+    return 0;
+  }
   const size_t lds = stft_mel_lds(T->n_fft, T->nnz);
   NSTL_CHECK_ARG(lds <= 160 * 1024, "nstl_features: n_fft %d too large for the fused STFT/mel kernel", T->n_fft);
   hipLaunchKernelGGL(stft_mel_kernel, dim3((F + FFT_FPB - 1) / FFT_FPB), dim3(FFT_NT), lds, st, y, n_samples, hop,
