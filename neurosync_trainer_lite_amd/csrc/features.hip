@@ -1088,6 +1088,42 @@ FeatLayout feat_layout(int64_t n_samples, int sr) {
 
 __global__ void init_key(int* k) { *k = 0; }  // mel power >= 0: bits of 0.f
 
+// The autocorrelation depends on the audio only, so nstl_features forks it onto a
+// side stream (one per device, created once) and joins before the lag reduction:
+// the f64-MFMA-bound autocorrelation runs beside the latency-bound STFT/mel, DCT
+// and CMVN chain instead of after it.  NSTL_FEATURES_FORK=0 keeps one stream.
+struct FeatFork {
+  int dev = -1;
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+std::mutex g_fork_mu;  // held from the fork record to the join wait of one call
+
+bool fork_on() {
+  static const bool on = [] {
+    const char* e = getenv("NSTL_FEATURES_FORK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// caller holds g_fork_mu
+FeatFork* get_fork() {
+  static std::vector<FeatFork> forks;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  for (auto& f : forks)
+    if (f.dev == dev) return &f;
+  FeatFork f;
+  f.dev = dev;
+  if (hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&f.join, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  forks.push_back(f);
+  return &forks.back();
+}
+
 // NSTL_FEATURES_FFT=0: the frames -> DFT GEMM -> power -> mel GEMM path instead
 // of the fused STFT/mel kernel (A/B comparisons; also any n_fft with a prime
 // factor > 7)
@@ -1176,6 +1212,19 @@ extern "C" int nstl_features(const float* y, int64_t n_samples, int sr, float* o
   float* mf = (float*)(ws + L.mfcc);
   double* ac = (double*)(ws + L.ac);
   int* key = (int*)(ws + L.key);
+  std::unique_lock<std::mutex> fork_lk(g_fork_mu, std::defer_lock);
+  FeatFork* fk = nullptr;
+  if (fork_on()) {
+    fork_lk.lock();
+    fk = get_fork();
+  }
+  if (fk != nullptr) {
+    if (hipEventRecord(fk->fork, st) != hipSuccess || hipStreamWaitEvent(fk->side, fk->fork, 0) != hipSuccess)
+      return nstl::fail((int)hipErrorLaunchFailure, "nstl_features: side-stream fork failed");
+    if (int rc = nstl_autocorr(y, n_samples, L.n_fft, L.hop, N_AC, ac, L.F, fk->side)) return rc;
+    if (hipEventRecord(fk->join, fk->side) != hipSuccess)
+      return nstl::fail((int)hipErrorLaunchFailure, "nstl_features: side-stream join failed");
+  }
 
   if (use_fft(T)) {
     // fused STFT/mel: mel power -> db buffer, clip-wide max -> key
@@ -1210,7 +1259,12 @@ extern "C" int nstl_features(const float* y, int64_t n_samples, int sr, float* o
   hipLaunchKernelGGL(dct_kernel, dim3((L.F + 63) / 64), dim3(256), 0, st, db, L.F, T->dct, key, mf);
   NSTL_LAUNCH_CHECK("nstl_features dct");
   if (int rc = launch_cmvn(mf, L.F, N_MFCC, T->sg, (double*)(ws + L.cmvn), out, ld_out, L.F60, st)) return rc;
-  if (int rc = nstl_autocorr(y, n_samples, L.n_fft, L.hop, N_AC, ac, L.F, stream)) return rc;
+  if (fk != nullptr) {
+    if (hipStreamWaitEvent(st, fk->join, 0) != hipSuccess)
+      return nstl::fail((int)hipErrorLaunchFailure, "nstl_features: side-stream join failed");
+  } else if (int rc = nstl_autocorr(y, n_samples, L.n_fft, L.hop, N_AC, ac, L.F, stream)) {
+    return rc;
+  }
   const int64_t n_red = (int64_t)L.F60 * N_AC;
   hipLaunchKernelGGL(reduce_ac_kernel, dim3((unsigned)((n_red + 255) / 256)), dim3(256), 0, st, ac, L.F, N_AC, out,
                      ld_out, 3 * N_MFCC, L.F60);
