@@ -58,6 +58,8 @@ def _pad64(n):
     return (n + 63) // 64 * 64
 
 
+_UNBOUND = object()  # Seq2SeqEngine.ensure_bound: no p.grad seen yet
+
 class _Buffers:
     """Activation workspace for one (B, T, save) shape."""
 
@@ -396,8 +398,8 @@ class Seq2SeqEngine:
             self._rebind()
             self.refresh_shadow()
         gv = getattr(self, "_grad_views", None)
-        if gv is None:
-            gv = self._grad_views = [None] * len(self._params)
+        if gv is None:  # a sentinel, not None: a p.grad of None must fail the identity test
+            gv = self._grad_views = [_UNBOUND] * len(self._params)
         gbase = None
         for i, (n, p) in enumerate(self._params):
             gp = p.grad

@@ -191,6 +191,8 @@ def test_parameter_and_grad_binding_survive_user_edits(amp):
     _, model, crit, opt, _ = make(128, 2, 1, 6, amp=amp)
     names = [n for n, _ in model.named_parameters()]
     pm = dict(model.named_parameters())
+    for p_ in model.parameters():  # before the engine's first forward, too
+        p_.grad = None
     opt.zero_grad()
     loss = crit(model(src), trg)
     pm[names[0]].grad = None
