@@ -9,6 +9,7 @@
 // windowed frame lives in LDS as f64 (the reference is f64 from the window on).
 #include <algorithm>
 #include <cmath>
+#include <deque>
 #include <mutex>
 #include <vector>
 
@@ -1109,7 +1110,7 @@ bool fork_on() {
 
 // caller holds g_fork_mu
 FeatFork* get_fork() {
-  static std::vector<FeatFork> forks;
+  static std::deque<FeatFork> forks;  // stable addresses as devices are added
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   for (auto& f : forks)
