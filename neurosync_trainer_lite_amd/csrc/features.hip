@@ -852,6 +852,8 @@ __global__ __launch_bounds__(64 * SW_WAVES) void stft_mel_wave_kernel(
   for (int k = tid; k < 3 * N_MELS; k += 64 * SW_WAVES) band[k] = band_g[k];
   for (int k = tid; k < nnz; k += 64 * SW_WAVES) bw[k] = bw_g[k];
   __syncthreads();  // the tables: the only workgroup barrier
+  // the clip as a buffer resource (the launcher keeps 4 n_samples < 2^31)
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, (int)(n_samples * 4), 0x00020000);
   const int nb = n / 2 + 1, npairs = (F + 1) / 2;
   float vmax = 0.f;
   for (int pi = 0; pi < ppw; ++pi) {
@@ -860,12 +862,23 @@ __global__ __launch_bounds__(64 * SW_WAVES) void stft_mel_wave_kernel(
     const int f0 = 2 * pr;
     const bool two = f0 + 1 < F;
     const int64_t start = (int64_t)f0 * hop - n / 2;  // center=True, zero padding
+    // both frames' samples: every load of the lane in flight at once (one memory
+    // latency per pair; a load-use loop pays ~n/64 of them).  Buffer loads with
+    // 32-bit offsets: a sample outside the clip (the centre padding, a negative
+    // offset wraps past the range) reads as 0 from the range check.
+    float a[SW_MAXN / 64], b[SW_MAXN / 64];
+    const int o0 = (int)start * 4;
+#pragma unroll
+    for (int u = 0; u < SW_MAXN / 64; ++u) {
+      const int off = o0 + (lane + 64 * u) * 4;
+      a[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(yr, off, 0, 0));
+      b[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(yr, off + hop * 4, 0, 0));
+    }
     wave_lds_order();  // the previous pair's mel reads are done
-    for (int k = lane; k < n; k += 64) {
-      const int64_t i0 = start + k, i1 = i0 + hop;
-      const float a = i0 >= 0 && i0 < n_samples ? y[i0] * win[k] : 0.f;
-      const float b = two && i1 >= 0 && i1 < n_samples ? y[i1] * win[k] : 0.f;
-      buf[k] = make_float2(a, b);
+#pragma unroll
+    for (int u = 0; u < SW_MAXN / 64; ++u) {
+      const int k = lane + 64 * u;
+      if (k < n) buf[k] = make_float2(a[u] * win[k], two ? b[u] * win[k] : 0.f);
     }
     wave_lds_order();
     int ns = 1;
@@ -1146,7 +1159,7 @@ int launch_stft_mel(const FeatTables* T, const float* y, int64_t n_samples, int 
     const char* e = getenv("NSTL_STFT_WG");
     return e && e[0] == '1';
   }();
-  if (!wg_form && T->n_fft <= SW_MAXN) {
+  if (!wg_form && T->n_fft <= SW_MAXN && n_samples < (int64_t)1 << 29) {
     const size_t lw = stft_wave_lds(T->n_fft, T->nnz);
     int dev = 0, cus = 0, per_cu = 0;
     if (hipFuncSetAttribute((const void*)stft_mel_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
