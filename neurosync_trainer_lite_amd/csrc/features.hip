@@ -233,7 +233,8 @@ __global__ __launch_bounds__(AC2_NT) void autocorr2_kernel(const float* y, int64
 // image) and its diagonals complete 16 lags per tile.
 constexpr int AC3_TILES = 13;  // P columns 0..207: lags up to 192
 constexpr int AC3_WAVES = 4;
-constexpr int AC3_TW = 48;     // padded tile row (doubles): 16 zeros | 16 values | 16 zeros
+constexpr int AC3_TW = 48;
+constexpr int AC3_LD = 24;     // loads per lane in the one-batch frame load: frames up to 1536 samples     // padded tile row (doubles): 16 zeros | 16 values | 16 zeros
 __host__ __device__ inline int ac3_steps(int L) { return (L + 63) / 64; }
 int ac3_xlen(int L) {  // largest B index 64 (S - 1) + 16 (TILES - 1) + 63, and room for the padded tile
   return std::max(64 * ac3_steps(L) + 16 * (AC3_TILES - 1), 16 * AC3_TW);
@@ -258,45 +259,78 @@ __global__ __launch_bounds__(64 * AC3_WAVES) void autocorr3_kernel(const float* 
   if (f >= n_frames) return;  // whole waves only; nothing below synchronises the workgroup
   double* x = ac3_smem + (size_t)wv * xlen;
   const int64_t start = (int64_t)f * hop - L / 2;
-  // the frame, 8 loads in flight per lane
   double s = 0.0;
-  for (int k0 = 0; k0 < L; k0 += 8 * 64) {
-    float v[8];
+  float mean_f;
+  if (L <= 64 * AC3_LD && n < ((int64_t)1 << 29)) {
+    // every sample and window load of the lane in flight at once (one memory
+    // latency per frame), 32-bit buffer offsets; mean and window from registers
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, (int)(n * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc((void*)hann, 0, L * 8, 0x00020000);
+    const int st0 = (int)start, nn = (int)n;
+    float v[AC3_LD];
+    double h[AC3_LD];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int k = k0 + 64 * u + lane;
-      int64_t i = start + (k < L ? k : L - 1);
-      if (i < 0) i = -i;  // numpy 'reflect' (edge not repeated)
-      if (i >= n) i = 2 * (n - 1) - i;
-      v[u] = y[i];
+    for (int u = 0; u < AC3_LD; ++u) {
+      const int k = 64 * u + lane, kk = k < L ? k : L - 1;
+      int i = st0 + kk;
+      i = i < 0 ? -i : i;  // numpy 'reflect' (edge not repeated)
+      i = i >= nn ? 2 * (nn - 1) - i : i;
+      v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(yr, i * 4, 0, 0));
+      h[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(hr, kk * 8, 0, 0));
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int k = k0 + 64 * u + lane;
-      if (k < L) {
-        x[k] = (double)v[u];
-        s += (double)v[u];
+    for (int u = 0; u < AC3_LD; ++u)
+      if (64 * u + lane < L) s += (double)v[u];
+    s = wave_sum_d(s);
+    // the reference subtracts the mean in float32 (frames are float32 until the
+    // float64 window multiplies them)
+    mean_f = (float)(s / L);
+#pragma unroll
+    for (int u = 0; u < AC3_LD; ++u) {
+      const int k = 64 * u + lane;
+      if (k < L) x[k] = (double)(v[u] - mean_f) * h[u];
+    }
+    for (int k = L + lane; k < xlen; k += 64) x[k] = 0.0;
+  } else {
+    // the frame, 8 loads in flight per lane
+    for (int k0 = 0; k0 < L; k0 += 8 * 64) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + 64 * u + lane;
+        int64_t i = start + (k < L ? k : L - 1);
+        if (i < 0) i = -i;  // numpy 'reflect' (edge not repeated)
+        if (i >= n) i = 2 * (n - 1) - i;
+        v[u] = y[i];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + 64 * u + lane;
+        if (k < L) {
+          x[k] = (double)v[u];
+          s += (double)v[u];
+        }
       }
     }
-  }
-  for (int k = L + lane; k < xlen; k += 64) x[k] = 0.0;
-  s = wave_sum_d(s);
-  // the reference subtracts the mean in float32 (frames are float32 until the
-  // float64 window multiplies them)
-  const float mean_f = (float)(s / L);
-  for (int k0 = 0; k0 < L; k0 += 8 * 64) {
-    double h[8];
+    for (int k = L + lane; k < xlen; k += 64) x[k] = 0.0;
+    s = wave_sum_d(s);
+    // the reference subtracts the mean in float32 (frames are float32 until the
+    // float64 window multiplies them)
+    mean_f = (float)(s / L);
+    for (int k0 = 0; k0 < L; k0 += 8 * 64) {
+      double h[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int k = k0 + 64 * u + lane;
-      h[u] = hann[k < L ? k : L - 1];
-    }
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + 64 * u + lane;
+        h[u] = hann[k < L ? k : L - 1];
+      }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int k = k0 + 64 * u + lane;
-      if (k < L) {
-        const float c = (float)x[k] - mean_f;
-        x[k] = (double)c * h[u];
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + 64 * u + lane;
+        if (k < L) {
+          const float c = (float)x[k] - mean_f;
+          x[k] = (double)c * h[u];
+        }
       }
     }
   }
