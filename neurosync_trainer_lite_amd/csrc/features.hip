@@ -5,8 +5,10 @@
 // hop_length, per-frame DC removal, symmetric Hann (np.hanning), lags
 // 0..n_lags by direct products (the reference computes a full 2N-1-lag
 // np.correlate and keeps n_lags+1 of them), normalise by lag 0 when non-zero,
-// drop lag 0, replicate near-silent edge frames.  One workgroup per frame; the
-// windowed frame lives in LDS as f64 (the reference is f64 from the window on).
+// drop lag 0, replicate near-silent edge frames.  The windowed frame lives in LDS
+// as f64 (the reference is f64 from the window on); the default kernel
+// (autocorr3_kernel) runs the lag products as a per-frame f64 GEMM on the matrix
+// cores, one wave per frame; the VALU forms below it stay behind switches.
 #include <algorithm>
 #include <cmath>
 #include <deque>
