@@ -13,6 +13,7 @@
 // (2x2) each owning 64x64 = 4x4 MFMA 16x16 tiles, register-staged double-
 // buffered LDS (one barrier per K tile), XCD-aware tile order.
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../include/nstl.h"
 #include <map>
@@ -40,6 +41,7 @@ struct GemmParams {
   const char* aux; int64_t ld_aux; int aux_f32;
   float inv_keep; uint32_t thresh; uint64_t seed;
   const float* rope_cos; const float* rope_sin; int rope_T, rope_dim, rope_cols;
+  int rope_fast;  // ring epilogue: cos/sin recomputed from t * inv_freq instead of read from the tables
   float* ws;
   int debug_skip_epilogue; int k_chunk;  // split-K: partial slabs [z][M][N]
   float* colsum_part;  // [ceil(M/128)][N]: column sums of C as stored (dReLU ring epilogue)
@@ -648,6 +650,10 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
   // a pass's rows ib + it * RPI span < 64 rows: with rope_T >= 64 their positions
   // follow from the pass's first by one conditional wrap (no integer modulo per row)
   const bool rope_tinc = EM == EM_ROPE && p.rope_T >= 64;
+  float rope_if[4];  // inv_freq of this lane's 4 rotation pairs (NSTL_GEMM_ROPE=fast)
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    rope_if[e] = EM == EM_ROPE ? expf(-9.21034049987793f * (float)(2 * (rope_pr + e)) / (float)p.rope_dim) : 0.f;
   const int r0 = lane / LPR;
   // dReLU epilogue: column sums of the stored dh (the FFN1 bias gradient)
   const bool csum_on = EM == EM_DRELU && p.colsum_part != nullptr;
@@ -689,7 +695,16 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
           } else {
             t = i % p.rope_T;
           }
-          if (rope_vec) {
+          if (rope_vec && p.rope_fast) {
+            // angle = f32(t) * inv_freq exactly as rotation_tables() forms it, then the
+            // hardware sin / cos (~1e-6 from the tables, below bf16 rounding)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float a = (float)t * rope_if[e];
+              sn[e] = __sinf(a);
+              cs[e] = __cosf(a);
+            }
+          } else if (rope_vec) {
             cs = *(const f32x4*)(p.rope_cos + t * rhalf + rope_pr);
             sn = *(const f32x4*)(p.rope_sin + t * rhalf + rope_pr);
           } else {
@@ -2032,6 +2047,13 @@ int make_params(const nstl_gemm_args* a, GemmParams& p) {
   p.seed = a->seed;
   p.rope_cos = a->rope_cos; p.rope_sin = a->rope_sin;
   p.rope_T = a->rope_T; p.rope_dim = a->rope_dim; p.rope_cols = a->rope_cols;
+  {
+    // NSTL_GEMM_ROPE=fast (A/B, read per call): the bf16 ring epilogue recomputes the
+    // RoPE angles (v_sin / v_cos, as the attention backward does) instead of loading
+    // 2 x 16 B of table per row; the f32 parity-mode kernels always use the tables
+    const char* e = getenv("NSTL_GEMM_ROPE");
+    p.rope_fast = e != nullptr && strcmp(e, "fast") == 0;
+  }
   p.ws = nullptr;
   p.debug_skip_epilogue = getenv_debug_skip_epi();
   // NSTL_GEMM_DIRECT=0: the LDS-staged EM_BF16 epilogue (A/B; read per call).  The
