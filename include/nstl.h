@@ -348,7 +348,8 @@ enum {
   NSTL_K_ATTN_BWD_FUSED,     /* one-kernel attention backward */
   NSTL_K_ATTN_BWD_SPLIT,     /* dQ + dK/dV kernel pairs */
   NSTL_K_ATTN_BWD_GENERIC,
-  NSTL_K_GEMM_LT,            /* plain bf16 GEMMs run on hipBLASLt (NSTL_GEMM_LT) */
+  NSTL_K_GEMM4,              /* 4-wave persistent 256x256 GEMM launches (csrc/gemm4.h) */
+  NSTL_K_GEMM4_TILES,        /*   ... their 256x256 output tiles */
   NSTL_K_COUNT
 };
 /* Copies min(n, NSTL_K_COUNT) counters to out; returns NSTL_K_COUNT. */

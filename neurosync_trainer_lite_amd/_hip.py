@@ -124,7 +124,7 @@ EXPORTS = [
 # nstl_kernel_counts order (NSTL_K_* in include/nstl.h)
 KERNEL_COUNT_NAMES = ["gemm128", "gemm_ring", "gemm_ring_tiles", "gemm_group", "gemm_group_tiles",
                       "gemm_splitk_reduce", "gemm_fp8", "attn_fwd", "attn_fwd_generic", "attn_bwd_fused",
-                      "attn_bwd_split", "attn_bwd_generic", "gemm_lt"]
+                      "attn_bwd_split", "attn_bwd_generic", "gemm4", "gemm4_tiles"]
 
 _lib = None
 

@@ -1268,9 +1268,25 @@ extern "C" int nstl_features(const float* y, int64_t n_samples, int sr, float* o
     fork_lk.lock();
     fk = get_fork();
   }
+  // Once the side stream is forked, every return joins it first: the side stream
+  // reads y and writes the workspace, and the caller's allocator may hand those
+  // blocks out again on st as soon as st has passed its last use of them.
+  struct ForkJoin {
+    FeatFork* fk = nullptr;
+    hipStream_t st = nullptr;
+    bool joined = false;
+    ~ForkJoin() {
+      if (fk != nullptr && !joined) {
+        (void)hipEventRecord(fk->join, fk->side);
+        (void)hipStreamWaitEvent(st, fk->join, 0);
+      }
+    }
+  } fj;
   if (fk != nullptr) {
     if (hipEventRecord(fk->fork, st) != hipSuccess || hipStreamWaitEvent(fk->side, fk->fork, 0) != hipSuccess)
       return nstl::fail((int)hipErrorLaunchFailure, "nstl_features: side-stream fork failed");
+    fj.fk = fk;
+    fj.st = st;
     if (int rc = nstl_autocorr(y, n_samples, L.n_fft, L.hop, N_AC, ac, L.F, fk->side)) return rc;
     if (hipEventRecord(fk->join, fk->side) != hipSuccess)
       return nstl::fail((int)hipErrorLaunchFailure, "nstl_features: side-stream join failed");
@@ -1310,6 +1326,7 @@ extern "C" int nstl_features(const float* y, int64_t n_samples, int sr, float* o
   NSTL_LAUNCH_CHECK("nstl_features dct");
   if (int rc = launch_cmvn(mf, L.F, N_MFCC, T->sg, (double*)(ws + L.cmvn), out, ld_out, L.F60, st)) return rc;
   if (fk != nullptr) {
+    fj.joined = true;
     if (hipStreamWaitEvent(st, fk->join, 0) != hipSuccess)
       return nstl::fail((int)hipErrorLaunchFailure, "nstl_features: side-stream join failed");
   } else if (int rc = nstl_autocorr(y, n_samples, L.n_fft, L.hop, N_AC, ac, L.F, stream)) {

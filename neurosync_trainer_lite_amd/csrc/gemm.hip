@@ -696,8 +696,10 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
             t = i % p.rope_T;
           }
           if (rope_vec && p.rope_fast) {
-            // angle = f32(t) * inv_freq exactly as rotation_tables() forms it, then the
-            // hardware sin / cos (~1e-6 from the tables, below bf16 rounding)
+            // angle = f32(t) * inv_freq with inv_freq = expf(-ln(1e4) * 2i / d), which is
+            // NOT the tables' pow form, then the hardware sin / cos, which lose accuracy as
+            // the angle grows: only a kernel-level tolerance covers this (off by default;
+            // it needs a parity test against the tables at the largest production T first)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float a = (float)t * rope_if[e];
@@ -2107,7 +2109,8 @@ bool big_ok(const nstl_gemm_args* a) {
 }  // namespace
 
 namespace nstl {
-int lt_gemm(const nstl_gemm_args* a, hipStream_t st, int* handled);  // lt.hip
+int gemm4(const nstl_gemm_args* a, hipStream_t st, int* handled);                   // gemm4.hip
+int gemm4_grouped(const nstl_gemm_args* args, int n, hipStream_t st, int* handled);  // gemm4.hip
 }
 
 extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
@@ -2115,9 +2118,9 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   if (int rc = make_params(a, p)) return rc;
   NSTL_CHECK_ARG(!a->sq_part, "nstl_gemm: sq_part is produced by nstl_gemm_grouped only");
   if (a->dtype == NSTL_FP8) return gemm_f8(a, p, (hipStream_t)stream);
-  {  // plain bf16 GEMMs (no fused epilogue beyond a bias) on hipBLASLt
+  {  // full 256^2 tiles: the 4-wave persistent kernel (gemm4.hip); the rest below
     int handled = 0;
-    if (int rc = nstl::lt_gemm(a, (hipStream_t)stream, &handled)) return rc;
+    if (int rc = nstl::gemm4(a, (hipStream_t)stream, &handled)) return rc;
     if (handled) return 0;
   }
   const int esz = a->dtype == NSTL_F32 ? 4 : 2;
@@ -2186,6 +2189,11 @@ extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream
   for (int g = 0; g < n; ++g)
     NSTL_CHECK_ARG(!args[g].sq_part || em == EM_F32, "nstl_gemm_grouped: sq_part needs f32 output");
   hipStream_t st = (hipStream_t)stream;
+  {  // full tiles, beta 0: the 4-wave persistent kernel (gemm4.hip)
+    int handled = 0;
+    if (int rc = nstl::gemm4_grouped(args, n, st, &handled)) return rc;
+    if (handled) return 0;
+  }
   dim3 grid(tiles), block(BIG_NT);
 #define NSTL_GROUP_LAUNCH(AKv, BKv)                                                                        \
   if (em == EM_F32) hipLaunchKernelGGL((gemm256r_group_kernel<AKv, BKv, EM_F32>), grid, block, 0, st, gp); \

@@ -1,0 +1,601 @@
+// 4-wave persistent 256 x 256 MFMA GEMM for gfx950 (device code, shared by
+// gemm4.hip and tools/micro/gemm4_bench.hip).
+//
+//   C[i, j] = alpha * sum_r A(i, r) B(j, r)  (+ epilogue)
+//
+// For full 256 x 256 tiles it replaces the 8-wave ring kernel (gemm.hip) and
+// the library dispatch of round 3.
+//
+// Wave layout.  One workgroup = 4 waves, one per SIMD; wave (wm, wn) owns the
+// 128 x 128 block (wm, wn) of the tile: 8 x 8 accumulators of
+// v_mfma_f32_16x16x32_bf16 (operands swapped, so lane (g = l >> 4, c = l & 15)
+// holds row 16a + c, columns 16b + 4g .. +3 of acc[a][b]), 256 f32 per lane in
+// AGPRs.  A wave reads 16 fragments per 64 MFMAs (the 8-wave ring: 12 per 32).
+//
+// K loop (BK = 64).  Two 64 KB stages; A slots at [0, 32K) / [32K, 64K), B at
+// [64K, 96K) / [96K, 128K).  K-major images have 128-byte rows (one whole cache
+// line per row and stage: with 64-byte rows every DMA piece fetched half lines,
+// and the K loop ran 8-12 % slower, tools/micro/gemm4_bench.hip); chunk c of row
+// r sits at c ^ ((r >> 1) & 7).  MN-major images are 64 rows (k) x 512 B
+// (ImgMN<512>, transpose reads).  A step is two half-steps of 64 MFMAs: h = 0
+// computes k 0..31 of stage s (register set F0) while reading k 32..63 into F1;
+// h = 1 computes F1 while reading stage s + 1's k 0..31 into F0 and issuing
+// stage s + 2's 16 LDS-DMA pieces (buffer_load ... lds; per-lane 32-bit source
+// offsets fixed per tile, the K advance a scalar offset) into the slot stage s
+// just vacated.  One barrier per step, before h = 1: the counted vmcnt retires
+// this wave's pieces of stage s + 1, the barrier publishes every wave's, and
+// every wave is done reading stage s.  Reads and DMA pieces are interleaved with
+// the MFMAs in a fixed order (sched_barrier): one wave per SIMD has no partner
+// wave to hide them.
+//
+// Persistent tiles.  Workgroup w runs tiles w, w + G, ... (XCD-aware order).
+// The stage sequence runs on across tiles: the last two steps of a tile stage
+// the next tile's first two stages and its last half-step reads the next tile's
+// first fragments, so the next K loop starts with no fill.  The first half-step
+// of a tile takes C = 0 (no accumulator zeroing).  The epilogue runs from
+// registers (no LDS staging, no barrier).  Its stores are the youngest VMEM
+// operations when the next tile's step 0 waits for its stage 1, so that wait
+// is counted past them (vmcnt retires in issue order) and they drain under the
+// next tile's first step.
+#pragma once
+#include "common.h"
+#include <type_traits>
+
+namespace g4 {
+
+constexpr int NT = 256;
+constexpr int TILE = 256;
+constexpr int BK = 64;
+constexpr int OPS = 32768;         // one operand's stage image
+constexpr int SMEM = 4 * OPS;      // 128 KB of stages
+constexpr int ROPE_LDS = 32768;    // RoPE tables (EM_ROPE): T * rope_dim * 4 bytes at most
+constexpr int GROUP_MAX = 16;
+
+// epilogue kinds (the ring kernel's EM_* numbering)
+enum { EM_BF16 = 1, EM_RELU_DROP = 2, EM_ROPE = 3, EM_DRELU = 4, EM_F32 = 5 };
+
+struct Params {
+  const char* A; int64_t lda;
+  const char* B; int64_t ldb;
+  char* C; int64_t ldc;
+  int M, N, K;
+  float alpha;
+  const float* bias;               // [N] or null (BF16, RELU_DROP, ROPE)
+  float inv_keep; uint32_t thresh; uint64_t seed;
+  const float* rope_cos; const float* rope_sin; int rope_T, rope_dim, rope_cols;
+  float* colsum_part;              // [M / 128][N] (DRELU)
+  uint64_t* relu_mask;             // keep & positive bits, the ring layout (RELU_DROP writes, DRELU reads)
+  float* sq_part;                  // [tiles][8] sums of squares of C (F32)
+  uint32_t a_bytes, b_bytes;       // extents of A and B (buffer range checks)
+  int tiles_m, tiles_n;
+};
+
+struct GroupParams {
+  Params g[GROUP_MAX];
+  int tile_end[GROUP_MAX];
+  int n;
+};
+static_assert(sizeof(GroupParams) <= 4096, "kernel arguments");
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+NSTL_DEV uint32_t lds_addr(const char* p) { return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p; }
+
+#define G4_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+#define G4_SB() __builtin_amdgcn_sched_barrier(0)
+#define G4_LGKM0()                                      \
+  do {                                                  \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    G4_SB();                                            \
+  } while (0)
+
+// one 1 KB DMA piece: lane l writes bytes [16 l, 16 l + 16) of `lds`
+NSTL_DEV void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds, 16, voff, soff, 0, 0);
+}
+
+// Per-lane DMA source offsets of this wave's 8 pieces of one operand's stage,
+// relative to the tile's first row (K-major) / column (MN-major): fixed per
+// problem.  The tile's offset and the K advance go in the scalar offset.
+// Full tiles only: no row clamping.
+template <bool KMAJ>
+NSTL_DEV void dma_lane_offsets(uint32_t (&vo)[8], int64_t ld, int wave, int lane) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int q = wave * 8 + s;
+    if (KMAJ) {  // 128-byte rows (64 k), 8 rows per piece
+      const int row = 8 * q + (lane >> 3), pc = lane & 7;
+      const int lc = pc ^ ((row >> 1) & 7);
+      vo[s] = (uint32_t)(((int64_t)row * ld + lc * 8) * 2);
+    } else {     // 512-byte rows (256 m/n), 2 rows (k) per piece, ImgMN<512>
+      const int row = 2 * q + (lane >> 5), pc = lane & 31;
+      const int x = (row & 3) | (((row >> 3) & 1) << 2);
+      const int lc = pc ^ (x << 1);
+      vo[s] = (uint32_t)(((int64_t)row * ld + lc * 8) * 2);
+    }
+  }
+}
+
+// LDS fragment reads as inline asm: the compiler would otherwise wait vmcnt(0)
+// before LDS reads that may alias an in-flight DMA (gemm.hip).  Offsets are
+// immediates; the caller orders them with lgkmcnt + sched_barrier.
+template <int OFF>
+NSTL_DEV void ds_b128(bf16x8& f, uint32_t addr) {
+  i32x4_t v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  f = __builtin_bit_cast(bf16x8, v);
+}
+template <int OFF>
+NSTL_DEV void ds_tr2(bf16x8& f, uint32_t a0, uint32_t a1) {
+  i32x2_t v0, v1;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v0) : "v"(a0), "i"(OFF));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v1) : "v"(a1), "i"(OFF));
+  const bf16x4 b0 = __builtin_bit_cast(bf16x4, v0), b1 = __builtin_bit_cast(bf16x4, v1);
+  f = (bf16x8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+}
+
+// Per-lane LDS read addresses of one operand, slot 0.  K-major: one base per
+// half-step (the swizzle makes h a lane-dependent offset), row block j at
+// + 2048 j.  MN-major: 8 x 2 transpose-read addresses (block j), h at + 16 KB.
+template <bool KMAJ>
+struct RdAddr {
+  uint32_t k[2];
+  uint32_t t[8][2];
+};
+template <bool KMAJ>
+NSTL_DEV void rd_addr(RdAddr<KMAJ>& r, uint32_t img, int blk0, int lane) {
+  if (KMAJ) {
+    const int row = blk0 + (lane & 15), sw = (row >> 1) & 7;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) r.k[h] = img + row * 128 + (((4 * h + (lane >> 4)) ^ sw) << 4);
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int byte = (blk0 + 16 * j + 4 * pp) * 2;
+      r.t[j][0] = img + ImgMN<512>::off(8 * g + q, byte);
+      r.t[j][1] = img + ImgMN<512>::off(8 * g + 4 + q, byte);
+    }
+  }
+}
+template <bool KMAJ, int H, int J>
+NSTL_DEV void rd_frag(bf16x8& f, const RdAddr<KMAJ>& r, uint32_t so) {
+  // slot offset `so` added at the read (not hoisted: sched_barriers fence each read)
+  if constexpr (KMAJ) ds_b128<J * 2048>(f, r.k[H] + so);
+  else ds_tr2<H * 16384>(f, r.t[J][0] + so, r.t[J][1] + so);
+}
+// item J of 16: A block J (J < 8), B block J - 8
+template <bool AK, bool BKM, int H, int J>
+NSTL_DEV void rd_item(bf16x8 (&fa)[8], bf16x8 (&fb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb, uint32_t so) {
+  if constexpr (J < 8) rd_frag<AK, H, J>(fa[J], ra, so);
+  else rd_frag<BKM, H, J - 8>(fb[J - 8], rb, so);
+}
+
+// DMA state: buffer resources and per-lane offsets (per problem), the tile's
+// scalar byte offsets, the bytes per 64-deep stage
+struct Dma {
+  __amdgpu_buffer_rsrc_t ra, rb;
+  uint32_t va[8], vb[8];
+  uint32_t ta, tb;
+  uint32_t a_kb, b_kb;
+};
+template <bool AK, bool BKM>
+NSTL_DEV void dma_lanes(Dma& d, const Params& p, int wave, int lane) {
+  dma_lane_offsets<AK>(d.va, p.lda, wave, lane);
+  dma_lane_offsets<BKM>(d.vb, p.ldb, wave, lane);
+}
+// the scalar part of a tile (resources rebuilt from the kernel arguments every
+// tile: a resource chosen by a branch is not provably uniform, and the compiler
+// would wrap every DMA in a readfirstlane loop)
+template <bool AK, bool BKM>
+NSTL_DEV void dma_tile(Dma& d, const Params& p, int m0, int n0) {
+  d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)p.a_bytes, 0x00020000);
+  d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, (int)p.b_bytes, 0x00020000);
+  d.a_kb = AK ? 2 * BK : (uint32_t)(2 * BK * p.lda);
+  d.b_kb = BKM ? 2 * BK : (uint32_t)(2 * BK * p.ldb);
+  d.ta = __builtin_amdgcn_readfirstlane(AK ? (uint32_t)(m0 * p.lda * 2) : (uint32_t)(m0 * 2));
+  d.tb = __builtin_amdgcn_readfirstlane(BKM ? (uint32_t)(n0 * p.ldb * 2) : (uint32_t)(n0 * 2));
+}
+
+NSTL_DEV void mma16z(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+}
+
+// One half-step: 64 MFMAs on (ca, cb) (ZC: C = 0); if RD, the 16 reads into
+// (na, nb) follow MFMAs 1, 4, ..., 46; if DMA, the 16 pieces follow MFMAs 2, 6,
+// ..., 62 (A pieces to adst, B pieces to bdst, stage offsets sa / sb).  The
+// reads early and the pieces spread: tools/micro/gemm4_bench.hip measured the
+// other placements 1-7 % slower.
+// DBG (timing experiments only, wrong results): 1 no DMA, 2 no reads, 8 no MFMA.
+template <bool AK, bool BKM, bool ZC, bool RD, int RH, bool DMA, int DBG, int I = 0>
+NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 (&cb)[8], bf16x8 (&na)[8],
+                        bf16x8 (&nb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb, uint32_t so, const Dma& d,
+                        char* adst, char* bdst, uint32_t sa, uint32_t sb) {
+  if constexpr (I < 64) {
+    if constexpr (!(DBG & 8)) {
+      if constexpr (ZC) mma16z(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
+      else mma16(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
+    }
+    G4_SB();
+    if constexpr (RD && !(DBG & 2) && I % 3 == 1 && I / 3 < 16) {
+      rd_item<AK, BKM, RH, I / 3>(na, nb, ra, rb, so);
+      G4_SB();
+    }
+    if constexpr (DMA && !(DBG & 1) && (I & 3) == 2) {
+      constexpr int q = I >> 2;
+      if constexpr (q < 8) dma16(d.ra, adst + q * 1024, d.va[q], d.ta + sa);
+      else dma16(d.rb, bdst + (q - 8) * 1024, d.vb[q - 8], d.tb + sb);
+      G4_SB();
+    }
+    half_step<AK, BKM, ZC, RD, RH, DMA, DBG, I + 1>(acc, ca, cb, na, nb, ra, rb, so, d, adst, bdst, sa, sb);
+  }
+}
+
+// grouped tile order over XCD-contiguous id ranges (as the ring kernel)
+NSTL_DEV void tile_coords(int id, int nt_m, int nt_n, int& m0, int& n0) {
+  constexpr int GROUP_M = 4;
+  const int per_group = GROUP_M * nt_n;
+  const int first_m = (id / per_group) * GROUP_M;
+  const int gm = min(nt_m - first_m, GROUP_M);
+  const int in_g = id % per_group;
+  m0 = (first_m + in_g % gm) * TILE;
+  n0 = (in_g / gm) * TILE;
+}
+
+NSTL_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  const bf16 a = (bf16)lo, b = (bf16)hi;
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+
+// ReLU keep&positive bits in the ring kernel's word layout (gemm.hip
+// relu_mask_index): word ((row >> 6) * 8 + (row & 7)) * ceil(N / 8) + col / 8,
+// byte (row & 63) >> 3, bit col & 7.  Lane (g, c) of acc[a][b] holds rows
+// 16a + c: byte 2(a & 3) + (c >> 3) of word (row block a >> 2, r0 = c & 7, column
+// group 2b + (g >> 1)), bits 4(g & 1) .. +3.
+NSTL_DEV int64_t mask_word(int N, int row, int col) {
+  return ((int64_t)(row >> 6) * 8 + (row & 7)) * ((N + 7) >> 3) + (col >> 3);
+}
+
+// RoPE tables in LDS (EM_ROPE): row t holds rope_dim / 2 (cos, sin) pairs,
+// 16-byte chunk k (pairs 2k, 2k + 1) at k ^ (t & 15): the 16 lanes of a read
+// (16 consecutive positions, one chunk) hit 16 distinct bank slots
+NSTL_DEV int rope_off(int t, int chunk, int row_bytes) { return t * row_bytes + ((chunk ^ (t & 15)) << 4); }
+
+// An accumulator tile read out of the AGPRs at the point of use ...  Left to the
+// compiler, the epilogue's VALU uses split the accumulators' live range at the
+// epilogue entry: all 256 are copied to VGPRs at once and the DMA offsets and
+// next fragments spill around them.
+NSTL_DEV f32x4 rd_acc(f32x4& x) {
+  // ... and zeroed in place for the next tile (an MFMA with C = 0 instead would
+  // give the first step's results new registers: copies and spills)
+  float r0, r1, r2, r3;
+  asm volatile(
+      "v_accvgpr_read_b32 %0, %4\n\t"
+      "v_accvgpr_read_b32 %1, %5\n\t"
+      "v_accvgpr_read_b32 %2, %6\n\t"
+      "v_accvgpr_read_b32 %3, %7\n\t"
+      "v_accvgpr_write_b32 %4, 0\n\t"
+      "v_accvgpr_write_b32 %5, 0\n\t"
+      "v_accvgpr_write_b32 %6, 0\n\t"
+      "v_accvgpr_write_b32 %7, 0"
+      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "+a"(x[0]), "+a"(x[1]), "+a"(x[2]), "+a"(x[3]));
+  return (f32x4){r0, r1, r2, r3};
+}
+
+// ---------------------------------------------------------------------------
+// Epilogues, from registers.  row0 / col0: the wave's 128 x 128 block.
+// bf16 outputs: per (a, pair of column blocks bp, bp + 1) the elementwise math
+// runs on the accumulator layout (lane: 4 columns of block bp and 4 of bp + 1,
+// row 16a + c), then a permlane16 swap of the packed pairs gives each lane 8
+// consecutive columns: one 16-byte store (16 rows x 64 B per wave instruction).
+// No epilogue loads from memory after its first store (vmcnt retires in issue
+// order, so such a load would wait for the stores before it): the inputs are
+// loaded first (bias, dReLU mask words) or read from LDS (RoPE tables).
+template <int EM>
+NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, int lane, int wave, int tile_id,
+                       const char* rope_lds) {
+  const int g = lane >> 4, c = lane & 15, odd = g & 1;
+  const float alpha = p.alpha;
+  if constexpr (EM == EM_F32) {
+    // f32 out: lane stores its 4 columns (16 B); sum of squares of the stored
+    // values -> sq_part (the clip norm's partial, training_utils.py:73)
+    float ssq = 0.f;
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      float* crow = (float*)p.C + (int64_t)(row0 + 16 * a + c) * p.ldc + col0 + 4 * g;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const f32x4 v = rd_acc(acc[a][b]) * alpha;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ssq += v[e] * v[e];
+        *(f32x4*)(crow + 16 * b) = v;
+        G4_SB();
+      }
+    }
+    // the sum is formed unconditionally (a conditional one kept every stored value
+    // alive until after the stores, and spilled them)
+    const double tsum = wave_sum_d((double)ssq);
+    if (p.sq_part != nullptr && lane == 0) {
+      p.sq_part[tile_id * 8 + 2 * wave] = (float)tsum;
+      p.sq_part[tile_id * 8 + 2 * wave + 1] = 0.f;
+    }
+  } else {
+    float bias[8][4];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        bias[b][e] = (EM != EM_DRELU && p.bias != nullptr) ? p.bias[col0 + 16 * b + 4 * g + e] : 0.f;
+    const uint32_t seed_term = nstl_seed_term(p.seed);
+    const bool rmask = (EM == EM_RELU_DROP || EM == EM_DRELU) && p.relu_mask != nullptr;
+    // mask nibbles: [row block hb][column block b], 4 rows (a & 3) x 4 bits
+    uint32_t mbits[2][8];
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) mbits[hb][b] = 0;
+    if (EM == EM_DRELU) {
+      // the lane's nibble of each word: byte 2 a2 + (c >> 3), bits 4 (g & 1)
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const uint64_t w = p.relu_mask[mask_word(p.N, row0 + 64 * hb + c, col0 + 16 * b + 4 * g)];
+          uint32_t s = 0;
+#pragma unroll
+          for (int a2 = 0; a2 < 4; ++a2) s |= ((uint32_t)(w >> (8 * (2 * a2 + (c >> 3)) + 4 * odd)) & 0xF) << (4 * a2);
+          mbits[hb][b] = s;
+        }
+    }
+    float csum[8][4];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[b][e] = 0.f;
+    const int rope_rb = p.rope_dim * 4;  // bytes per table row in LDS
+    bf16* const cbase = (bf16*)p.C + (int64_t)(row0 + c) * p.ldc + col0;
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      const int row = row0 + 16 * a + c;
+      bf16* crow = cbase + (int64_t)(16 * a) * p.ldc;
+      const int t = EM == EM_ROPE ? row % p.rope_T : 0;
+#pragma unroll
+      for (int bp = 0; bp < 8; bp += 2) {
+        f32x4 uv[2] = {rd_acc(acc[a][bp]), rd_acc(acc[a][bp + 1])};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int b = bp + s;
+          const int col = col0 + 16 * b + 4 * g;
+          f32x4 v = uv[s] * alpha;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bias[b][e];
+          if constexpr (EM == EM_RELU_DROP) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            if (p.thresh) {
+              const uint32_t pair = (uint32_t)row * (uint32_t)(p.N >> 1) + (uint32_t)(col >> 1);
+#pragma unroll
+              for (int e = 0; e < 4; e += 2) {
+                bool k0, k1;
+                nstl_keep2_32(seed_term, pair + (e >> 1), p.thresh, k0, k1);
+                v[e] = k0 ? v[e] * p.inv_keep : 0.f;
+                v[e + 1] = k1 ? v[e + 1] * p.inv_keep : 0.f;
+              }
+            }
+            if (rmask) {
+              uint32_t nib = 0;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) nib |= ((bf16)v[e] > (bf16)0.f ? 1u : 0u) << e;  // as stored
+              mbits[a >> 2][b] |= nib << (4 * (a & 3));
+            }
+          } else if constexpr (EM == EM_ROPE) {
+            if (col < p.rope_cols) {
+              // pairs (col, col + 1), (col + 2, col + 3): chunk (col % rope_dim) / 4
+              const f32x4 cs = *(const f32x4*)(rope_lds + rope_off(t, (col % p.rope_dim) >> 2, rope_rb));
+              const float x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
+              v[0] = x0 * cs[0] - x1 * cs[1];
+              v[1] = x0 * cs[1] + x1 * cs[0];
+              v[2] = x2 * cs[2] - x3 * cs[3];
+              v[3] = x2 * cs[3] + x3 * cs[2];
+            }
+          } else if constexpr (EM == EM_DRELU) {
+            const uint32_t nib = mbits[a >> 2][b] >> (4 * (a & 3));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = ((nib >> e) & 1) ? v[e] * p.inv_keep : 0.f;
+            if (p.colsum_part != nullptr) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) csum[b][e] += (float)(bf16)v[e];  // sum what is stored
+            }
+          }
+          uv[s] = v;
+        }
+        const uint32_t x0 = pack_bf16x2(uv[0][0], uv[0][1]), x1 = pack_bf16x2(uv[0][2], uv[0][3]);
+        const uint32_t y0 = pack_bf16x2(uv[1][0], uv[1][1]), y1 = pack_bf16x2(uv[1][2], uv[1][3]);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        *(uint4*)(crow + 16 * (bp + odd) + 4 * (g - odd)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        G4_SB();  // one (a, bp) group at a time: hoisting the accumulator reads spills
+      }
+    }
+    if (EM == EM_RELU_DROP && rmask) {
+      // word (hb, r0 = c & 7, column group 2b + (g >> 1)) = OR over the 4 lanes
+      // (g, g ^ 1) x (c, c ^ 8) of their nibbles at byte 2 a2 + (c >> 3), bit 4 (g & 1)
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const uint32_t s = mbits[hb][b];
+          uint64_t w = 0;
+#pragma unroll
+          for (int a2 = 0; a2 < 4; ++a2) w |= (uint64_t)((s >> (4 * a2)) & 0xF) << (8 * (2 * a2 + (c >> 3)) + 4 * odd);
+          uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+          lo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0x128, 0xF, 0xF, false);  // c ^ 8 (row_ror:8)
+          hi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0x128, 0xF, 0xF, false);
+          const auto slo = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // g ^ 1
+          const auto shi = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+          lo = slo[0] | slo[1];
+          hi = shi[0] | shi[1];
+          if (c < 8 && odd == 0)
+            p.relu_mask[mask_word(p.N, row0 + 64 * hb + c, col0 + 16 * b + 4 * g)] = ((uint64_t)hi << 32) | lo;
+        }
+    }
+    if (EM == EM_DRELU && p.colsum_part != nullptr) {
+      // fold the 16 lanes c of each column inside the 16-lane row (DPP), then lane
+      // c == 0 writes the wave's 128-row partial of its 8 x 4 columns
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = csum[b][e];
+          x += NSTL_DPP(x, 0xB1);   // quad_perm [1, 0, 3, 2]
+          x += NSTL_DPP(x, 0x4E);   // quad_perm [2, 3, 0, 1]
+          x += NSTL_DPP(x, 0x141);  // row_half_mirror
+          x += NSTL_DPP(x, 0x140);  // row_mirror
+          csum[b][e] = x;
+        }
+      if (c == 0) {
+        float* dst = p.colsum_part + (int64_t)(row0 >> 7) * p.N + col0 + 4 * g;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) *(f32x4*)(dst + 16 * b) = (f32x4){csum[b][0], csum[b][1], csum[b][2], csum[b][3]};
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The persistent kernel.  Preconditions (host-checked): bf16 operands; every
+// problem's M, N multiples of 256, K a multiple of 64 with K >= 256; 16-byte
+// aligned rows; operand extents < 2^31 bytes; EM_ROPE: T * rope_dim * 4 <=
+// ROPE_LDS and rope_dim % 4 == 0; EM_F32: beta 0.  Tiles of up to 16 problems
+// (gp.tile_end; one problem: n = 1).
+template <bool AK, bool BKM, int EM, bool GROUPED, int DBG = 0>
+__global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + (EM == EM_ROPE ? ROPE_LDS : 0)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int T = gp.tile_end[gp.n - 1];
+  const int G = gridDim.x;
+  int t = blockIdx.x;
+  if (t >= T) return;
+  const uint32_t smem_u32 = lds_addr(smem);
+  char* const adst0 = smem + wave * 8 * 1024;
+  char* const bdst0 = smem + 2 * OPS + wave * 8 * 1024;
+  const char* rope_lds = smem + SMEM;
+  if constexpr (EM == EM_ROPE) {
+    // the whole cos/sin table, once per workgroup (one problem per launch)
+    const Params& p0 = gp.g[0];
+    const int half = p0.rope_dim >> 1, chunks = p0.rope_dim >> 2;
+    for (int i = tid; i < p0.rope_T * chunks; i += NT) {
+      const int tt = i / chunks, k = i - tt * chunks;
+      const float2 cs = *(const float2*)(p0.rope_cos + tt * half + 2 * k);
+      const float2 sn = *(const float2*)(p0.rope_sin + tt * half + 2 * k);
+      *(f32x4*)(smem + SMEM + rope_off(tt, k, p0.rope_dim * 4)) = (f32x4){cs.x, sn.x, cs.y, sn.y};
+    }
+    __syncthreads();
+  }
+
+  // tile index -> (problem, m0, n0); XCD-aware order within each problem
+  auto locate = [&](int tt, int& prob, int& m0, int& n0) {
+    prob = 0;
+    if (GROUPED)
+      while (prob + 1 < gp.n && tt >= gp.tile_end[prob]) ++prob;
+    const int first = prob ? gp.tile_end[prob - 1] : 0;
+    const Params& q = gp.g[prob];
+    tile_coords(xcd_remap(tt - first, gp.tile_end[prob] - first), q.tiles_m, q.tiles_n, m0, n0);
+  };
+  int prob, m0, n0;
+  locate(t, prob, m0, n0);
+  Dma d;
+  dma_lanes<AK, BKM>(d, gp.g[prob], wave, lane);
+  dma_tile<AK, BKM>(d, gp.g[prob], m0, n0);
+  RdAddr<AK> ra;
+  RdAddr<BKM> rb;
+  rd_addr<AK>(ra, smem_u32, wm * 128, lane);
+  rd_addr<BKM>(rb, smem_u32 + 2 * OPS, wn * 128, lane);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 f0a[8], f0b[8], f1a[8], f1b[8];
+  // prologue of the first tile: stages 0 and 1 landed (both: step 0's counted
+  // wait assumes an epilogue's stores behind stage 1), stage 0's k 0..31 read
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma16(d.ra, adst0 + s * OPS + q * 1024, d.va[q], d.ta + (uint32_t)s * d.a_kb);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma16(d.rb, bdst0 + s * OPS + q * 1024, d.vb[q], d.tb + (uint32_t)s * d.b_kb);
+  }
+  G4_VMCNT(0);
+  __builtin_amdgcn_s_barrier();
+  G4_SB();
+#define G4_RD0(J) rd_item<AK, BKM, 0, J>(f0a, f0b, ra, rb, 0u)
+  G4_RD0(0); G4_RD0(1); G4_RD0(2); G4_RD0(3); G4_RD0(4); G4_RD0(5); G4_RD0(6); G4_RD0(7);
+  G4_RD0(8); G4_RD0(9); G4_RD0(10); G4_RD0(11); G4_RD0(12); G4_RD0(13); G4_RD0(14); G4_RD0(15);
+#undef G4_RD0
+  G4_LGKM0();
+  uint32_t gs = 0;  // global step counter: stage slot = gs & 1
+
+  // step: h = 0 on F0 (ZC: the tile's first), the counted wait + barrier, h = 1
+  // on F1 with the reads of the following stage into F0 and the DMA of stage
+  // `dma_stage` of the tile `dd` describes.  WAITN: how many VMEM operations may
+  // stay in flight (issued after this wave's pieces of the stage to retire).
+  auto step = [&](auto zc_c, auto waitn_c, uint32_t dma_stage, const Dma& dd) {
+    constexpr bool ZC = decltype(zc_c)::value;
+    constexpr int WAITN = decltype(waitn_c)::value;
+    const uint32_t so = (gs & 1) * OPS;
+    half_step<AK, BKM, ZC, true, 1, false, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, so, dd, adst0, bdst0, 0, 0);
+    G4_LGKM0();
+    if constexpr (WAITN == 0) G4_VMCNT(0);
+    else if constexpr (WAITN == 32) G4_VMCNT(32);
+    else G4_VMCNT(63);
+    __builtin_amdgcn_s_barrier();
+    G4_SB();
+    half_step<AK, BKM, false, true, 0, true, DBG>(acc, f1a, f1b, f0a, f0b, ra, rb, so ^ OPS, dd, adst0 + so,
+                                                  bdst0 + so, dma_stage * dd.a_kb, dma_stage * dd.b_kb);
+    G4_LGKM0();
+    ++gs;
+  };
+  using NZ = std::false_type;
+  using W0 = std::integral_constant<int, 0>;
+  // an epilogue issues at least 32 (bf16: 16 B per lane and 8 columns) or 64 (f32)
+  // stores after the next tile's stage 1 pieces
+  using WE = std::integral_constant<int, EM == EM_F32 ? 63 : 32>;
+
+  for (;;) {
+    const Params& p = gp.g[prob];
+    const int nk = p.K / BK;
+    const int tn = t + G;
+    const bool has_next = tn < T;
+    // the next tile (after the workgroup's last: itself again, a harmless refill
+    // of slots nobody reads afterwards, drained before exit)
+    int nprob = prob, nm0 = m0, nn0 = n0;
+    if (has_next) locate(tn, nprob, nm0, nn0);
+    // step kt stages stage kt + 2: this tile's while kt + 2 < nk, then the next
+    // tile's 0 and 1 (one loop body: more step sites make the register
+    // allocator give the fragment sets different registers per site, and spill)
+    step(NZ{}, WE{}, 2u, d);
+    for (int kt = 1; kt < nk; ++kt) {
+      if (kt == nk - 2) {
+        if (GROUPED && nprob != prob) dma_lanes<AK, BKM>(d, gp.g[nprob], wave, lane);
+        dma_tile<AK, BKM>(d, gp.g[nprob], nm0, nn0);
+      }
+      const int ds = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
+      step(NZ{}, W0{}, (uint32_t)ds, d);
+    }
+    epilogue<EM>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, t, rope_lds);
+    if (!has_next) break;
+    t = tn;
+    prob = nprob;
+    m0 = nm0;
+    n0 = nn0;
+  }
+  G4_VMCNT(0);  // the refill must land before the workgroup's LDS is released
+}
+
+}  // namespace g4

@@ -1,0 +1,184 @@
+// Host side of the 4-wave persistent GEMM (gemm4.h): eligibility, parameters,
+// launch.  nstl_gemm / nstl_gemm_grouped (gemm.hip) try it first; problems it
+// does not take (partial tiles, split-K, beta != 0, fp8, the dReLU epilogue
+// without keep bits, RoPE tables past the LDS budget, ...) stay on the 8-wave
+// ring kernel.  NSTL_GEMM4=0 sends everything to the ring kernel (A/B runs).
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+
+#include "../../include/nstl.h"
+#include "common.h"
+#include "gemm4.h"
+#include "status.h"
+
+namespace {
+
+// read per call (a getenv per GEMM), so a test can compare both paths in one process
+int gemm4_env() {
+  const char* e = getenv("NSTL_GEMM4");
+  return e ? atoi(e) : 1;
+}
+
+// compute units of the current device (persistent grid size), cached per device
+int cus_of_current() {
+  static std::mutex mu;
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+// the epilogue kind this kernel runs for `a`, or 0 (not eligible)
+int g4_mode(const nstl_gemm_args* a) {
+  if (a->dtype != NSTL_BF16 || a->split_k > 1 || a->beta != 0.f || (a->sq_part != nullptr && a->c_dtype != NSTL_F32))
+    return 0;
+  const bool bf_out = a->c_dtype == NSTL_BF16;
+  switch (a->epilogue) {
+    case NSTL_EPI_NONE:
+      return bf_out ? g4::EM_BF16 : g4::EM_F32;
+    case NSTL_EPI_BIAS:
+      return bf_out ? g4::EM_BF16 : 0;
+    case NSTL_EPI_BIAS_RELU_DROP:
+      return bf_out && (a->N & 1) == 0 ? g4::EM_RELU_DROP : 0;
+    case NSTL_EPI_BIAS_ROPE:
+      return bf_out && a->rope_dim % 4 == 0 && a->rope_cols % 16 == 0 &&
+                     (int64_t)a->rope_T * a->rope_dim * 4 <= g4::ROPE_LDS
+                 ? g4::EM_ROPE
+                 : 0;
+    case NSTL_EPI_DRELU_DROP:
+      return bf_out && a->relu_mask != nullptr ? g4::EM_DRELU : 0;
+    default:
+      return 0;
+  }
+}
+
+bool g4_shape_ok(const nstl_gemm_args* a) {
+  if (a->M % g4::TILE || a->N % g4::TILE || a->K % g4::BK || a->K < 3 * g4::BK) return false;
+  if (!a->a_kmajor && a->b_kmajor) return false;  // layouts used: TT, TN, NN
+  if (((uintptr_t)a->A | (uintptr_t)a->B | (uintptr_t)a->C) % 16) return false;
+  if (a->lda % 8 || a->ldb % 8) return false;
+  if (a->ldc % (a->c_dtype == NSTL_F32 ? 4 : 8)) return false;
+  // operand extents for the 32-bit buffer offsets
+  const int64_t ae = a->a_kmajor ? ((int64_t)(a->M - 1) * a->lda + a->K) * 2 : ((int64_t)(a->K - 1) * a->lda + a->M) * 2;
+  const int64_t be = a->b_kmajor ? ((int64_t)(a->N - 1) * a->ldb + a->K) * 2 : ((int64_t)(a->K - 1) * a->ldb + a->N) * 2;
+  return ae < (1ll << 31) && be < (1ll << 31);
+}
+
+void fill(g4::Params& q, const nstl_gemm_args* a) {
+  memset(&q, 0, sizeof(q));
+  q.A = (const char*)a->A; q.lda = a->lda;
+  q.B = (const char*)a->B; q.ldb = a->ldb;
+  q.C = (char*)a->C; q.ldc = a->ldc;
+  q.M = a->M; q.N = a->N; q.K = a->K;
+  q.alpha = a->alpha;
+  q.bias = a->bias;
+  q.thresh = nstl_drop_thresh(a->p_drop);
+  q.inv_keep = 1.0f / (1.0f - a->p_drop);
+  q.seed = a->seed;
+  q.rope_cos = a->rope_cos; q.rope_sin = a->rope_sin;
+  q.rope_T = a->rope_T; q.rope_dim = a->rope_dim; q.rope_cols = a->rope_cols;
+  q.colsum_part = a->colsum_part;
+  q.relu_mask = a->relu_mask;
+  q.sq_part = a->sq_part;
+  q.a_bytes = (uint32_t)(a->a_kmajor ? ((int64_t)(a->M - 1) * a->lda + a->K) * 2 : ((int64_t)(a->K - 1) * a->lda + a->M) * 2);
+  q.b_bytes = (uint32_t)(a->b_kmajor ? ((int64_t)(a->N - 1) * a->ldb + a->K) * 2 : ((int64_t)(a->K - 1) * a->ldb + a->N) * 2);
+  q.tiles_m = a->M / g4::TILE;
+  q.tiles_n = a->N / g4::TILE;
+}
+
+template <bool AK, bool BKM, bool GROUPED>
+void launch_em(int em, dim3 grid, hipStream_t st, const g4::GroupParams& gp) {
+  const dim3 block(g4::NT);
+  switch (em) {
+    case g4::EM_BF16: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_BF16, GROUPED>), grid, block, 0, st, gp); break;
+    case g4::EM_RELU_DROP:
+      hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_RELU_DROP, GROUPED>), grid, block, 0, st, gp);
+      break;
+    case g4::EM_ROPE: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_ROPE, GROUPED>), grid, block, 0, st, gp); break;
+    case g4::EM_DRELU: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_DRELU, GROUPED>), grid, block, 0, st, gp); break;
+    default: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_F32, GROUPED>), grid, block, 0, st, gp); break;
+  }
+}
+
+// the instantiations the step uses: forward and dX (A K-major) with every
+// epilogue; the weight gradients (NN) with f32 output, grouped or not
+int launch(int em, bool ak, bool bk, bool grouped, int G, hipStream_t st, const g4::GroupParams& gp) {
+  const int tiles = gp.tile_end[gp.n - 1];
+  const dim3 grid(tiles < G ? tiles : G);
+  if (ak && bk) {
+    if (grouped) return 0;
+    launch_em<true, true, false>(em, grid, st, gp);
+  } else if (ak && !bk) {
+    if (grouped) return 0;
+    launch_em<true, false, false>(em, grid, st, gp);
+  } else {
+    if (em != g4::EM_F32) return 0;
+    if (grouped) hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, true>), grid, dim3(g4::NT), 0, st, gp);
+    else hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false>), grid, dim3(g4::NT), 0, st, gp);
+  }
+  return 1;
+}
+
+}  // namespace
+
+namespace nstl {
+
+// One problem: *handled = 1 when the 4-wave kernel took it.
+int gemm4(const nstl_gemm_args* a, hipStream_t st, int* handled) {
+  *handled = 0;
+  if (!gemm4_env() || !g4_shape_ok(a)) return 0;
+  const int em = g4_mode(a);
+  if (!em) return 0;
+  if (!a->a_kmajor && em != g4::EM_F32) return 0;
+  const int G = cus_of_current();
+  if (G <= 0) return 0;
+  g4::GroupParams gp;
+  memset(&gp, 0, sizeof(gp));
+  fill(gp.g[0], a);
+  gp.n = 1;
+  gp.tile_end[0] = gp.g[0].tiles_m * gp.g[0].tiles_n;
+  if (!launch(em, a->a_kmajor, a->b_kmajor, false, G, st, gp)) return 0;
+  NSTL_LAUNCH_CHECK("nstl_gemm (4-wave persistent)");
+  nstl::count(NSTL_K_GEMM4);
+  nstl::count(NSTL_K_GEMM4_TILES, gp.tile_end[0]);
+  *handled = 1;
+  return 0;
+}
+
+// A group of weight-gradient problems (same layout, f32 output, beta 0).
+int gemm4_grouped(const nstl_gemm_args* args, int n, hipStream_t st, int* handled) {
+  *handled = 0;
+  if (!gemm4_env() || n < 1 || n > g4::GROUP_MAX) return 0;
+  for (int i = 0; i < n; ++i) {
+    const nstl_gemm_args* a = args + i;
+    if (!g4_shape_ok(a) || g4_mode(a) != g4::EM_F32 || a->epilogue != NSTL_EPI_NONE) return 0;
+    if (a->a_kmajor != args[0].a_kmajor || a->b_kmajor != args[0].b_kmajor) return 0;
+  }
+  const int G = cus_of_current();
+  if (G <= 0) return 0;
+  g4::GroupParams gp;
+  memset(&gp, 0, sizeof(gp));
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    fill(gp.g[i], args + i);
+    tiles += gp.g[i].tiles_m * gp.g[i].tiles_n;
+    gp.tile_end[i] = tiles;
+  }
+  gp.n = n;
+  if (!launch(g4::EM_F32, args[0].a_kmajor, args[0].b_kmajor, true, G, st, gp)) return 0;
+  NSTL_LAUNCH_CHECK("nstl_gemm_grouped (4-wave persistent)");
+  nstl::count(NSTL_K_GEMM4);
+  nstl::count(NSTL_K_GEMM4_TILES, tiles);
+  *handled = 1;
+  return 0;
+}
+
+}  // namespace nstl

@@ -242,6 +242,7 @@ class Seq2SeqEngine:
         # column-quantized once per forward.  Every other backward GEMM stays bf16.
         self.fp8_bwd = False
         self._fp8_wt = None        # weight name -> (e4m3 W^T [in, out], f32 scales [in])
+        self._fp8_wt_fresh = False  # did the current forward quantize _fp8_wt
         self._fp8_dy = {}          # M -> (e4m3 [M, D], scales [M])
         # NSTL_WT=1: the input-gradient GEMMs (dX = dY W) read a transposed bf16 copy
         # W^T [in, out] (K-major, the layout both the ring kernel and hipBLASLt run
@@ -1065,6 +1066,9 @@ class Seq2SeqEngine:
         self.p = float(self.dropout) if training else 0.0
         self._xq = {}  # e4m3 activation copies never outlive a forward
         self.await_stage("vec")  # biases and LayerNorm parameters of every stage
+        # e4m3 W2^T is quantized only by forwards run with the fp8 backward on; the
+        # backward of a forward that did not refresh it must not use an older copy
+        self._fp8_wt_fresh = bool(self.fp8 and self.fp8_bwd)
         if self.fp8:
             self.sync_pending()  # every fp8 weight is quantized up front
             self._fp8_weights()
@@ -1119,7 +1123,8 @@ class Seq2SeqEngine:
         pred = self.decode(bb, mem, T, xdec0=bb.xdec0)
         if save:
             self.generation += 1
-            self.saved = dict(bb=bb, T=T, p=self.p, seed=self.base_seed, gen=self.generation, x_src=self.x_src)
+            self.saved = dict(bb=bb, T=T, p=self.p, seed=self.base_seed, gen=self.generation, x_src=self.x_src,
+                              fp8_wt=self._fp8_wt_fresh)
         return pred[:, :self.out_dim].view(B, T, self.out_dim)
 
     # -------------------------------------------------------------- backward
@@ -1261,7 +1266,7 @@ class Seq2SeqEngine:
         dh = bb.dh if dh is None else dh
         w2 = pre + "ffn.linear2.weight"
         dyq = self._fp8_dy_bufs(dy.shape[0]) if self.fp8 and self.fp8_bwd and self._fp8_wt \
-            and w2 in self._fp8_wt else None
+            and w2 in self._fp8_wt and self.saved.get("fp8_wt", False) else None
         self._ln_bwd(s_out, st, pre + norm, bb.dres, bb.dres, dy, 1, (seed_drop, 0), bf,
                      bias_of=pre + "ffn.linear2.bias", q8=dyq)
         self._dw(dy, h, w2, 1, bf, ws, bias=False)

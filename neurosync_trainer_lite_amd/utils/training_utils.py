@@ -111,26 +111,30 @@ def train_one_epoch(epoch, model, dataloader, criterion, optimizer, device, clip
         gradient_norms.append(norm_v)
         epoch_loss += loss_v
 
-    for batch_idx, (src, trg) in enumerate(dataloader):
-        src, trg = src.to(device, non_blocking=True), trg.to(device, non_blocking=True)
-        optimizer.zero_grad()
-        current_step = batch_step + (epoch * n_batches) + batch_idx
-        loss = criterion(model(src), trg, current_step=current_step, total_steps=total_steps)
-        loss.backward()
-        norm = _step_fused(model, optimizer, clip)
-        report(pending.push(((loss.detach(), norm), (batch_idx, batch_step))))
-        batch_step += 1
-        if val_dataloader is not None and batch_idx % validation_interval == 0:
-            report(pending.flush())
-            val_iter, vl = _validation_step(model, val_iter, val_dataloader, criterion, device)
-            print(f"[Epoch {epoch} - Batch {batch_idx}] Validation Loss: {vl:.4f}")
-            val_steps.append(batch_step)
-            val_losses.append(vl)
-    report(pending.flush())
-    if fused:
-        optimizer.overlap_next_forward = False
-        optimizer.trust_backward_norm = False
-        optimizer._sync()
+    try:
+        for batch_idx, (src, trg) in enumerate(dataloader):
+            src, trg = src.to(device, non_blocking=True), trg.to(device, non_blocking=True)
+            optimizer.zero_grad()
+            current_step = batch_step + (epoch * n_batches) + batch_idx
+            loss = criterion(model(src), trg, current_step=current_step, total_steps=total_steps)
+            loss.backward()
+            norm = _step_fused(model, optimizer, clip)
+            report(pending.push(((loss.detach(), norm), (batch_idx, batch_step))))
+            batch_step += 1
+            if val_dataloader is not None and batch_idx % validation_interval == 0:
+                report(pending.flush())
+                val_iter, vl = _validation_step(model, val_iter, val_dataloader, criterion, device)
+                print(f"[Epoch {epoch} - Batch {batch_idx}] Validation Loss: {vl:.4f}")
+                val_steps.append(batch_step)
+                val_losses.append(vl)
+        report(pending.flush())
+    finally:
+        # reset on every exit, exceptions included: a caller that catches one and
+        # then writes p.grad outside autograd must not clip with a stale norm
+        if fused:
+            optimizer.overlap_next_forward = False
+            optimizer.trust_backward_norm = False
+            optimizer._sync()
     print_epoch_summary(epoch, total_epochs, epoch_loss, n_batches, time.time() - start_time)
     save_loss_plot(epoch, train_steps, train_losses, val_steps, val_losses, save_dir="dataset/validation_plots/loss")
     save_gradient_norm_plot(epoch, gradient_norms, save_dir="dataset/validation_plots/gradient_norms")

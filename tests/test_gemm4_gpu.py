@@ -1,0 +1,225 @@
+"""The 4-wave persistent GEMM (csrc/gemm4.h) against the 8-wave ring kernel and
+float64, through nstl_gemm / nstl_gemm_grouped.
+
+Both kernels accumulate k in the same order (one 16x16x32 MFMA per 32-deep k
+slice, slices in order), so their f32 accumulators agree bit for bit and every
+epilogue that does the same elementwise math gives bit-identical bf16 outputs.
+The ReLU keep bits must match word for word: the forward writes them in the
+ring kernel's layout and the dReLU epilogue of either kernel (or the fp8 one)
+reads them.  Column sums and sums of squares are formed in a different order
+and are held to f32 rounding.  NSTL_GEMM4=0 (read per call) selects the ring
+kernel for the reference run.
+"""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from neurosync_trainer_lite_amd import _hip as K
+    from neurosync_trainer_lite_amd.engine import rotation_tables
+
+DEV = "cuda:0"
+bf = torch.bfloat16
+
+
+def rnd(*shape, dtype=torch.float32, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g, dtype=torch.float64) * scale).to(dtype).to(DEV)
+
+
+def f64(t):
+    return t.detach().double().cpu()
+
+
+def rel_err(got, ref):
+    got, ref = f64(got), f64(ref)
+    return (got - ref).abs().max().item() / (ref.abs().max().item() + 1e-30)
+
+
+def both(monkeypatch, fn):
+    """fn() under the 4-wave kernel and under the ring kernel; the launch counts of
+    the first run prove which kernel ran."""
+    monkeypatch.setenv("NSTL_GEMM4", "1")
+    K.kernel_counts_reset()
+    a = fn()
+    torch.cuda.synchronize()
+    c = K.kernel_counts()
+    monkeypatch.setenv("NSTL_GEMM4", "0")
+    b = fn()
+    torch.cuda.synchronize()
+    monkeypatch.delenv("NSTL_GEMM4")
+    return a, b, c
+
+
+# shapes: one round of 256^2 tiles and several (the persistent tile loop and the
+# cross-tile prefetch), K-major and MN-major B
+SHAPES = [(1024, 1024, 256), (2048, 3072, 512), (8192, 2048, 320)]
+
+
+@pytest.mark.parametrize("M,N,Kd", SHAPES)
+@pytest.mark.parametrize("bkm", [True, False])
+def test_gemm4_bias_matches_ring_bitwise(monkeypatch, M, N, Kd, bkm):
+    X = rnd(M, Kd, dtype=bf, seed=1)
+    W = rnd(N, Kd, dtype=bf, scale=0.05, seed=2) if bkm else rnd(Kd, N, dtype=bf, scale=0.05, seed=2)
+    b = rnd(N, seed=3)
+
+    def run():
+        C = torch.empty(M, N, dtype=bf, device=DEV)
+        K.gemm(X, W, C, M, N, Kd, a_kmajor=True, b_kmajor=bkm, epilogue=K.EPI_BIAS, bias=b)
+        return C
+
+    c4, cr, cnt = both(monkeypatch, run)
+    assert cnt["gemm4"] == 1 and cnt["gemm4_tiles"] == (M // 256) * (N // 256), cnt
+    assert torch.equal(c4, cr)
+    ref = (f64(X) @ (f64(W).T if bkm else f64(W))) + f64(b)
+    assert rel_err(c4, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,Kd", [(2048, 4096, 256), (8192, 1024, 512)])
+def test_gemm4_relu_dropout_mask_matches_ring(monkeypatch, M, N, Kd):
+    """ReLU + dropout: identical outputs and identical keep&positive words."""
+    X, W, b = rnd(M, Kd, dtype=bf, seed=11), rnd(N, Kd, dtype=bf, scale=0.05, seed=12), rnd(N, seed=13)
+    kw = dict(epilogue=K.EPI_BIAS_RELU_DROP, bias=b, p_drop=0.3, seed=77)
+    words = K.gemm_relu_mask_words(X, W, torch.empty(M, N, dtype=bf, device=DEV), M, N, Kd, **kw)
+    assert words == (M // 64) * 8 * (N // 8)
+
+    def run():
+        C = torch.empty(M, N, dtype=bf, device=DEV)
+        mask = torch.full((words,), -1, dtype=torch.int64, device=DEV)
+        K.gemm(X, W, C, M, N, Kd, relu_mask=mask, **kw)
+        return C, mask
+
+    (c4, m4), (cr, mr), cnt = both(monkeypatch, run)
+    assert cnt["gemm4"] == 1, cnt
+    assert torch.equal(c4, cr)
+    assert torch.equal(m4, mr)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(2048, 1024, 512), (4096, 4096, 256)])
+def test_gemm4_drelu_mask_colsum_matches_ring(monkeypatch, M, N, Kd):
+    """dReLU from the keep bits (+ column sums of the stored dh): outputs bitwise,
+    column sums to f32 rounding, both against each other and float64."""
+    # keep bits from a forward of the same shape (written by the ring kernel)
+    X, W1, b1 = rnd(M, 128, dtype=bf, seed=21), rnd(N, 128, dtype=bf, seed=22), rnd(N, seed=23)
+    fw = dict(epilogue=K.EPI_BIAS_RELU_DROP, bias=b1, p_drop=0.3, seed=5)
+    h = torch.empty(M, N, dtype=bf, device=DEV)
+    words = K.gemm_relu_mask_words(X, W1, h, M, N, 128, **fw)
+    mask = torch.zeros(words, dtype=torch.int64, device=DEV)
+    K.gemm(X, W1, h, M, N, 128, relu_mask=mask, **fw)
+    dY, W2 = rnd(M, Kd, dtype=bf, seed=24), rnd(Kd, N, dtype=bf, scale=0.05, seed=25)
+    bw = dict(a_kmajor=True, b_kmajor=False, epilogue=K.EPI_DRELU_DROP, aux=h, ld_aux=N, p_drop=0.3, relu_mask=mask)
+    rows = K.gemm_colsum_rows(dY, W2, h, M, N, Kd, **bw)
+    assert rows == M // 128
+
+    def run():
+        d = torch.empty(M, N, dtype=bf, device=DEV)
+        part = torch.empty(rows, N, dtype=torch.float32, device=DEV)
+        K.gemm(dY, W2, d, M, N, Kd, colsum_part=part, **bw)
+        return d, part
+
+    (d4, p4), (dr, pr), cnt = both(monkeypatch, run)
+    assert cnt["gemm4"] == 1, cnt
+    assert torch.equal(d4, dr)
+    assert rel_err(p4.sum(0), f64(d4).sum(0)) < 1e-5
+    assert rel_err(p4, pr) < 1e-5
+    ref = (f64(dY) @ f64(W2)) * (f64(h) > 0).double() / 0.7
+    assert rel_err(d4, ref) < 1e-2
+
+
+@pytest.mark.parametrize("T,rope_cols", [(128, 2048), (64, 1024)])
+def test_gemm4_rope_matches_ring(monkeypatch, T, rope_cols):
+    """q|k|v + RoPE (the tables staged in LDS): bitwise against the ring kernel
+    (which reads them from global memory)."""
+    M, N, Kd = 4096, 3072, 256
+    X, W, b = rnd(M, Kd, dtype=bf, seed=31), rnd(N, Kd, dtype=bf, scale=0.05, seed=32), rnd(N, seed=33)
+    cs, sn = rotation_tables(T, 64, DEV)
+
+    def run():
+        C = torch.empty(M, N, dtype=bf, device=DEV)
+        K.gemm(X, W, C, M, N, Kd, epilogue=K.EPI_BIAS_ROPE, bias=b, rope=(cs, sn, T, 64), rope_cols=rope_cols)
+        return C
+
+    c4, cr, cnt = both(monkeypatch, run)
+    assert cnt["gemm4"] == 1, cnt
+    assert torch.equal(c4, cr)
+
+
+def test_gemm4_rope_table_past_lds_stays_on_ring(monkeypatch):
+    """T * rope_dim * 4 > 32 KB (C5's T = 256): the ring kernel runs it."""
+    M, N, Kd, T = 2048, 1024, 256, 256
+    X, W, b = rnd(M, Kd, dtype=bf, seed=34), rnd(N, Kd, dtype=bf, scale=0.05, seed=35), rnd(N, seed=36)
+    cs, sn = rotation_tables(T, 64, DEV)
+    C = torch.empty(M, N, dtype=bf, device=DEV)
+    K.kernel_counts_reset()
+    K.gemm(X, W, C, M, N, Kd, epilogue=K.EPI_BIAS_ROPE, bias=b, rope=(cs, sn, T, 64), rope_cols=N)
+    torch.cuda.synchronize()
+    c = K.kernel_counts()
+    assert c["gemm4"] == 0 and c["gemm_ring"] == 1, c
+
+
+@pytest.mark.parametrize("Mt", [1024, 4096])
+def test_gemm4_grouped_dw_sq_partials(monkeypatch, Mt):
+    """Grouped weight gradients (NN, f32 out, beta 0): every problem bitwise against
+    the ring kernel's grouped launch; the sum-of-squares partials (4 per tile here,
+    8 there) agree in total."""
+    shapes = [(1024, 512), (256, 1024), (512, 768), (768, 256)]
+    ins = [(rnd(Mt, n, dtype=bf, seed=40 + i), rnd(Mt, k, dtype=bf, seed=50 + i)) for i, (n, k) in enumerate(shapes)]
+    nt = sum((n // 256) * (k // 256) for n, k in shapes)
+
+    def run():
+        probs, outs = [], []
+        sq = torch.full((nt * 8,), float("nan"), dtype=torch.float32, device=DEV)
+        used = 0
+        for (dY, X), (n, k) in zip(ins, shapes):
+            G = torch.empty(n, k, dtype=torch.float32, device=DEV)
+            t = (n // 256) * (k // 256) * 8
+            probs.append((dY, X, G, n, k, Mt, dict(a_kmajor=False, b_kmajor=False, beta=0.0, sq_part=sq[used:used + t])))
+            used += t
+            outs.append(G)
+        K.gemm_grouped(probs)
+        return outs, sq
+
+    (o4, s4), (orr, sr), cnt = both(monkeypatch, run)
+    assert cnt["gemm4"] == 1 and cnt["gemm_group"] == 0, cnt
+    for a, b_, (n, k), (dY, X) in zip(o4, orr, shapes, ins):
+        assert torch.equal(a, b_), (n, k)
+        assert rel_err(a, f64(dY).T @ f64(X)) < 1e-5
+    assert not torch.isnan(s4).any()
+    tot = sum(float((g.double() ** 2).sum()) for g in o4)
+    assert abs(float(s4.double().sum()) - tot) < 1e-5 * tot
+    assert abs(float(s4.double().sum()) - float(sr.double().sum())) < 1e-5 * tot
+
+
+def test_gemm4_f32_out_and_alpha(monkeypatch):
+    """f32 output, alpha != 1, MN-major B (a dX into a fresh f32 buffer)."""
+    M, N, Kd = 4096, 2048, 768
+    dY, W = rnd(M, Kd, dtype=bf, seed=61), rnd(Kd, N, dtype=bf, scale=0.05, seed=62)
+
+    def run():
+        C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+        K.gemm(dY, W, C, M, N, Kd, a_kmajor=True, b_kmajor=False, alpha=0.5)
+        return C
+
+    c4, cr, cnt = both(monkeypatch, run)
+    assert cnt["gemm4"] == 1, cnt
+    assert torch.equal(c4, cr)
+    assert rel_err(c4, 0.5 * f64(dY) @ f64(W)) < 2e-6
+
+
+def test_gemm4_stress_many_rounds():
+    """16 rounds of tiles per workgroup on a K just above the cross-tile minimum
+    (nk = 3: the next tile's stages are staged from the tile's second step on),
+    checked against float64 on every row."""
+    M, N, Kd = 16384, 4096, 192
+    X, W = rnd(M, Kd, dtype=bf, seed=71), rnd(N, Kd, dtype=bf, scale=0.05, seed=72)
+    C = torch.empty(M, N, dtype=bf, device=DEV)
+    K.kernel_counts_reset()
+    K.gemm(X, W, C, M, N, Kd)
+    torch.cuda.synchronize()
+    assert K.kernel_counts()["gemm4"] == 1
+    ref = (X.double() @ W.double().T)
+    err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err

@@ -136,14 +136,13 @@ def test_gemm_relu_dropout_and_backward(dt):
 
 
 @pytest.mark.parametrize("case", ["fwd_bias", "dx_bf16", "dx_f32_beta1", "fwd_f32"])
-def test_gemm_plain_on_hipblaslt(case):
-    """Plain bf16-output GEMMs (no fused epilogue beyond a bias, beta 0) run on
-    hipBLASLt through nstl_gemm (NSTL_GEMM_LT, default on): the launch counter sees
-    them, and the results match the f64 product in both layouts nstl_gemm maps onto
-    the library's column-major convention (K-major B with bias; MN-major B).  f32
-    output (beta 0 or 1) stays on the ring kernel (the library measured slower)."""
-    if os.environ.get("NSTL_GEMM_LT") == "0":
-        pytest.skip("hipBLASLt path off")
+def test_gemm4_plain(case):
+    """Plain GEMMs on full 256^2 tiles run on the 4-wave persistent kernel
+    (csrc/gemm4.h) through nstl_gemm: the launch counter sees them, and the results
+    match the f64 product for K-major and MN-major B, bf16 (with bias) and f32
+    output.  f32 output with beta != 0 stays on the ring kernel."""
+    if os.environ.get("NSTL_GEMM4") == "0":
+        pytest.skip("4-wave kernel off")
     dt, M, N, Kd = torch.bfloat16, 4096, 1024 + 256, 1024 + 64
     b = rnd(N, seed=503)
     K.kernel_counts_reset()
@@ -166,21 +165,21 @@ def test_gemm_plain_on_hipblaslt(case):
             ref = f64(C0) + f64(dY) @ f64(W)
     torch.cuda.synchronize()
     c = K.kernel_counts()
-    if C.dtype == dt:
-        assert c["gemm_lt"] == 1 and c["gemm_ring"] == 0, c
+    if case != "dx_f32_beta1":
+        assert c["gemm4"] == 1 and c["gemm4_tiles"] == (M // 256) * (N // 256) and c["gemm_ring"] == 0, c
     else:
-        assert c["gemm_lt"] == 0 and c["gemm_ring"] == 1, c
-    check(C, ref, 1e-2 if C.dtype == dt else 1e-4, "hipBLASLt " + case)
+        assert c["gemm4"] == 0 and c["gemm_ring"] == 1, c
+    check(C, ref, 1e-2 if C.dtype == dt else 1e-4, "gemm4 " + case)
 
 
-@pytest.mark.parametrize("case", ["k_not_64", "few_tiles", "misaligned_c"])
-def test_gemm_plain_outside_hipblaslt_stays_native(case):
-    """A plain bf16 GEMM that hipBLASLt's eligibility rule turns away (K not a
-    multiple of 64, fewer than 32 tiles of 256^2, a C pointer off 16-byte
-    alignment) runs on the hand-written kernels, with the same result."""
+@pytest.mark.parametrize("case", ["k_not_64", "partial_tile", "misaligned_c", "few_tiles"])
+def test_gemm_outside_gemm4(case):
+    """A GEMM the 4-wave kernel turns away (K not a multiple of 64, a partial 256^2
+    tile, a C pointer off 16-byte alignment) runs on the ring / 128 kernels with the
+    same result; a small full-tile problem (16 tiles) runs on the 4-wave kernel."""
     dt = torch.bfloat16
-    M, N, Kd = {"k_not_64": (4096, 2048, 1000), "few_tiles": (1024, 1024, 1024),
-                "misaligned_c": (4096, 2048, 1024)}[case]
+    M, N, Kd = {"k_not_64": (4096, 2048, 1000), "partial_tile": (4096 + 128, 2048, 1024),
+                "misaligned_c": (4096, 2048, 1024), "few_tiles": (1024, 1024, 1024)}[case]
     X, W = rnd(M, Kd, dtype=dt, seed=511), rnd(N, Kd, dtype=dt, scale=0.05, seed=512)
     if case == "misaligned_c":
         buf = torch.empty(M * N + 8, dtype=dt, device=DEV)
@@ -191,8 +190,11 @@ def test_gemm_plain_outside_hipblaslt_stays_native(case):
     K.gemm(X, W, C, M, N, Kd)
     torch.cuda.synchronize()
     c = K.kernel_counts()
-    assert c["gemm_lt"] == 0 and c["gemm_ring"] + c["gemm128"] == 1, c
-    check(C, f64(X) @ f64(W).T, 1e-2, "native " + case)
+    if case == "few_tiles":
+        assert c["gemm4"] == 1 and c["gemm_ring"] + c["gemm128"] == 0, c
+    else:
+        assert c["gemm4"] == 0 and c["gemm_ring"] + c["gemm128"] == 1, c
+    check(C, f64(X) @ f64(W).T, 1e-2, "outside gemm4 " + case)
 
 
 def test_gemm_rejects_bad_args():

@@ -136,11 +136,14 @@ def test_bf16_production_step_matches_oracle(problem):
     params, src, trg, o_loss, o_norm, o_pred, o_grads = problem
     pred, loss, norm, grads, c = run_step(params, src, trg, amp=True)
     # the kernels the 228M bench runs
-    # hand-written ring GEMMs for every fused epilogue; the plain bf16 ones on hipBLASLt
-    # (NSTL_GEMM_LT, the library's tuned kernels) unless switched off
-    assert c["gemm_ring"] + c["gemm_lt"] >= 16 * L, c
-    assert c["gemm_ring"] >= 7 * L, c  # q|k|v+RoPE, FFN1 ReLU-dropout, dReLU, cross k|v+RoPE per layer pair
-    assert c["gemm_group"] == L + L // 4 and c["gemm_group_tiles"] == L * 256 + (L // 4) * 768, c
+    # every full-tile GEMM on the 4-wave persistent kernel (plain, bias, q|k|v+RoPE,
+    # FFN1 ReLU-dropout, dReLU, the grouped weight gradients: one launch per decoder
+    # layer, one per 4 encoder layers); the ring kernel keeps the f32 beta-1 dX
+    # (residual accumulation) and the memory gradient
+    n_grouped = L + L // 4
+    assert c["gemm4"] >= 16 * L + n_grouped, c
+    assert c["gemm4_tiles"] >= L * 256 + (L // 4) * 768, c
+    assert c["gemm_group"] == 0, c
     assert c["attn_fwd"] == 3 * L and c["attn_bwd_fused"] == 3 * L, c
     assert c["attn_bwd_split"] == 0 and c["attn_fwd_generic"] == 0 and c["attn_bwd_generic"] == 0, c
     assert c["gemm_splitk_reduce"] <= 2, c  # only the 61-column head's weight gradient may split
@@ -158,7 +161,7 @@ def test_bf16_production_step_matches_oracle(problem):
 def test_fp32_production_step_matches_oracle(problem):
     params, src, trg, o_loss, o_norm, o_pred, o_grads = problem
     pred, loss, norm, grads, c = run_step(params, src, trg, amp=False)
-    assert c["gemm_ring"] == 0 and c["gemm_lt"] == 0 and c["gemm128"] > 0, c  # fp32 parity mode: the 128 kernel
+    assert c["gemm_ring"] == 0 and c["gemm4"] == 0 and c["gemm128"] > 0, c  # fp32 parity mode: the 128 kernel
     assert c["attn_fwd"] == 3 * L and c["attn_bwd_split"] == 3 * L, c
     assert rel(pred, o_pred) < 1e-4
     assert ((pred.double() - o_pred.double()) ** 2).mean().item() < 1e-3
@@ -257,7 +260,7 @@ def test_bf16_full_depth_step_matches_oracle():
     Lf = 8
     params, src, trg, o_loss, o_norm, o_pred, o_grads = make_problem(Lf, 81, 1.0)
     pred, loss, norm, grads, c = run_step(params, src, trg, amp=True, n_layers=Lf)
-    assert c["gemm_group"] == Lf + Lf // 4, c
+    assert c["gemm_group"] == 0 and c["gemm4"] >= 16 * Lf + Lf + Lf // 4, c
     mse = ((pred.double() - o_pred.double()) ** 2).mean().item()
     assert rel(pred, o_pred) < 3e-2 and mse < 1e-3, (rel(pred, o_pred), mse)
     assert abs(loss - o_loss.item()) < 2e-2 * abs(o_loss.item())

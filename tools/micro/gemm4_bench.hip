@@ -1,0 +1,205 @@
+// Microbenchmark + check of the 4-wave 256^2 GEMM (csrc/gemm4.h) on the 228M
+// step's shapes.  hipcc -O3 --offload-arch=gfx950 -o tools/micro/gemm4_bench \
+//   tools/micro/gemm4_bench.hip ; run on the GPU box.
+// Each shape: max |C - ref| / max |ref| against an f32 naive GEMM on every 7th
+// row, then the median of 20 timed launches.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <vector>
+
+#include "../../neurosync_trainer_lite_amd/csrc/gemm4.h"
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    hipError_t e = (x);                                                          \
+    if (e != hipSuccess) {                                                       \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      exit(1);                                                                   \
+    }                                                                            \
+  } while (0)
+
+__global__ void ref_gemm(const bf16* A, int64_t lda, const bf16* B, int64_t ldb, int bkm, float* C, int M, int N,
+                         int K, int rstep) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.y * rstep;
+  if (j >= N || i >= M) return;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float b = bkm ? (float)B[(int64_t)j * ldb + k] : (float)B[(int64_t)k * ldb + j];
+    s += (float)A[(int64_t)i * lda + k] * b;
+  }
+  C[(int64_t)blockIdx.y * N + j] = s;
+}
+
+__global__ void fill(bf16* x, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    x[i] = (bf16)(((float)(h & 0xFFFF) / 65536.f - 0.5f) * 0.2f);
+  }
+}
+
+template <bool BKM, int DBG = 0>
+void launch(const g4::Params& p, hipStream_t st) {
+  static int G = 0;
+  if (!G) {
+    hipDeviceProp_t prop;
+    hipGetDeviceProperties(&prop, 0);
+    G = getenv("G4_ONESHOT") ? 1 << 30 : prop.multiProcessorCount;
+  }
+  g4::GroupParams gp{};
+  gp.g[0] = p;
+  gp.g[0].tiles_m = p.M / 256;
+  gp.g[0].tiles_n = p.N / 256;
+  gp.n = 1;
+  gp.tile_end[0] = gp.g[0].tiles_m * gp.g[0].tiles_n;
+  const int grid = std::min(G, gp.tile_end[0]);
+  hipLaunchKernelGGL((g4::gemm4_kernel<true, BKM, g4::EM_BF16, false, DBG>), dim3(grid), dim3(g4::NT), 0, st, gp);
+}
+typedef void (*LaunchFn)(const g4::Params&, hipStream_t);
+
+// the bf16 direct epilogue's store pattern alone (one 256^2 tile per workgroup)
+__global__ __launch_bounds__(256, 1) void store_tile(bf16* C, int N, int ldc) {
+  const int nt_n = N / 256;
+  const int tm = blockIdx.x / nt_n, tn = blockIdx.x % nt_n;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, c = lane & 15, odd = g & 1;
+  bf16* cbase = C + (int64_t)(tm * 256 + wm * 128 + c) * ldc + tn * 256 + wn * 128;
+  const uint4 v = make_uint4(lane, wave, tm, tn);
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int bp = 0; bp < 8; bp += 2) *(uint4*)(cbase + (int64_t)(16 * a) * ldc + 16 * (bp + odd) + 4 * (g - odd)) = v;
+}
+
+int main(int argc, char** argv) {
+  struct Shape { const char* name; int M, N, K, bkm; };
+  const Shape shapes[] = {
+      {"fwd out   16384x1024x1024", 16384, 1024, 1024, 1},
+      {"fwd ffn2  16384x1024x4096", 16384, 1024, 4096, 1},
+      {"fwd ffn1  16384x4096x1024", 16384, 4096, 1024, 1},
+      {"fwd qkv   16384x3072x1024", 16384, 3072, 1024, 1},
+      {"dX  out   16384x1024x1024", 16384, 1024, 1024, 0},
+      {"dX  ffn2  16384x1024x4096", 16384, 1024, 4096, 0},
+      {"dX  ffn1  16384x4096x1024", 16384, 4096, 1024, 0},
+      {"sq  4096^3", 4096, 4096, 4096, 1},
+  };
+  const int reps = 20;
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  const int64_t maxA = 16384LL * 4096, maxB = 4096LL * 4096, maxC = 16384LL * 4096;
+  bf16 *A, *B, *C;
+  float* R;
+  CK(hipMalloc(&A, maxA * 2));
+  CK(hipMalloc(&B, maxB * 2));
+  CK(hipMalloc(&C, maxC * 2));
+  CK(hipMalloc(&R, maxC * 4));
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, st, A, maxA, 1u);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, st, B, maxB, 2u);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (const Shape& s : shapes) {
+    g4::Params p{};
+    p.A = (const char*)A; p.lda = s.K;
+    p.B = (const char*)B; p.ldb = s.bkm ? s.K : s.N;
+    p.C = (char*)C; p.ldc = s.N;
+    p.M = s.M; p.N = s.N; p.K = s.K;
+    p.alpha = 1.f; p.bias = nullptr;
+    p.a_bytes = (uint32_t)((int64_t)s.M * s.K * 2);
+    p.b_bytes = (uint32_t)((int64_t)s.N * s.K * 2);
+    auto run = [&]() { if (s.bkm) launch<true>(p, st); else launch<false>(p, st); };
+    run();
+    CK(hipStreamSynchronize(st));
+    const int rstep = 7, nr = (s.M + rstep - 1) / rstep;
+    hipLaunchKernelGGL(ref_gemm, dim3((s.N + 255) / 256, nr), dim3(256), 0, st, A, (int64_t)s.K, B, p.ldb, s.bkm, R,
+                       s.M, s.N, s.K, rstep);
+    CK(hipStreamSynchronize(st));
+    std::vector<bf16> hc((size_t)s.M * s.N);
+    std::vector<float> hr((size_t)nr * s.N);
+    CK(hipMemcpy(hc.data(), C, hc.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hr.data(), R, hr.size() * 4, hipMemcpyDeviceToHost));
+    double maxd = 0, maxr = 0;
+    for (int r = 0; r < nr; ++r)
+      for (int j = 0; j < s.N; ++j) {
+        const double ref = hr[(size_t)r * s.N + j], got = (float)hc[(size_t)r * rstep * s.N + j];
+        maxd = std::max(maxd, fabs(got - ref));
+        maxr = std::max(maxr, fabs(ref));
+      }
+    for (int w = 0; w < 3; ++w) run();
+    std::vector<float> ts;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0, st));
+      run();
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ts.push_back(ms);
+    }
+    std::sort(ts.begin(), ts.end());
+    const double us = ts[reps / 2] * 1e3, fl = 2.0 * s.M * s.N * s.K;
+    printf("%-28s %8.1f us  %7.1f TF/s  err %.2e %s\n", s.name, us, fl / us * 1e-6, maxd / maxr,
+           maxd / maxr < 1e-2 ? "ok" : "BAD");
+    fflush(stdout);
+  }
+  for (int n : {1024, 4096}) {
+    const int tiles = 16384 / 256 * (n / 256);
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(store_tile, dim3(tiles), dim3(256), 0, st, C, n, n);
+    std::vector<float> ts;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0, st));
+      hipLaunchKernelGGL(store_tile, dim3(tiles), dim3(256), 0, st, C, n, n);
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ts.push_back(ms);
+    }
+    std::sort(ts.begin(), ts.end());
+    const double us = ts[reps / 2] * 1e3;
+    printf("store-only 16384x%d (%d tiles): %.1f us, %.2f TB/s\n", n, tiles, us, 16384.0 * n * 2 / us * 1e-6);
+  }
+  // ablations on two single-round shapes (timing only: results are wrong)
+  struct Abl { int dbg; LaunchFn f; const char* what; };
+  const Abl abl[] = {
+      {0, launch<true, 0>, "baseline"},
+      {1, launch<true, 1>, "no DMA in loop"},
+      {2, launch<true, 2>, "no frag reads"},
+      {3, launch<true, 3>, "no DMA, no reads"},
+      {7, launch<true, 7>, "MFMA only"},
+      {8, launch<true, 8>, "no MFMA"},
+  };
+  const Shape ash[] = {{"fwd ffn2  16384x1024x4096", 16384, 1024, 4096, 1}, {"sq  4096^3", 4096, 4096, 4096, 1}};
+  for (const Shape& s : ash) {
+    g4::Params p{};
+    p.A = (const char*)A; p.lda = s.K;
+    p.B = (const char*)B; p.ldb = s.K;
+    p.C = (char*)C; p.ldc = s.N;
+    p.M = s.M; p.N = s.N; p.K = s.K;
+    p.alpha = 1.f;
+    p.a_bytes = (uint32_t)((int64_t)s.M * s.K * 2);
+    p.b_bytes = (uint32_t)((int64_t)s.N * s.K * 2);
+    for (const Abl& a : abl) {
+      for (int w = 0; w < 3; ++w) a.f(p, st);
+      std::vector<float> ts;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0, st));
+        a.f(p, st);
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ts.push_back(ms);
+      }
+      std::sort(ts.begin(), ts.end());
+      const double us = ts[reps / 2] * 1e3, fl = 2.0 * s.M * s.N * s.K;
+      printf("  abl %-28s dbg %d %-22s %8.1f us  %7.1f TF/s\n", s.name, a.dbg, a.what, us, fl / us * 1e-6);
+      fflush(stdout);
+    }
+  }
+  return 0;
+}
