@@ -48,10 +48,20 @@ def frames_flops(W, T, D, n_attn=24):
 
 
 def _is_bf16_gemm(name):
-    # the hand-written kernels, and the hipBLASLt (Tensile "Cijk_...") kernels that
-    # nstl_gemm hands its plain bf16-output GEMMs to (NSTL_GEMM_LT): the same launches
-    # the in-run HIP-event timing of nstl_gemm sees
-    return ("gemm" in name or "Cijk_" in name) and "splitk" not in name and "f8" not in name
+    # every hand-written bf16 GEMM kernel: the same launches the in-run HIP-event
+    # timing of nstl_gemm / nstl_gemm_grouped sees
+    return "gemm" in name and "splitk" not in name and "f8" not in name
+
+
+# GEMM families for the per-family split of traffic and MFMA busy (kernel names
+# as rocprofv3 reports them, demangled)
+def _gemm_family(name):
+    if "gemm4_kernel" in name:
+        # template <AK, BKM, EM, GROUPED, DBG>: the grouped weight gradients are <false, false, 5, true
+        return "gemm4_grouped_dw" if "<false, false, 5, true" in name else "gemm4"
+    if "gemm256r" in name or "gemm256_kernel" in name:
+        return "ring"
+    return "gemm128"
 
 
 def _pmc_dispatches(d):
@@ -118,6 +128,17 @@ def measure_gemm_counters(args):
             return res
         kib[c] = sum(v) / len(v)
     res["traffic"] = round((2.0 * kib["FETCH_SIZE"] + kib["WRITE_SIZE"]) * 1024.0)
+    # the same per GEMM family (bytes per launch, mean over the family's dispatches)
+    fam = {}
+    for f in ("gemm4", "gemm4_grouped_dw", "ring", "gemm128"):
+        per = {}
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            v = [x[2][c] for x in runs[c].values() if _is_bf16_gemm(x[0]) and _gemm_family(x[0]) == f and c in x[2]]
+            per[c] = (sum(v) / len(v), len(v)) if v else None
+        if per["FETCH_SIZE"] and per["WRITE_SIZE"]:
+            fam[f] = {"traffic": round((2.0 * per["FETCH_SIZE"][0] + per["WRITE_SIZE"][0]) * 1024.0),
+                      "dispatches": per["FETCH_SIZE"][1]}
+    res["traffic_by_family"] = fam
     res["note"] = ("measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 1+1-step child run of "
                    "this workload, mean over its bf16 GEMM-family dispatches")
 
@@ -131,7 +152,9 @@ def measure_gemm_counters(args):
         return {"mfma_busy": round(mfma / (grbm / 8 * 1024), 4), "clock_ghz": round(grbm / 8 / ns, 3),
                 "dispatches": len(xs)}
     res["mfma_busy"] = {"gemm_family": busy(_is_bf16_gemm),
-                        "grouped_dw": busy(lambda n: "group_kernel" in n and _is_bf16_gemm(n)),
+                        "grouped_dw": busy(lambda n: _is_bf16_gemm(n) and _gemm_family(n) == "gemm4_grouped_dw"),
+                        "by_family": {f: busy(lambda n, f=f: _is_bf16_gemm(n) and _gemm_family(n) == f)
+                                      for f in ("gemm4", "gemm4_grouped_dw", "ring", "gemm128")},
                         "source": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, child run (1+1 steps); "
                                   "busy = MFMA cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); profiled runs "
                                   "clock a few % below un-profiled ones"}
@@ -374,9 +397,10 @@ def main():
 
     # PMC traffic passes first: child processes, started before this one touches the GPU
     traffic, traffic_src, mfma_busy = None, "skipped (--no-traffic or n>1)", None
+    counters = {}
     if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_traffic:
-        ctr = measure_gemm_counters(args)
-        traffic, traffic_src, mfma_busy = ctr["traffic"], ctr["note"], ctr["mfma_busy"]
+        counters = measure_gemm_counters(args)
+        traffic, traffic_src, mfma_busy = counters["traffic"], counters["note"], counters["mfma_busy"]
     rank, world, local = parallel.init_from_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -442,18 +466,30 @@ def main():
             return ev_pool.pop(), ev_pool.pop()
         return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
+    def launched_family():
+        # which kernel the last nstl_gemm call ran (launch counters, sampled steps only)
+        c = K.kernel_counts()
+        K.kernel_counts_reset()
+        if c["gemm4"]:
+            return "gemm4"
+        if c["gemm_ring"] or c["gemm_group"]:
+            return "ring"
+        return "gemm128" if c["gemm128"] else "other"
+
     def timed_gemm(A, B_, C, M, N, Kd, **kw):
         if not sample[0]:
             real_gemm(A, B_, C, M, N, Kd, **kw)
             return
         st = stream_of(kw.get("stream"))
         e0, e1 = take_events()
+        K.kernel_counts_reset()
         e0.record(st)
         real_gemm(A, B_, C, M, N, Kd, **kw)
         e1.record(st)
         ebytes = A.element_size()
         cbytes = C.element_size()
-        gemm_events.append((e0, e1, 2.0 * M * N * Kd, (M * Kd + N * Kd) * ebytes + M * N * cbytes, ebytes == 1, False))
+        gemm_events.append((e0, e1, 2.0 * M * N * Kd, (M * Kd + N * Kd) * ebytes + M * N * cbytes, ebytes == 1, False,
+                            launched_family()))
 
     # Timing events around every launch cost ~1.7 ms per step (228M), so they are
     # recorded in the last `--gemm-sample-steps` timed steps only.
@@ -466,12 +502,14 @@ def main():
             return
         st = stream_of(stream)
         e0, e1 = take_events()
+        K.kernel_counts_reset()
         e0.record(st)
         real_grouped(problems, stream=stream)
         e1.record(st)
         fl = sum(2.0 * M * N * Kd for _, _, _, M, N, Kd, _ in problems)
         by = sum((M * Kd + N * Kd) * A.element_size() + M * N * C.element_size() for A, _, C, M, N, Kd, _ in problems)
-        gemm_events.append((e0, e1, fl, by, False, True))
+        fam = launched_family()
+        gemm_events.append((e0, e1, fl, by, False, True, "gemm4_grouped_dw" if fam == "gemm4" else fam))
 
     K.gemm = timed_gemm
     K.gemm_grouped = timed_grouped
@@ -500,37 +538,51 @@ def main():
     # bf16 launches -> `roofline` (vs the bf16 peak); fp8 launches (--fp8) -> `roofline_fp8`
     ev16 = [e for e in gemm_events if not e[4]]
     ev8 = [e for e in gemm_events if e[4]]
-    all_ms = sum(a.elapsed_time(b) for a, b, _, _, _, _ in gemm_events)
-    gemm_ms = sum(a.elapsed_time(b) for a, b, _, _, _, _ in ev16)
-    gemm_flops = sum(f for _, _, f, _, _, _ in ev16)
-    gemm_alg_bytes = sum(x for _, _, _, x, _, _ in ev16) / max(1, len(ev16))
+    all_ms = sum(a.elapsed_time(b) for a, b, _, _, _, _, _ in gemm_events)
+    gemm_ms = sum(a.elapsed_time(b) for a, b, _, _, _, _, _ in ev16)
+    gemm_flops = sum(f for _, _, f, _, _, _, _ in ev16)
+    gemm_alg_bytes = sum(x for _, _, _, x, _, _, _ in ev16) / max(1, len(ev16))
     n_launch = len(ev16)
     fp8_roof = None
     if ev8:
-        ms8 = sum(a.elapsed_time(b) for a, b, _, _, _, _ in ev8)
-        tf8 = sum(f for _, _, f, _, _, _ in ev8) / (ms8 * 1e-3) / 1e12
+        ms8 = sum(a.elapsed_time(b) for a, b, _, _, _, _, _ in ev8)
+        tf8 = sum(f for _, _, f, _, _, _, _ in ev8) / (ms8 * 1e-3) / 1e12
         fp8_roof = {"bound": "mfma", "kernel": "gemm256f8_kernel (e4m3 operands, row scales; which GEMMs: config.fp8_scope)",
                     "achieved": round(tf8, 1), "peak": FP8_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(tf8 / FP8_DENSE_PEAK_TFLOPS, 4), "launches": len(ev8),
                     "avg_launch_us": round(ms8 * 1e3 / len(ev8), 2),
-                    "algorithmic_bytes_per_launch": round(sum(x for _, _, _, x, _, _ in ev8) / len(ev8)),
+                    "algorithmic_bytes_per_launch": round(sum(x for _, _, _, x, _, _, _ in ev8) / len(ev8)),
                     "share_of_step": round(ms8 / (max(1, min(args.steps, args.gemm_sample_steps)) * elapsed / args.steps * 1e3), 3)}
     n_sampled = max(1, min(args.steps, args.gemm_sample_steps))
     # the largest single kernel by time: the grouped weight-gradient launches
-    # (gemm256r_group_kernel), the kernel round 1's verdict priced on its own
+    # (gemm4_kernel, grouped NN form), the kernel round 1's verdict priced on its own
     evg = [e for e in ev16 if e[5]]
     dom_roof = None
     if evg:
-        msg = sum(a.elapsed_time(b) for a, b, _, _, _, _ in evg)
-        tfg = sum(f for _, _, f, _, _, _ in evg) / (msg * 1e-3) / 1e12
-        dom_roof = {"bound": "mfma", "kernel": "gemm256r_group_kernel (grouped weight gradients, f32 accumulate into "
-                                               "the gradient arena; decoder layer = 1 launch, 4 encoder layers = 1)",
+        msg = sum(a.elapsed_time(b) for a, b, _, _, _, _, _ in evg)
+        tfg = sum(f for _, _, f, _, _, _, _ in evg) / (msg * 1e-3) / 1e12
+        dom_roof = {"bound": "mfma", "kernel": "gemm4_kernel<false, false, EM_F32, grouped> (grouped weight gradients, "
+                                               "f32 into the gradient arena; decoder layer = 1 launch, 4 encoder "
+                                               "layers = 1)",
                     "achieved": round(tfg, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(tfg / BF16_DENSE_PEAK_TFLOPS, 4), "launches": len(evg),
                     "avg_launch_us": round(msg * 1e3 / len(evg), 2),
-                    "algorithmic_bytes_per_launch": round(sum(x for _, _, _, x, _, _ in evg) / len(evg)),
+                    "algorithmic_bytes_per_launch": round(sum(x for _, _, _, x, _, _, _ in evg) / len(evg)),
                     "share_of_step": round(msg / (n_sampled * elapsed / args.steps * 1e3), 3)}
     achieved_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+    # the same per kernel family (which kernel each launch ran: launch counters)
+    by_family = {}
+    for fam in ("gemm4", "gemm4_grouped_dw", "ring", "gemm128"):
+        ev = [e for e in ev16 if e[6] == fam]
+        if not ev:
+            continue
+        ms_f = sum(a.elapsed_time(b) for a, b, _, _, _, _, _ in ev)
+        tf_f = sum(f for _, _, f, _, _, _, _ in ev) / (ms_f * 1e-3) / 1e12
+        by_family[fam] = {"launches": len(ev), "achieved": round(tf_f, 1),
+                          "frac": round(tf_f / BF16_DENSE_PEAK_TFLOPS, 4),
+                          "avg_launch_us": round(ms_f * 1e3 / len(ev), 2),
+                          "algorithmic_bytes_per_launch": round(sum(x for _, _, _, x, _, _, _ in ev) / len(ev)),
+                          "share_of_step": round(ms_f / (n_sampled * elapsed / args.steps * 1e3), 3)}
     ms_step = elapsed / args.steps * 1e3
     frames = B * T * world * args.steps
     value = frames / elapsed
@@ -656,8 +708,11 @@ def main():
             "config": {"workload": "228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam)",
                        "model": "NeuroSync Seq2Seq 228M", "global_batch": B * world, "seq_len": T,
                        "frames_per_step": B * T * world, "parallelism": "dp%d" % world},
-            "roofline": {"bound": "mfma", "kernel": "nstl GEMM family (gemm256r_kernel, its grouped form, gemm_kernel; the plain bf16-output GEMMs on hipBLASLt), every launch "
-                                                    "of the last %d timed steps" % n_sampled,
+            "roofline": {"bound": "mfma", "kernel": "nstl GEMM family, all hand-written: gemm4_kernel (4-wave persistent "
+                                                    "256^2: every full-tile forward / dX / grouped dW), gemm256r_kernel "
+                                                    "(8-wave ring: f32 beta-1 dX, the memory gradient), gemm_kernel "
+                                                    "(128^2: small shapes); every launch of the last %d timed steps"
+                                                    % n_sampled,
                          "achieved": round(achieved_tf, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)",
@@ -671,6 +726,15 @@ def main():
             "step_mfma_frac": round(step_tf / BF16_DENSE_PEAK_TFLOPS, 4),
             "final_loss": round(loss_v, 4),
         }
+        fam_traffic = counters.get("traffic_by_family") or {}
+        for fam, d in by_family.items():
+            t = fam_traffic.get(fam)
+            if t:
+                d["traffic"] = t["traffic"]
+                d["traffic_vs_algorithmic"] = round(t["traffic"] / d["algorithmic_bytes_per_launch"], 3)
+            if mfma_busy is not None and mfma_busy["by_family"].get(fam):
+                d["mfma_busy"] = mfma_busy["by_family"][fam]
+        out["roofline"]["by_family"] = by_family
         if mfma_busy is not None:
             out["roofline"]["mfma_busy"] = mfma_busy["gemm_family"]
         if dom_roof is not None:

@@ -211,8 +211,9 @@ def kernel_counts():
     n = len(KERNEL_COUNT_NAMES)
     buf = (ctypes.c_int64 * n)()
     total = lib().nstl_kernel_counts(ctypes.cast(buf, _vp), n)
-    if total != n:
+    if total != n and not os.environ.get("NSTL_LIB_PATH"):
         raise RuntimeError("nstl_kernel_counts: library has %d counters, bindings %d" % (total, n))
+    # an older build loaded for an A/B (NSTL_LIB_PATH) may have fewer: the rest read 0
     return dict(zip(KERNEL_COUNT_NAMES, buf))
 
 

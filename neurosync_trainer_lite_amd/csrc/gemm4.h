@@ -127,11 +127,14 @@ NSTL_DEV void ds_b128(bf16x8& f, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
   f = __builtin_bit_cast(bf16x8, v);
 }
+// the two transpose reads of an MN-major fragment: rows 8g + q and 8g + 4 + q of
+// the image, 4 rows = 2048 bytes apart (the ImgMN<512> swizzle does not depend on
+// row bit 2), so one address serves both
 template <int OFF>
-NSTL_DEV void ds_tr2(bf16x8& f, uint32_t a0, uint32_t a1) {
+NSTL_DEV void ds_tr2(bf16x8& f, uint32_t a0) {
   i32x2_t v0, v1;
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v0) : "v"(a0), "i"(OFF));
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v1) : "v"(a1), "i"(OFF));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v1) : "v"(a0), "i"(OFF + 2048));
   const bf16x4 b0 = __builtin_bit_cast(bf16x4, v0), b1 = __builtin_bit_cast(bf16x4, v1);
   f = (bf16x8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
 }
@@ -142,7 +145,7 @@ NSTL_DEV void ds_tr2(bf16x8& f, uint32_t a0, uint32_t a1) {
 template <bool KMAJ>
 struct RdAddr {
   uint32_t k[2];
-  uint32_t t[8][2];
+  uint32_t t[8];
 };
 template <bool KMAJ>
 NSTL_DEV void rd_addr(RdAddr<KMAJ>& r, uint32_t img, int blk0, int lane) {
@@ -153,24 +156,41 @@ NSTL_DEV void rd_addr(RdAddr<KMAJ>& r, uint32_t img, int blk0, int lane) {
   } else {
     const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int byte = (blk0 + 16 * j + 4 * pp) * 2;
-      r.t[j][0] = img + ImgMN<512>::off(8 * g + q, byte);
-      r.t[j][1] = img + ImgMN<512>::off(8 * g + 4 + q, byte);
-    }
+    for (int j = 0; j < 8; ++j) r.t[j] = img + ImgMN<512>::off(8 * g + q, (blk0 + 16 * j + 4 * pp) * 2);
   }
 }
-template <bool KMAJ, int H, int J>
-NSTL_DEV void rd_frag(bf16x8& f, const RdAddr<KMAJ>& r, uint32_t so) {
-  // slot offset `so` added at the read (not hoisted: sched_barriers fence each read)
-  if constexpr (KMAJ) ds_b128<J * 2048>(f, r.k[H] + so);
-  else ds_tr2<H * 16384>(f, r.t[J][0] + so, r.t[J][1] + so);
+// Read slots of one half-step in issue order: A block 0..7, then B block 0..7; a
+// K-major block is one ds_read_b128, an MN-major block two transpose reads (sub 0,
+// 1).  Slot offsets are immediates (SO: the stage slot's byte offset).
+template <bool AK, bool BKM>
+constexpr int n_reads() { return (AK ? 8 : 16) + (BKM ? 8 : 16); }
+template <int SO, bool KMAJ, int H, int J, int SUB>
+NSTL_DEV void rd_one(bf16x8& f, const RdAddr<KMAJ>& r) {
+  if constexpr (KMAJ) {
+    i32x4_t v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(r.k[H]), "i"(SO + J * 2048));
+    f = __builtin_bit_cast(bf16x8, v);
+  } else {
+    // two transpose reads, 4 rows = 2048 bytes apart, fill the halves of f
+    i32x2_t v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(r.t[J]), "i"(SO + H * 16384 + SUB * 2048));
+    const bf16x4 b = __builtin_bit_cast(bf16x4, v);
+    if constexpr (SUB == 0) f = (bf16x8){b[0], b[1], b[2], b[3], f[4], f[5], f[6], f[7]};
+    else f = (bf16x8){f[0], f[1], f[2], f[3], b[0], b[1], b[2], b[3]};
+  }
 }
-// item J of 16: A block J (J < 8), B block J - 8
-template <bool AK, bool BKM, int H, int J>
-NSTL_DEV void rd_item(bf16x8 (&fa)[8], bf16x8 (&fb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb, uint32_t so) {
-  if constexpr (J < 8) rd_frag<AK, H, J>(fa[J], ra, so);
-  else rd_frag<BKM, H, J - 8>(fb[J - 8], rb, so);
+// read slot R of the half-step
+template <bool AK, bool BKM, int SO, int H, int R>
+NSTL_DEV void rd_slot(bf16x8 (&fa)[8], bf16x8 (&fb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb) {
+  constexpr int NA = AK ? 8 : 16;
+  if constexpr (R < NA) {
+    constexpr int J = AK ? R : R / 2, SUB = AK ? 0 : R % 2;
+    rd_one<SO, AK, H, J, SUB>(fa[J], ra);
+  } else {
+    constexpr int Q = R - NA;
+    constexpr int J = BKM ? Q : Q / 2, SUB = BKM ? 0 : Q % 2;
+    rd_one<SO, BKM, H, J, SUB>(fb[J], rb);
+  }
 }
 
 // DMA state: buffer resources and per-lane offsets (per problem), the tile's
@@ -199,37 +219,50 @@ NSTL_DEV void dma_tile(Dma& d, const Params& p, int m0, int n0) {
   d.tb = __builtin_amdgcn_readfirstlane(BKM ? (uint32_t)(n0 * p.ldb * 2) : (uint32_t)(n0 * 2));
 }
 
-NSTL_DEV void mma16z(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+// every read slot of a half-step (slot 0, h = 0): the first tile's prologue
+template <bool AK, bool BKM, int R>
+NSTL_DEV void rd_all(bf16x8 (&fa)[8], bf16x8 (&fb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb) {
+  if constexpr (R < n_reads<AK, BKM>()) {
+    rd_slot<AK, BKM, 0, 0, R>(fa, fb, ra, rb);
+    rd_all<AK, BKM, R + 1>(fa, fb, ra, rb);
+  }
 }
 
-// One half-step: 64 MFMAs on (ca, cb) (ZC: C = 0); if RD, the 16 reads into
-// (na, nb) follow MFMAs 1, 4, ..., 46; if DMA, the 16 pieces follow MFMAs 2, 6,
-// ..., 62 (A pieces to adst, B pieces to bdst, stage offsets sa / sb).  The
-// reads early and the pieces spread: tools/micro/gemm4_bench.hip measured the
-// other placements 1-7 % slower.
+// One half-step: 64 MFMAs on (ca, cb); if RD, the half-step's reads (16 to 32
+// instructions: read slots, rd_slot) into (na, nb) spread over MFMAs 1 .. 46 (read
+// slot r after MFMA 1 + 46 r / R: each transpose read gets a gap of its own as far
+// as the count allows, and the last read has 17 MFMAs to land before the closing
+// lgkmcnt(0)); if DMA, the 16 pieces follow MFMAs 2, 6, ..., 62 (A pieces to adst,
+// B pieces to bdst, stage offsets sa / sb).  RSO: the read slot's byte offset.
 // DBG (timing experiments only, wrong results): 1 no DMA, 2 no reads, 8 no MFMA.
-template <bool AK, bool BKM, bool ZC, bool RD, int RH, bool DMA, int DBG, int I = 0>
-NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 (&cb)[8], bf16x8 (&na)[8],
-                        bf16x8 (&nb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb, uint32_t so, const Dma& d,
-                        char* adst, char* bdst, uint32_t sa, uint32_t sb) {
-  if constexpr (I < 64) {
-    if constexpr (!(DBG & 8)) {
-      if constexpr (ZC) mma16z(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
-      else mma16(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
-    }
-    G4_SB();
-    if constexpr (RD && !(DBG & 2) && I % 3 == 1 && I / 3 < 16) {
-      rd_item<AK, BKM, RH, I / 3>(na, nb, ra, rb, so);
+template <bool AK, bool BKM, int RSO, int RH, int I, int R>
+NSTL_DEV void rd_after(bf16x8 (&na)[8], bf16x8 (&nb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb) {
+  constexpr int NR = n_reads<AK, BKM>();
+  if constexpr (R < NR) {
+    if constexpr (1 + (46 * R) / NR == I) {
+      rd_slot<AK, BKM, RSO, RH, R>(na, nb, ra, rb);
       G4_SB();
+      rd_after<AK, BKM, RSO, RH, I, R + 1>(na, nb, ra, rb);
+    } else if constexpr (1 + (46 * R) / NR < I) {
+      rd_after<AK, BKM, RSO, RH, I, R + 1>(na, nb, ra, rb);
     }
+  }
+}
+template <bool AK, bool BKM, bool RD, int RSO, int RH, bool DMA, int DBG, int I = 0>
+NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 (&cb)[8], bf16x8 (&na)[8],
+                        bf16x8 (&nb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb, const Dma& d, char* adst,
+                        char* bdst, uint32_t sa, uint32_t sb) {
+  if constexpr (I < 64) {
+    if constexpr (!(DBG & 8)) mma16(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
+    G4_SB();
+    if constexpr (RD && !(DBG & 2)) rd_after<AK, BKM, RSO, RH, I, 0>(na, nb, ra, rb);
     if constexpr (DMA && !(DBG & 1) && (I & 3) == 2) {
       constexpr int q = I >> 2;
       if constexpr (q < 8) dma16(d.ra, adst + q * 1024, d.va[q], d.ta + sa);
       else dma16(d.rb, bdst + (q - 8) * 1024, d.vb[q - 8], d.tb + sb);
       G4_SB();
     }
-    half_step<AK, BKM, ZC, RD, RH, DMA, DBG, I + 1>(acc, ca, cb, na, nb, ra, rb, so, d, adst, bdst, sa, sb);
+    half_step<AK, BKM, RD, RSO, RH, DMA, DBG, I + 1>(acc, ca, cb, na, nb, ra, rb, d, adst, bdst, sa, sb);
   }
 }
 
@@ -360,7 +393,8 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
     for (int a = 0; a < 8; ++a) {
       const int row = row0 + 16 * a + c;
       bf16* crow = cbase + (int64_t)(16 * a) * p.ldc;
-      const int t = EM == EM_ROPE ? row % p.rope_T : 0;
+      // position of the row (a power-of-two T, the production case: a mask)
+      const int t = EM != EM_ROPE ? 0 : ((p.rope_T & (p.rope_T - 1)) == 0 ? row & (p.rope_T - 1) : row % p.rope_T);
 #pragma unroll
       for (int bp = 0; bp < 8; bp += 2) {
         f32x4 uv[2] = {rd_acc(acc[a][bp]), rd_acc(acc[a][bp + 1])};
@@ -391,6 +425,9 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
               mbits[a >> 2][b] |= nib << (4 * (a & 3));
             }
           } else if constexpr (EM == EM_ROPE) {
+            // products rounded before the add, as the reference's f32 elementwise
+            // rotation (model.py:60-83); no FMA contraction
+#pragma clang fp contract(off)
             if (col < p.rope_cols) {
               // pairs (col, col + 1), (col + 2, col + 3): chunk (col % rope_dim) / 4
               const f32x4 cs = *(const f32x4*)(rope_lds + rope_off(t, (col % p.rope_dim) >> 2, rope_rb));
@@ -466,7 +503,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
 
 // ---------------------------------------------------------------------------
 // The persistent kernel.  Preconditions (host-checked): bf16 operands; every
-// problem's M, N multiples of 256, K a multiple of 64 with K >= 256; 16-byte
+// problem's M, N multiples of 256, K a multiple of 128 with K >= 256; 16-byte
 // aligned rows; operand extents < 2^31 bytes; EM_ROPE: T * rope_dim * 4 <=
 // ROPE_LDS and rope_dim % 4 == 0; EM_F32: beta 0.  Tiles of up to 16 problems
 // (gp.tile_end; one problem: n = 1).
@@ -498,16 +535,18 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   }
 
   // tile index -> (problem, m0, n0); XCD-aware order within each problem
-  auto locate = [&](int tt, int& prob, int& m0, int& n0) {
+  // (and the tile's index within its problem: sq_part is per problem)
+  auto locate = [&](int tt, int& prob, int& m0, int& n0, int& lt) {
     prob = 0;
     if (GROUPED)
       while (prob + 1 < gp.n && tt >= gp.tile_end[prob]) ++prob;
     const int first = prob ? gp.tile_end[prob - 1] : 0;
     const Params& q = gp.g[prob];
-    tile_coords(xcd_remap(tt - first, gp.tile_end[prob] - first), q.tiles_m, q.tiles_n, m0, n0);
+    lt = tt - first;
+    tile_coords(xcd_remap(lt, gp.tile_end[prob] - first), q.tiles_m, q.tiles_n, m0, n0);
   };
-  int prob, m0, n0;
-  locate(t, prob, m0, n0);
+  int prob, m0, n0, lt;
+  locate(t, prob, m0, n0, lt);
   Dma d;
   dma_lanes<AK, BKM>(d, gp.g[prob], wave, lane);
   dma_tile<AK, BKM>(d, gp.g[prob], m0, n0);
@@ -534,34 +573,31 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   G4_VMCNT(0);
   __builtin_amdgcn_s_barrier();
   G4_SB();
-#define G4_RD0(J) rd_item<AK, BKM, 0, J>(f0a, f0b, ra, rb, 0u)
-  G4_RD0(0); G4_RD0(1); G4_RD0(2); G4_RD0(3); G4_RD0(4); G4_RD0(5); G4_RD0(6); G4_RD0(7);
-  G4_RD0(8); G4_RD0(9); G4_RD0(10); G4_RD0(11); G4_RD0(12); G4_RD0(13); G4_RD0(14); G4_RD0(15);
-#undef G4_RD0
+  rd_all<AK, BKM, 0>(f0a, f0b, ra, rb);
   G4_LGKM0();
-  uint32_t gs = 0;  // global step counter: stage slot = gs & 1
 
-  // step: h = 0 on F0 (ZC: the tile's first), the counted wait + barrier, h = 1
-  // on F1 with the reads of the following stage into F0 and the DMA of stage
-  // `dma_stage` of the tile `dd` describes.  WAITN: how many VMEM operations may
-  // stay in flight (issued after this wave's pieces of the stage to retire).
-  auto step = [&](auto zc_c, auto waitn_c, uint32_t dma_stage, const Dma& dd) {
-    constexpr bool ZC = decltype(zc_c)::value;
+  // step on stage slot S: h = 0 on F0, the counted wait + barrier, h = 1 on F1
+  // with the reads of the following stage (slot 1 - S) into F0 and the DMA of
+  // stage `dma_stage` of the tile `dd` describes into slot S.  WAITN: how many VMEM
+  // operations may stay in flight (issued after this wave's pieces of the stage to
+  // retire).  The slot is a template constant: every LDS read takes it as an
+  // immediate offset (no address arithmetic in the loop).
+  auto step = [&](auto slot_c, auto waitn_c, uint32_t dma_stage, const Dma& dd) {
+    constexpr int S = decltype(slot_c)::value;
     constexpr int WAITN = decltype(waitn_c)::value;
-    const uint32_t so = (gs & 1) * OPS;
-    half_step<AK, BKM, ZC, true, 1, false, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, so, dd, adst0, bdst0, 0, 0);
+    half_step<AK, BKM, true, S * OPS, 1, false, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, dd, adst0, bdst0, 0, 0);
     G4_LGKM0();
     if constexpr (WAITN == 0) G4_VMCNT(0);
     else if constexpr (WAITN == 32) G4_VMCNT(32);
     else G4_VMCNT(63);
     __builtin_amdgcn_s_barrier();
     G4_SB();
-    half_step<AK, BKM, false, true, 0, true, DBG>(acc, f1a, f1b, f0a, f0b, ra, rb, so ^ OPS, dd, adst0 + so,
-                                                  bdst0 + so, dma_stage * dd.a_kb, dma_stage * dd.b_kb);
+    half_step<AK, BKM, true, (1 - S) * OPS, 0, true, DBG>(acc, f1a, f1b, f0a, f0b, ra, rb, dd, adst0 + S * OPS,
+                                                         bdst0 + S * OPS, dma_stage * dd.a_kb, dma_stage * dd.b_kb);
     G4_LGKM0();
-    ++gs;
   };
-  using NZ = std::false_type;
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
   using W0 = std::integral_constant<int, 0>;
   // an epilogue issues at least 32 (bf16: 16 B per lane and 8 columns) or 64 (f32)
   // stores after the next tile's stage 1 pieces
@@ -574,26 +610,30 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     const bool has_next = tn < T;
     // the next tile (after the workgroup's last: itself again, a harmless refill
     // of slots nobody reads afterwards, drained before exit)
-    int nprob = prob, nm0 = m0, nn0 = n0;
-    if (has_next) locate(tn, nprob, nm0, nn0);
-    // step kt stages stage kt + 2: this tile's while kt + 2 < nk, then the next
-    // tile's 0 and 1 (one loop body: more step sites make the register
-    // allocator give the fragment sets different registers per site, and spill)
-    step(NZ{}, WE{}, 2u, d);
-    for (int kt = 1; kt < nk; ++kt) {
-      if (kt == nk - 2) {
-        if (GROUPED && nprob != prob) dma_lanes<AK, BKM>(d, gp.g[nprob], wave, lane);
-        dma_tile<AK, BKM>(d, gp.g[nprob], nm0, nn0);
+    int nprob = prob, nm0 = m0, nn0 = n0, nlt = lt;
+    if (has_next) locate(tn, nprob, nm0, nn0, nlt);
+    // step kt (slot kt & 1: nk is even, so every tile starts on slot 0) stages
+    // stage kt + 2: this tile's while kt + 2 < nk, then the next tile's 0 and 1.
+    // Three step sites (more make the register allocator give the fragment sets
+    // different registers per site, and spill).
+    step(S0{}, WE{}, 2u, d);
+    for (int kt = 1; kt < nk; kt += 2) {
+      step(S1{}, W0{}, (uint32_t)(kt + 2 < nk ? kt + 2 : kt + 2 - nk), d);
+      if (kt + 1 < nk) {
+        if (kt + 1 == nk - 2) {
+          if (GROUPED && nprob != prob) dma_lanes<AK, BKM>(d, gp.g[nprob], wave, lane);
+          dma_tile<AK, BKM>(d, gp.g[nprob], nm0, nn0);
+        }
+        step(S0{}, W0{}, (uint32_t)(kt + 3 < nk ? kt + 3 : kt + 3 - nk), d);
       }
-      const int ds = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
-      step(NZ{}, W0{}, (uint32_t)ds, d);
     }
-    epilogue<EM>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, t, rope_lds);
+    epilogue<EM>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds);
     if (!has_next) break;
     t = tn;
     prob = nprob;
     m0 = nm0;
     n0 = nn0;
+    lt = nlt;
   }
   G4_VMCNT(0);  // the refill must land before the workgroup's LDS is released
 }

@@ -41,6 +41,11 @@ int g4_mode(const nstl_gemm_args* a) {
   if (a->dtype != NSTL_BF16 || a->split_k > 1 || a->beta != 0.f || (a->sq_part != nullptr && a->c_dtype != NSTL_F32))
     return 0;
   const bool bf_out = a->c_dtype == NSTL_BF16;
+  // side outputs only with the epilogue that produces them (anything else goes on
+  // to nstl_gemm's own argument checks)
+  if (a->colsum_part != nullptr && a->epilogue != NSTL_EPI_DRELU_DROP) return 0;
+  if (a->relu_mask != nullptr && a->epilogue != NSTL_EPI_BIAS_RELU_DROP && a->epilogue != NSTL_EPI_DRELU_DROP)
+    return 0;
   switch (a->epilogue) {
     case NSTL_EPI_NONE:
       return bf_out ? g4::EM_BF16 : g4::EM_F32;
@@ -61,7 +66,8 @@ int g4_mode(const nstl_gemm_args* a) {
 }
 
 bool g4_shape_ok(const nstl_gemm_args* a) {
-  if (a->M % g4::TILE || a->N % g4::TILE || a->K % g4::BK || a->K < 3 * g4::BK) return false;
+  // K: whole pairs of 64-deep stages (every tile starts on stage slot 0), at least two pairs
+  if (a->M % g4::TILE || a->N % g4::TILE || a->K % (2 * g4::BK) || a->K < 4 * g4::BK) return false;
   if (!a->a_kmajor && a->b_kmajor) return false;  // layouts used: TT, TN, NN
   if (((uintptr_t)a->A | (uintptr_t)a->B | (uintptr_t)a->C) % 16) return false;
   if (a->lda % 8 || a->ldb % 8) return false;

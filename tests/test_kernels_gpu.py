@@ -143,7 +143,7 @@ def test_gemm4_plain(case):
     output.  f32 output with beta != 0 stays on the ring kernel."""
     if os.environ.get("NSTL_GEMM4") == "0":
         pytest.skip("4-wave kernel off")
-    dt, M, N, Kd = torch.bfloat16, 4096, 1024 + 256, 1024 + 64
+    dt, M, N, Kd = torch.bfloat16, 4096, 1024 + 256, 1024 + 128
     b = rnd(N, seed=503)
     K.kernel_counts_reset()
     if case in ("fwd_bias", "fwd_f32"):

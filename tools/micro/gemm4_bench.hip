@@ -94,11 +94,11 @@ int main(int argc, char** argv) {
   bf16 *A, *B, *C;
   float* R;
   CK(hipMalloc(&A, maxA * 2));
-  CK(hipMalloc(&B, maxB * 2));
+  CK(hipMalloc(&B, maxA * 2));
   CK(hipMalloc(&C, maxC * 2));
   CK(hipMalloc(&R, maxC * 4));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, st, A, maxA, 1u);
-  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, st, B, maxB, 2u);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, st, B, maxA, 2u);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -163,6 +163,56 @@ int main(int argc, char** argv) {
     const double us = ts[reps / 2] * 1e3;
     printf("store-only 16384x%d (%d tiles): %.1f us, %.2f TB/s\n", n, tiles, us, 16384.0 * n * 2 / us * 1e-6);
   }
+  {  // weight-gradient layout (A and B MN-major, f32 out): dW = dY^T X, K = tokens
+    const int Mt = 16384;
+    struct WS { const char* name; int n, k; };
+    const WS ws[] = {{"dW  4096x4096 K=16384", 4096, 4096}, {"dW  1024x4096 K=16384", 1024, 4096},
+                     {"dW  1024x1024 K=16384", 1024, 1024}};
+    float* Cf;
+    CK(hipMalloc(&Cf, 4096LL * 4096 * 4));
+    for (const WS& w : ws) {
+      g4::GroupParams gp{};
+      g4::Params& p = gp.g[0];
+      p.A = (const char*)A; p.lda = w.n; p.B = (const char*)B; p.ldb = w.k;
+      p.C = (char*)Cf; p.ldc = w.k; p.M = w.n; p.N = w.k; p.K = Mt; p.alpha = 1.f;
+      p.a_bytes = (uint32_t)((int64_t)Mt * w.n * 2); p.b_bytes = (uint32_t)((int64_t)Mt * w.k * 2);
+      p.tiles_m = w.n / 256; p.tiles_n = w.k / 256;
+      gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
+      const int grid = std::min(256, gp.tile_end[0]);
+      auto run = [&]() {
+        hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 0>), dim3(grid), dim3(g4::NT), 0, st, gp);
+      };
+      if ((int64_t)Mt * std::max(w.n, w.k) > maxA || (int64_t)Mt * w.k > maxA) continue;
+      run();
+      CK(hipStreamSynchronize(st));
+      // check row 0 and row n-1 of the output against a direct sum
+      std::vector<bf16> ha((size_t)Mt * w.n), hb((size_t)Mt * w.k);
+      std::vector<float> hc((size_t)w.n * w.k);
+      CK(hipMemcpy(ha.data(), A, ha.size() * 2, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hb.data(), B, hb.size() * 2, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hc.data(), Cf, hc.size() * 4, hipMemcpyDeviceToHost));
+      double maxd = 0, maxr = 0;
+      for (int i : {0, w.n / 2 + 3, w.n - 1})
+        for (int j = 0; j < w.k; j += 37) {
+          double ref = 0;
+          for (int r = 0; r < Mt; ++r) ref += (double)(float)ha[(size_t)r * w.n + i] * (double)(float)hb[(size_t)r * w.k + j];
+          maxd = std::max(maxd, fabs(hc[(size_t)i * w.k + j] - ref));
+          maxr = std::max(maxr, fabs(ref));
+        }
+      for (int it = 0; it < 3; ++it) run();
+      std::vector<float> ts;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0, st)); run(); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+      }
+      std::sort(ts.begin(), ts.end());
+      const double us = ts[reps / 2] * 1e3, fl = 2.0 * w.n * w.k * Mt;
+      printf("%-28s %8.1f us  %7.1f TF/s  err %.2e %s\n", w.name, us, fl / us * 1e-6, maxd / maxr,
+             maxd / maxr < 1e-4 ? "ok" : "BAD");
+      fflush(stdout);
+    }
+  }
+  if (getenv("G4_NO_ABL")) return 0;
   // ablations on two single-round shapes (timing only: results are wrong)
   struct Abl { int dbg; LaunchFn f; const char* what; };
   const Abl abl[] = {
