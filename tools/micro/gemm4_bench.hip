@@ -212,6 +212,61 @@ int main(int argc, char** argv) {
       fflush(stdout);
     }
   }
+  {  // ablations of the weight-gradient layout (dW 4096^2, K = 16384): timing only
+    const int Mt = 16384, n = 4096, k = 4096;
+    float* Cf;
+    CK(hipMalloc(&Cf, (size_t)n * k * 4));
+    g4::GroupParams gp{};
+    g4::Params& p = gp.g[0];
+    p.A = (const char*)A; p.lda = n; p.B = (const char*)B; p.ldb = k;
+    p.C = (char*)Cf; p.ldc = k; p.M = n; p.N = k; p.K = Mt; p.alpha = 1.f;
+    p.a_bytes = (uint32_t)((int64_t)Mt * n * 2); p.b_bytes = (uint32_t)((int64_t)Mt * k * 2);
+    p.tiles_m = n / 256; p.tiles_n = k / 256;
+    gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
+    struct AblMM { int dbg; void (*f)(const g4::GroupParams&, hipStream_t); const char* what; };
+    const AblMM am[] = {
+        {0, [](const g4::GroupParams& g, hipStream_t s) { hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 0>), dim3(256), dim3(256), 0, s, g); }, "baseline"},
+        {1, [](const g4::GroupParams& g, hipStream_t s) { hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 1>), dim3(256), dim3(256), 0, s, g); }, "no DMA in loop"},
+        {2, [](const g4::GroupParams& g, hipStream_t s) { hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 2>), dim3(256), dim3(256), 0, s, g); }, "no frag reads"},
+        {3, [](const g4::GroupParams& g, hipStream_t s) { hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 3>), dim3(256), dim3(256), 0, s, g); }, "no DMA, no reads"},
+        {8, [](const g4::GroupParams& g, hipStream_t s) { hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 8>), dim3(256), dim3(256), 0, s, g); }, "no MFMA"},
+        {16, [](const g4::GroupParams& g, hipStream_t s) { hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 16>), dim3(256), dim3(256), 0, s, g); }, "DMA early in h1"},
+    };
+    for (const AblMM& a : am) {
+      for (int w = 0; w < 3; ++w) a.f(gp, st);
+      std::vector<float> ts;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0, st)); a.f(gp, st); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+      }
+      std::sort(ts.begin(), ts.end());
+      const double us = ts[reps / 2] * 1e3, fl = 2.0 * n * k * Mt;
+      printf("  abl dW 4096^2 K=16384 dbg %d %-20s %8.1f us  %7.1f TF/s\n", a.dbg, a.what, us, fl / us * 1e-6);
+    }
+  }
+  {  // early DMA on the forward / dX shapes
+    for (int bkm = 1; bkm >= 0; --bkm)
+      for (int dbg : {0, 16}) {
+        g4::Params p{};
+        const int M = 16384, N = 1024, Kd = 4096;
+        p.A = (const char*)A; p.lda = Kd; p.B = (const char*)B; p.ldb = bkm ? Kd : N;
+        p.C = (char*)C; p.ldc = N; p.M = M; p.N = N; p.K = Kd; p.alpha = 1.f;
+        p.a_bytes = (uint32_t)((int64_t)M * Kd * 2); p.b_bytes = (uint32_t)((int64_t)N * Kd * 2);
+        auto f = [&]() {
+          if (bkm) { if (dbg) launch<true, 16>(p, st); else launch<true, 0>(p, st); }
+          else { if (dbg) launch<false, 16>(p, st); else launch<false, 0>(p, st); }
+        };
+        for (int w = 0; w < 3; ++w) f();
+        std::vector<float> ts;
+        for (int r = 0; r < reps; ++r) {
+          CK(hipEventRecord(e0, st)); f(); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+          float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        const double us = ts[reps / 2] * 1e3, fl = 2.0 * M * N * Kd;
+        printf("  %s ffn2 16384x1024x4096 dbg %2d %8.1f us  %7.1f TF/s\n", bkm ? "fwd" : "dX ", dbg, us, fl / us * 1e-6);
+      }
+  }
   if (getenv("G4_NO_ABL")) return 0;
   // ablations on two single-round shapes (timing only: results are wrong)
   struct Abl { int dbg; LaunchFn f; const char* what; };
