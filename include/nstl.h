@@ -350,8 +350,14 @@ enum {
   NSTL_K_ATTN_BWD_GENERIC,
   NSTL_K_GEMM4,              /* 4-wave persistent 256x256 GEMM launches (csrc/gemm4.h) */
   NSTL_K_GEMM4_TILES,        /*   ... their 256x256 output tiles */
+  NSTL_K_GEMM4_SK,           /*   ... launches with a stream-K tail (grid not dividing the tiles) */
   NSTL_K_COUNT
 };
+/* Workgroups a persistent one-per-CU grid launches on `stream` (the GEMM and
+ * attention-forward grids): 8 x the fewest CUs the stream's CU mask leaves on one
+ * XCD (mask bit i = a CU of XCD i % 8).  A compute stream that cedes CUs to the
+ * gradient collectives should cede them evenly over the XCDs. */
+int nstl_stream_cus(void* stream);
 /* Copies min(n, NSTL_K_COUNT) counters to out; returns NSTL_K_COUNT. */
 int nstl_kernel_counts(int64_t* out, int n);
 void nstl_kernel_counts_reset(void);

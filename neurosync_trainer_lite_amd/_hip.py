@@ -118,13 +118,13 @@ EXPORTS = [
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_clip_coef", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
     "nstl_features", "nstl_stft_mel", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
     "nstl_version", "nstl_fp8_quant_rows", "nstl_fp8_quant_cols", "nstl_kernel_counts", "nstl_kernel_counts_reset",
-    "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs", "nstl_transpose_bf16",
+    "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs", "nstl_transpose_bf16", "nstl_stream_cus",
 ]
 
 # nstl_kernel_counts order (NSTL_K_* in include/nstl.h)
 KERNEL_COUNT_NAMES = ["gemm128", "gemm_ring", "gemm_ring_tiles", "gemm_group", "gemm_group_tiles",
                       "gemm_splitk_reduce", "gemm_fp8", "attn_fwd", "attn_fwd_generic", "attn_bwd_fused",
-                      "attn_bwd_split", "attn_bwd_generic", "gemm4", "gemm4_tiles"]
+                      "attn_bwd_split", "attn_bwd_generic", "gemm4", "gemm4_tiles", "gemm4_sk"]
 
 _lib = None
 
@@ -182,6 +182,8 @@ def lib():
         L.nstl_kernel_counts.argtypes = [_vp, _i32]
         L.nstl_kernel_counts.restype = _i32
         L.nstl_kernel_counts_reset.restype = None
+        L.nstl_stream_cus.argtypes = [_vp]
+        L.nstl_stream_cus.restype = _i32
         _lib = L
     return _lib
 
@@ -219,6 +221,11 @@ def kernel_counts():
 
 def kernel_counts_reset():
     lib().nstl_kernel_counts_reset()
+
+
+def stream_cus(stream=None):
+    """Persistent-grid workgroups for `stream` (nstl_stream_cus: its CU mask, balanced over the XCDs)."""
+    return lib().nstl_stream_cus(stream if stream is not None else stream_of())
 
 
 def ptr(t):

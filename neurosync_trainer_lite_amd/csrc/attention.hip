@@ -498,7 +498,9 @@ NSTL_DEV float swap_pair(float v) {
 // moves (the per-element form waited on one ds_bpermute and two table reads at
 // a time).  Tables [T][RS] with row stride RS floats (32 in global memory, 36
 // in the fused kernel's LDS copy: the rows 4g + r of a wave's four lane groups
-// then fall on distinct banks).  rope_apply needs every lane of the wave active.
+// then fall on distinct banks).  The sin table comes out with the lane's sign
+// folded in (ts = -sin on odd lanes), so every element is x cos + partner ts:
+// one multiply and one FMA.  rope_apply needs every lane of the wave active.
 template <int RS>
 NSTL_DEV void rope_tab(float (&tc)[4][4], float (&ts)[4][4], int row0, int c, const float* cs, const float* sn) {
 #pragma unroll
@@ -507,31 +509,33 @@ NSTL_DEV void rope_tab(float (&tc)[4][4], float (&ts)[4][4], int row0, int c, co
     for (int dt = 0; dt < 4; ++dt) {
       const int i = (row0 + r) * RS + dt * 8 + (c >> 1);
       tc[dt][r] = cs[i];
-      ts[dt][r] = sn[i];
+      ts[dt][r] = (c & 1) ? -sn[i] : sn[i];
     }
 }
-NSTL_DEV void rope_apply(float (&v)[4][4], const float (&tc)[4][4], const float (&ts)[4][4], int c) {
+NSTL_DEV void rope_apply(float (&v)[4][4], const float (&tc)[4][4], const float (&ts)[4][4]) {
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const float x = v[dt][r], partner = swap_pair(x);
-      v[dt][r] = (c & 1) ? (x * tc[dt][r] - partner * ts[dt][r]) : (x * tc[dt][r] + partner * ts[dt][r]);
+      v[dt][r] = fmaf(partner, ts[dt][r], x * tc[dt][r]);
     }
 }
-// The same cos / sin values recomputed: angle = float(t) * inv_freq_i exactly as
-// rotation_tables() forms it (f32 product), then the hardware sin / cos
-// (v_sin_f32 / v_cos_f32 on angle / 2pi).  Against the f32 tables the error is
-// ~1e-6 absolute, far below the bf16 rounding of the dQ / dK it rotates.
+// The same cos / sin values recomputed: angle = float(t) * inv_freq_i as
+// rotation_tables() forms it (f32 product; inv_freq by the hardware exp), then
+// the hardware sin / cos (v_sin_f32 / v_cos_f32 on angle / 2pi).  Against the
+// f32 tables the error is ~1e-6 absolute, far below the bf16 rounding of the
+// dQ / dK it rotates.
 NSTL_DEV void rope_tab_fast(float (&tc)[4][4], float (&ts)[4][4], int row0, int c) {
+  const float sgn = (c & 1) ? -1.f : 1.f;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
     const float two_i = (float)(2 * (dt * 8 + (c >> 1)));
-    const float inv_freq = expf(-9.21034049987793f * two_i / (float)DH);  // f32(ln 10000)
+    const float inv_freq = __expf(-9.21034049987793f * two_i / (float)DH);  // f32(ln 10000)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float a = (float)(row0 + r) * inv_freq;
-      ts[dt][r] = __sinf(a);
+      ts[dt][r] = sgn * __sinf(a);
       tc[dt][r] = __cosf(a);
     }
   }
@@ -543,7 +547,7 @@ NSTL_DEV void rope_back_tile(float (&v)[4][4], int row0, int c, const float* cs,
   float tc[4][4], ts[4][4];
   if (fast) rope_tab_fast(tc, ts, row0, c);
   else rope_tab<DH / 2>(tc, ts, row0, c, cs, sn);
-  rope_apply(v, tc, ts, c);
+  rope_apply(v, tc, ts);
 }
 
 // Bias gradients fused into the backward stores: column sums of a wave's stored
@@ -553,6 +557,21 @@ NSTL_DEV void rope_back_tile(float (&v)[4][4], int row0, int c, const float* cs,
 // writes one partial row: deterministic, no float atomics.
 template <typename T>
 NSTL_DEV void wave_colsum16x64(const float (&v)[4][4], float* red, int w, int lane) {
+  if constexpr (sizeof(T) == 2) {
+    // bf16: one v_mfma_f32_16x16x16_bf16 per 16 columns, ones x tile: the lane's
+    // four rows 4g + r of column 16 dt + c are exactly its B operand, and every
+    // result row is the column sum of the stored (bf16) values -- lane c of lane
+    // group 0 holds column 16 dt + c, no cross-lane reduction
+    const s16x4 ones = __builtin_bit_cast(s16x4, (bf16x4){(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f});
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 x = {(bf16)v[dt][0], (bf16)v[dt][1], (bf16)v[dt][2], (bf16)v[dt][3]};
+      const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ones, __builtin_bit_cast(s16x4, x),
+                                                                (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      if (lane < 16) red[w * 64 + dt * 16 + lane] = d[0];
+    }
+    return;
+  }
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
     float cs = 0.f;
@@ -1073,8 +1092,8 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
       float tc[4][4], ts[4][4];
       if (rope_tabs) rope_tab<FUSED_RS>(tc, ts, k0 + 4 * g, c, cos_s, sin_s);
       else rope_tab_fast(tc, ts, k0 + 4 * g, c);
-      if (p.rope_q) rope_apply(vq, tc, ts, c);
-      if (p.rope_k) rope_apply(vk, tc, ts, c);
+      if (p.rope_q) rope_apply(vq, tc, ts);
+      if (p.rope_k) rope_apply(vk, tc, ts);
     }
     char* scr = scratch + w * 16 * RBK;
     const int64_t r0 = tok0 + k0;

@@ -70,10 +70,27 @@ struct Params {
   int tiles_m, tiles_n;
 };
 
+// Stream-K tail (slab != nullptr): when the tile count T is not a multiple of
+// the grid G (a compute stream that cedes CUs), tiles [0, dp_tiles) are dealt
+// whole (w, w + G, ...; dp_tiles = (T / G - 1) G) and the last G + T % G tiles
+// are cut into 256-deep K units and dealt as G equal contiguous unit ranges.  A
+// range spans at least one tile, so a tile has at most two contributors: each
+// writes its partial accumulators to its slab (write-through sc1 stores), takes
+// a ticket, and the second one adds the other's slab (sc1 loads) and runs the
+// epilogue.  x + y == y + x: the result does not depend on who arrives last.
+struct StreamK {
+  float* slab;          // [2 G slots][4 waves][64 (a, b)][64 lanes] f32x4 = 256 KB per slot
+  unsigned* cnt;        // [G + T % G][4 waves] tickets, zero between launches (the second arriver resets)
+  uint32_t slab_bytes;
+  int dp_tiles;
+  int units;            // 256-deep K units per tile (every problem the same K)
+};
+
 struct GroupParams {
   Params g[GROUP_MAX];
   int tile_end[GROUP_MAX];
   int n;
+  StreamK sk;
 };
 static_assert(sizeof(GroupParams) <= 4096, "kernel arguments");
 
@@ -209,14 +226,16 @@ NSTL_DEV void dma_lanes(Dma& d, const Params& p, int wave, int lane) {
 // the scalar part of a tile (resources rebuilt from the kernel arguments every
 // tile: a resource chosen by a branch is not provably uniform, and the compiler
 // would wrap every DMA in a readfirstlane loop)
+// (ks: the first 256-deep K unit of a stream-K segment)
 template <bool AK, bool BKM>
-NSTL_DEV void dma_tile(Dma& d, const Params& p, int m0, int n0) {
+NSTL_DEV void dma_tile(Dma& d, const Params& p, int m0, int n0, int ks) {
   d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)p.a_bytes, 0x00020000);
   d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, (int)p.b_bytes, 0x00020000);
   d.a_kb = AK ? 2 * BK : (uint32_t)(2 * BK * p.lda);
   d.b_kb = BKM ? 2 * BK : (uint32_t)(2 * BK * p.ldb);
-  d.ta = __builtin_amdgcn_readfirstlane(AK ? (uint32_t)(m0 * p.lda * 2) : (uint32_t)(m0 * 2));
-  d.tb = __builtin_amdgcn_readfirstlane(BKM ? (uint32_t)(n0 * p.ldb * 2) : (uint32_t)(n0 * 2));
+  const uint32_t k0 = (uint32_t)ks * 4u;  // stages
+  d.ta = __builtin_amdgcn_readfirstlane((AK ? (uint32_t)(m0 * p.lda * 2) : (uint32_t)(m0 * 2)) + k0 * d.a_kb);
+  d.tb = __builtin_amdgcn_readfirstlane((BKM ? (uint32_t)(n0 * p.ldb * 2) : (uint32_t)(n0 * 2)) + k0 * d.b_kb);
 }
 
 // every read slot of a half-step (slot 0, h = 0): the first tile's prologue
@@ -320,6 +339,129 @@ NSTL_DEV f32x4 rd_acc(f32x4& x) {
   return (f32x4){r0, r1, r2, r3};
 }
 
+// read without zeroing (a stream-K partial, kept for the sum)
+NSTL_DEV f32x4 rd_acc_keep(const f32x4& x) {
+  float r0, r1, r2, r3;
+  asm volatile(
+      "v_accvgpr_read_b32 %0, %4\n\t"
+      "v_accvgpr_read_b32 %1, %5\n\t"
+      "v_accvgpr_read_b32 %2, %6\n\t"
+      "v_accvgpr_read_b32 %3, %7"
+      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+      : "a"(x[0]), "a"(x[1]), "a"(x[2]), "a"(x[3]));
+  return (f32x4){r0, r1, r2, r3};
+}
+// x += y in place
+NSTL_DEV void add_acc(f32x4& x, const f32x4 y) {
+  float t0, t1, t2, t3;
+  asm volatile(
+      "v_accvgpr_read_b32 %0, %4\n\t"
+      "v_accvgpr_read_b32 %1, %5\n\t"
+      "v_accvgpr_read_b32 %2, %6\n\t"
+      "v_accvgpr_read_b32 %3, %7\n\t"
+      "v_add_f32 %0, %0, %8\n\t"
+      "v_add_f32 %1, %1, %9\n\t"
+      "v_add_f32 %2, %2, %10\n\t"
+      "v_add_f32 %3, %3, %11\n\t"
+      "v_accvgpr_write_b32 %4, %0\n\t"
+      "v_accvgpr_write_b32 %5, %1\n\t"
+      "v_accvgpr_write_b32 %6, %2\n\t"
+      "v_accvgpr_write_b32 %7, %3"
+      : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "+a"(x[0]), "+a"(x[1]), "+a"(x[2]), "+a"(x[3])
+      : "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]));
+}
+
+// The work of workgroup w: its whole tiles, then its stream-K unit range.  A
+// segment is tile t, K units [ks, ke) (ke < 0: the whole tile, any K).
+struct Seg {
+  int t, ks, ke;
+};
+struct Walker {
+  int t_dp, G, dp_tiles, U;
+  int pos, end;  // units: at most 2 G tiles x 64 (K = 16384) in the tail
+  NSTL_DEV void init(const GroupParams& gp, int T, int w, int G_, bool sk) {
+    G = G_;
+    t_dp = w;
+    if (sk) {
+      dp_tiles = gp.sk.dp_tiles;
+      U = gp.sk.units;
+      const int I = (T - dp_tiles) * U;
+      pos = w * I / G;
+      end = (w + 1) * I / G;
+    } else {
+      dp_tiles = T;
+      U = 1;
+      pos = end = 0;
+    }
+  }
+  NSTL_DEV bool next(Seg& s) {
+    if (t_dp < dp_tiles) {
+      s.t = t_dp;
+      s.ks = 0;
+      s.ke = -1;
+      t_dp += G;
+      return true;
+    }
+    if (pos >= end) return false;
+    s.t = dp_tiles + pos / U;
+    s.ks = pos % U;
+    s.ke = s.ks + end - pos < U ? s.ks + end - pos : U;
+    pos += s.ke - s.ks;
+    return true;
+  }
+};
+
+// The stream-K hand-off at the end of a segment, per wave (a wave's 128 x 128
+// block is its own: slab part, ticket and epilogue).  Returns whether this wave
+// finishes the block: a whole tile, or the second contributor (its accumulators
+// then hold the sum); the first contributor's epilogue runs with its stores off
+// (it zeroes the accumulators for the next segment).  The tile's head [0, ks)
+// belongs to the previous workgroup's range (its last segment, slot
+// 2 (w - 1) + 1), its tail to the next one's (first segment, slot 2 (w + 1)).
+// One straight-line pass whatever the case -- a branch over the accumulators
+// splits their live ranges and spills: stores and loads that do not apply go
+// through an empty buffer range (dropped; loads return 0).
+NSTL_DEV bool sk_handoff(const StreamK& sk, f32x4 (&acc)[8][8], const Seg& s, int wave, int lane) {
+  const int w = blockIdx.x;
+  const bool part = !(s.ke < 0 || (s.ks == 0 && s.ke == sk.units));
+  const bool tail = s.ks > 0;
+  const uint32_t mine = (uint32_t)(tail ? 2 * w : 2 * w + 1), other = (uint32_t)(tail ? 2 * w - 1 : 2 * w + 2);
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)sk.slab, 0, part ? (int)sk.slab_bytes : 0, 0x00020000);
+  const uint32_t wsoff = (uint32_t)wave * 65536u;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const f32x4 v = rd_acc_keep(acc[a][b]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, v), r, lane * 16 + (a * 8 + b) * 1024,
+                                             mine * 262144u + wsoff, 16 /* sc1: write-through */);
+      G4_SB();
+    }
+  G4_VMCNT(0);  // the slab part is written through before the ticket
+  unsigned old = 0;
+  if (part && lane == 0) {
+    unsigned* c = sk.cnt + 4 * (s.t - sk.dp_tiles) + wave;
+    old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == 1u) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const bool last = __builtin_amdgcn_readfirstlane(old) == 1u;
+  const __amdgpu_buffer_rsrc_t rl =
+      __builtin_amdgcn_make_buffer_rsrc((void*)sk.slab, 0, part && last ? (int)sk.slab_bytes : 0, 0x00020000);
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    i32x4_t y[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+      y[b] = __builtin_amdgcn_raw_buffer_load_b128(rl, lane * 16 + (a * 8 + b) * 1024, other * 262144u + wsoff,
+                                                   16 /* sc1 */);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) add_acc(acc[a][b], __builtin_bit_cast(f32x4, y[b]));
+    G4_SB();  // one row of blocks (8 loads) in flight at a time
+  }
+  return !part || last;
+}
+
 // ---------------------------------------------------------------------------
 // Epilogues, from registers.  row0 / col0: the wave's 128 x 128 block.
 // bf16 outputs: per (a, pair of column blocks bp, bp + 1) the elementwise math
@@ -331,29 +473,33 @@ NSTL_DEV f32x4 rd_acc(f32x4& x) {
 // loaded first (bias, dReLU mask words) or read from LDS (RoPE tables).
 template <int EM>
 NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, int lane, int wave, int tile_id,
-                       const char* rope_lds) {
+                       const char* rope_lds, bool fin = true) {
   const int g = lane >> 4, c = lane & 15, odd = g & 1;
   const float alpha = p.alpha;
   if constexpr (EM == EM_F32) {
     // f32 out: lane stores its 4 columns (16 B); sum of squares of the stored
     // values -> sq_part (the clip norm's partial, training_utils.py:73)
     float ssq = 0.f;
+    // stores through a buffer whose range is empty when this wave does not finish
+    // the block (a stream-K first contributor): no branch around them
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.C, 0, fin ? (int)((uint32_t)p.M * (uint32_t)p.ldc * 4u) : 0, 0x00020000);
 #pragma unroll
     for (int a = 0; a < 8; ++a) {
-      float* crow = (float*)p.C + (int64_t)(row0 + 16 * a + c) * p.ldc + col0 + 4 * g;
+      const uint32_t crow = ((uint32_t)(row0 + 16 * a + c) * (uint32_t)p.ldc + col0 + 4 * g) * 4u;
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         const f32x4 v = rd_acc(acc[a][b]) * alpha;
 #pragma unroll
         for (int e = 0; e < 4; ++e) ssq += v[e] * v[e];
-        *(f32x4*)(crow + 16 * b) = v;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, v), rc, crow + 64 * b, 0, 0);
         G4_SB();
       }
     }
     // the sum is formed unconditionally (a conditional one kept every stored value
     // alive until after the stores, and spilled them)
     const double tsum = wave_sum_d((double)ssq);
-    if (p.sq_part != nullptr && lane == 0) {
+    if (fin && p.sq_part != nullptr && lane == 0) {
       p.sq_part[tile_id * 8 + 2 * wave] = (float)tsum;
       p.sq_part[tile_id * 8 + 2 * wave + 1] = 0.f;
     }
@@ -455,7 +601,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
         const uint32_t y0 = pack_bf16x2(uv[1][0], uv[1][1]), y1 = pack_bf16x2(uv[1][2], uv[1][3]);
         const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-        *(uint4*)(crow + 16 * (bp + odd) + 4 * (g - odd)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        if (fin) *(uint4*)(crow + 16 * (bp + odd) + 4 * (g - odd)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         G4_SB();  // one (a, bp) group at a time: hoisting the accumulator reads spills
       }
     }
@@ -477,7 +623,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
           const auto shi = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
           lo = slo[0] | slo[1];
           hi = shi[0] | shi[1];
-          if (c < 8 && odd == 0)
+          if (fin && c < 8 && odd == 0)
             p.relu_mask[mask_word(p.N, row0 + 64 * hb + c, col0 + 16 * b + 4 * g)] = ((uint64_t)hi << 32) | lo;
         }
     }
@@ -495,7 +641,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
           x += NSTL_DPP(x, 0x140);  // row_mirror
           csum[b][e] = x;
         }
-      if (c == 0) {
+      if (fin && c == 0) {
         float* dst = p.colsum_part + (int64_t)(row0 >> 7) * p.N + col0 + 4 * g;
 #pragma unroll
         for (int b = 0; b < 8; ++b) *(f32x4*)(dst + 16 * b) = (f32x4){csum[b][0], csum[b][1], csum[b][2], csum[b][3]};
@@ -510,7 +656,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
 // aligned rows; operand extents < 2^31 bytes; EM_ROPE: T * rope_dim * 4 <=
 // ROPE_LDS and rope_dim % 4 == 0; EM_F32: beta 0.  Tiles of up to 16 problems
 // (gp.tile_end; one problem: n = 1).
-template <bool AK, bool BKM, int EM, bool GROUPED, int DBG = 0>
+template <bool AK, bool BKM, int EM, bool GROUPED, int DBG = 0, bool SK = false>
 __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM + (EM == EM_ROPE ? ROPE_LDS : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -518,8 +664,10 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   const int wm = wave >> 1, wn = wave & 1;
   const int T = gp.tile_end[gp.n - 1];
   const int G = gridDim.x;
-  int t = blockIdx.x;
-  if (t >= T) return;
+  Walker wk;
+  wk.init(gp, T, blockIdx.x, G, SK);
+  Seg sg;
+  if (!wk.next(sg)) return;
   const uint32_t smem_u32 = lds_addr(smem);
   char* const adst0 = smem + wave * 8 * 1024;
   char* const bdst0 = smem + 2 * OPS + wave * 8 * 1024;
@@ -549,10 +697,10 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     tile_coords(xcd_remap(lt, gp.tile_end[prob] - first), q.tiles_m, q.tiles_n, m0, n0);
   };
   int prob, m0, n0, lt;
-  locate(t, prob, m0, n0, lt);
+  locate(sg.t, prob, m0, n0, lt);
   Dma d;
   dma_lanes<AK, BKM>(d, gp.g[prob], wave, lane);
-  dma_tile<AK, BKM>(d, gp.g[prob], m0, n0);
+  dma_tile<AK, BKM>(d, gp.g[prob], m0, n0, sg.ks);
   RdAddr<AK> ra;
   RdAddr<BKM> rb;
   rd_addr<AK>(ra, smem_u32, wm * 128, lane);
@@ -608,13 +756,15 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
 
   for (;;) {
     const Params& p = gp.g[prob];
-    const int nk = p.K / BK;
-    const int tn = t + G;
-    const bool has_next = tn < T;
-    // the next tile (after the workgroup's last: itself again, a harmless refill
-    // of slots nobody reads afterwards, drained before exit)
+    // steps of this segment (a whole tile: K / 64)
+    const int nk = sg.ke < 0 ? p.K / BK : 4 * (sg.ke - sg.ks);
+    Seg ns;
+    const bool has_next = wk.next(ns);
+    // the next segment (after the workgroup's last: itself again, a harmless
+    // refill of slots nobody reads afterwards, drained before exit)
+    if (!has_next) ns = sg;
     int nprob = prob, nm0 = m0, nn0 = n0, nlt = lt;
-    if (has_next) locate(tn, nprob, nm0, nn0, nlt);
+    if (has_next) locate(ns.t, nprob, nm0, nn0, nlt);
     // step kt (slot kt & 1: nk is even, so every tile starts on slot 0) stages
     // stage kt + 2: this tile's while kt + 2 < nk, then the next tile's 0 and 1.
     // Three step sites (more make the register allocator give the fragment sets
@@ -625,14 +775,16 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
       if (kt + 1 < nk) {
         if (kt + 1 == nk - 2) {
           if (GROUPED && nprob != prob) dma_lanes<AK, BKM>(d, gp.g[nprob], wave, lane);
-          dma_tile<AK, BKM>(d, gp.g[nprob], nm0, nn0);
+          dma_tile<AK, BKM>(d, gp.g[nprob], nm0, nn0, ns.ks);
         }
         step(S0{}, W0{}, (uint32_t)(kt + 3 < nk ? kt + 3 : kt + 3 - nk), d);
       }
     }
-    epilogue<EM>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds);
+    bool fin = true;
+    if constexpr (SK) fin = sk_handoff(gp.sk, acc, sg, wave, lane);
+    epilogue<EM>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, fin);
     if (!has_next) break;
-    t = tn;
+    sg = ns;
     prob = nprob;
     m0 = nm0;
     n0 = nn0;

@@ -6,6 +6,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
 
 #include "../../include/nstl.h"
@@ -21,19 +22,63 @@ int gemm4_env() {
   return e ? atoi(e) : 1;
 }
 
-// compute units of the current device (persistent grid size), cached per device
-int cus_of_current() {
+// NSTL_GEMM4_SK=0: no stream-K tail (a partial last round of whole tiles instead)
+int sk_env() {
+  const char* e = getenv("NSTL_GEMM4_SK");
+  return e ? atoi(e) : 1;
+}
+
+// the stream-K slabs and tickets, per (device, stream): launches on different
+// streams never share them.  Tickets start at zero (hipMemset once) and every
+// tile's second arriver resets its own.
+struct SkSpace {
+  float* slab = nullptr;
+  unsigned* cnt = nullptr;
+  int G = 0;
+};
+bool sk_space(hipStream_t st, int G, g4::StreamK& sk) {
   static std::mutex mu;
-  static int cache[64] = {0};
+  static std::map<std::pair<int, hipStream_t>, SkSpace> spaces;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
   std::lock_guard<std::mutex> lk(mu);
-  if (!cache[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    cache[dev] = n;
+  SkSpace& s = spaces[{dev, st}];
+  if (s.G < G) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    if (hipStreamSynchronize(st) != hipSuccess) return false;  // the old space may be in use
+    if (s.slab) (void)hipFree(s.slab);
+    if (s.cnt) (void)hipFree(s.cnt);
+    s = SkSpace();
+    if (hipMalloc((void**)&s.slab, (size_t)2 * G * 262144) != hipSuccess) return false;
+    if (hipMalloc((void**)&s.cnt, (size_t)8 * G * sizeof(unsigned)) != hipSuccess) return false;
+    if (hipMemset(s.cnt, 0, (size_t)8 * G * sizeof(unsigned)) != hipSuccess) return false;
+    s.G = G;
   }
-  return cache[dev];
+  sk.slab = s.slab;
+  sk.cnt = s.cnt;
+  sk.slab_bytes = (uint32_t)((size_t)2 * G * 262144);
+  return true;
+}
+
+// whole tiles for the first T / G - 1 rounds, stream-K over the rest, when T is
+// not a multiple of G (and every problem's K splits into 256-deep units)
+void plan_sk(g4::GroupParams& gp, int G, hipStream_t st) {
+  memset(&gp.sk, 0, sizeof(gp.sk));
+  const int T = gp.tile_end[gp.n - 1];
+  if (T <= G || T % G == 0 || !sk_env()) return;
+  const int K = gp.g[0].K;
+  for (int i = 0; i < gp.n; ++i)
+    if (gp.g[i].K != K) return;
+  if (K % (4 * g4::BK)) return;
+  g4::StreamK sk;
+  if (!sk_space(st, G, sk)) {
+    (void)hipGetLastError();
+    return;
+  }
+  sk.dp_tiles = (T / G - 1) * G;
+  sk.units = K / (4 * g4::BK);
+  gp.sk = sk;
 }
 
 // the epilogue kind this kernel runs for `a`, or 0 (not eligible)
@@ -75,7 +120,9 @@ bool g4_shape_ok(const nstl_gemm_args* a) {
   // operand extents for the 32-bit buffer offsets
   const int64_t ae = a->a_kmajor ? ((int64_t)(a->M - 1) * a->lda + a->K) * 2 : ((int64_t)(a->K - 1) * a->lda + a->M) * 2;
   const int64_t be = a->b_kmajor ? ((int64_t)(a->N - 1) * a->ldb + a->K) * 2 : ((int64_t)(a->K - 1) * a->ldb + a->N) * 2;
-  return ae < (1ll << 31) && be < (1ll << 31);
+  // f32 C through a buffer resource (its epilogue's stores): 32-bit extent
+  const int64_t ce = a->c_dtype == NSTL_F32 ? (int64_t)a->M * a->ldc * 4 : 0;
+  return ae < (1ll << 31) && be < (1ll << 31) && ce < (1ll << 31);
 }
 
 void fill(g4::Params& q, const nstl_gemm_args* a) {
@@ -100,36 +147,46 @@ void fill(g4::Params& q, const nstl_gemm_args* a) {
   q.tiles_n = a->N / g4::TILE;
 }
 
-template <bool AK, bool BKM, bool GROUPED>
+template <bool AK, bool BKM, bool GROUPED, bool SK>
 void launch_em(int em, dim3 grid, hipStream_t st, const g4::GroupParams& gp) {
   const dim3 block(g4::NT);
   switch (em) {
-    case g4::EM_BF16: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_BF16, GROUPED>), grid, block, 0, st, gp); break;
+    case g4::EM_BF16: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_BF16, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
     case g4::EM_RELU_DROP:
-      hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_RELU_DROP, GROUPED>), grid, block, 0, st, gp);
+      hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_RELU_DROP, GROUPED, 0, SK>), grid, block, 0, st, gp);
       break;
-    case g4::EM_ROPE: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_ROPE, GROUPED>), grid, block, 0, st, gp); break;
-    case g4::EM_DRELU: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_DRELU, GROUPED>), grid, block, 0, st, gp); break;
-    default: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_F32, GROUPED>), grid, block, 0, st, gp); break;
+    case g4::EM_ROPE: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_ROPE, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
+    case g4::EM_DRELU: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_DRELU, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
+    default: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_F32, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
   }
 }
 
 // the instantiations the step uses: forward and dX (A K-major) with every
-// epilogue; the weight gradients (NN) with f32 output, grouped or not
-int launch(int em, bool ak, bool bk, bool grouped, int G, hipStream_t st, const g4::GroupParams& gp) {
-  const int tiles = gp.tile_end[gp.n - 1];
-  const dim3 grid(tiles < G ? tiles : G);
+// epilogue; the weight gradients (NN) with f32 output, grouped or not; each
+// with and without the stream-K tail
+template <bool SK>
+int launch_sk(int em, bool ak, bool bk, bool grouped, dim3 grid, hipStream_t st, const g4::GroupParams& gp) {
   if (ak && bk) {
     if (grouped) return 0;
-    launch_em<true, true, false>(em, grid, st, gp);
+    launch_em<true, true, false, SK>(em, grid, st, gp);
   } else if (ak && !bk) {
     if (grouped) return 0;
-    launch_em<true, false, false>(em, grid, st, gp);
+    launch_em<true, false, false, SK>(em, grid, st, gp);
   } else {
     if (em != g4::EM_F32) return 0;
-    if (grouped) hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, true>), grid, dim3(g4::NT), 0, st, gp);
-    else hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false>), grid, dim3(g4::NT), 0, st, gp);
+    if (grouped) hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, true, 0, SK>), grid, dim3(g4::NT), 0, st, gp);
+    else hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 0, SK>), grid, dim3(g4::NT), 0, st, gp);
   }
+  return 1;
+}
+
+int launch(int em, bool ak, bool bk, bool grouped, int G, hipStream_t st, g4::GroupParams& gp) {
+  const int tiles = gp.tile_end[gp.n - 1];
+  const dim3 grid(tiles < G ? tiles : G);
+  plan_sk(gp, G, st);
+  if (!gp.sk.slab) return launch_sk<false>(em, ak, bk, grouped, grid, st, gp);
+  if (!launch_sk<true>(em, ak, bk, grouped, grid, st, gp)) return 0;
+  nstl::count(NSTL_K_GEMM4_SK);
   return 1;
 }
 
@@ -144,7 +201,7 @@ int gemm4(const nstl_gemm_args* a, hipStream_t st, int* handled) {
   const int em = g4_mode(a);
   if (!em) return 0;
   if (!a->a_kmajor && em != g4::EM_F32) return 0;
-  const int G = cus_of_current();
+  const int G = nstl::stream_cus(st);
   if (G <= 0) return 0;
   g4::GroupParams gp;
   memset(&gp, 0, sizeof(gp));
@@ -168,7 +225,7 @@ int gemm4_grouped(const nstl_gemm_args* args, int n, hipStream_t st, int* handle
     if (!g4_shape_ok(a) || g4_mode(a) != g4::EM_F32 || a->epilogue != NSTL_EPI_NONE) return 0;
     if (a->a_kmajor != args[0].a_kmajor || a->b_kmajor != args[0].b_kmajor) return 0;
   }
-  const int G = cus_of_current();
+  const int G = nstl::stream_cus(st);
   if (G <= 0) return 0;
   g4::GroupParams gp;
   memset(&gp, 0, sizeof(gp));

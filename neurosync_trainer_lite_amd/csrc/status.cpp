@@ -2,6 +2,8 @@
 
 #include <stdarg.h>
 
+#include <stdlib.h>
+
 #include <atomic>
 
 #include "../../include/nstl.h"
@@ -25,6 +27,33 @@ static std::atomic<long long> g_counts[NSTL_K_COUNT];
 void count(int which, long long n) {
   if (which >= 0 && which < NSTL_K_COUNT) g_counts[which].fetch_add(n, std::memory_order_relaxed);
 }
+
+int stream_cus(hipStream_t st) {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 0;
+    cus[dev] = n;
+  }
+  const int ncu = cus[dev];
+  int g = ncu;
+  uint32_t m[32] = {0};
+  const int words = (ncu + 31) / 32;
+  if (ncu % 8 == 0 && words <= 32 && hipExtStreamGetCUMask(st, (uint32_t)words, m) == hipSuccess) {
+    int per[8] = {0};
+    for (int i = 0; i < ncu; ++i) per[i % 8] += (m[i / 32] >> (i % 32)) & 1;
+    int lo = per[0];
+    for (int x = 1; x < 8; ++x) lo = per[x] < lo ? per[x] : lo;
+    if (lo > 0) g = 8 * lo;
+  } else {
+    (void)hipGetLastError();  // no mask (or not queryable): every CU
+  }
+  const char* e = getenv("NSTL_PERSIST_CUS");
+  if (e && atoi(e) > 0 && atoi(e) < g) g = atoi(e);
+  return g;
+}
 }  // namespace nstl
 
 extern "C" int nstl_kernel_counts(int64_t* out, int n) {
@@ -32,6 +61,8 @@ extern "C" int nstl_kernel_counts(int64_t* out, int n) {
     out[i] = nstl::g_counts[i].load(std::memory_order_relaxed);
   return NSTL_K_COUNT;
 }
+
+extern "C" int nstl_stream_cus(void* stream) { return nstl::stream_cus((hipStream_t)stream); }
 
 extern "C" void nstl_kernel_counts_reset(void) {
   for (auto& c : nstl::g_counts) c.store(0, std::memory_order_relaxed);

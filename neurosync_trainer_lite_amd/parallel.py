@@ -17,16 +17,24 @@ parameter is copied back, with nothing overlapped.  Here:
     on RCCL's own stream, overlapping the remaining backward;
   * clip + Adam then run replicated on every rank on identical reduced grads.
 
-Default mode (NSTL_DP=zero1, ShardComm + utils.optim.FusedAdam.shard): no
-collective runs during backward -- a concurrent RCCL kernel holding even a few
-CUs turns the step's one-workgroup-per-CU GEMM rounds into two rounds
-(tools/cu_hog_bench.py: 4 held CUs cost +36 % step time).  After backward the
-gradient arena is reduce-scattered (f32), each rank clips with the global norm
-(one all-reduce of 1024 partial sums) and runs Adam on its 1/n shard, and the
-updated compute-dtype parameters are all-gathered.  Per step and rank that moves
-(n-1)/n of 4 + 2 bytes per parameter instead of an all-reduce's 2 * 4, and the
-optimizer's 30 B/param of HBM traffic drops to 1/n.  The f32 master weights and
-Adam moments outside a rank's shard go stale until consolidate() (checkpoints).
+Default mode (NSTL_DP=zero1, ShardComm + utils.optim.FusedAdam.shard): after
+backward the gradient arena is reduce-scattered (f32), each rank clips with the
+global norm (one all-reduce of 1024 partial sums) and runs Adam on its 1/n
+shard, and the updated compute-dtype parameters are all-gathered.  Per step and
+rank that moves (n-1)/n of 4 + 2 bytes per parameter instead of an
+all-reduce's 2 * 4, and the optimizer's 30 B/param of HBM traffic drops to 1/n.
+The f32 master weights and Adam moments outside a rank's shard go stale until
+consolidate() (checkpoints).
+
+NSTL_DP=zero1_overlap (GradShardReducer) moves the reduction into backward: as
+soon as a bucket of the arena is final it is reduced (SUM) onto the rank whose
+shard holds it, on RCCL's stream, so the reduce-scatter leaves the critical
+path; buckets never straddle a shard boundary, and the post-backward step skips
+its reduce-scatter.  A collective kernel resident during backward holds CUs the
+step's persistent grids would otherwise use: run the compute stream on a CU
+mask that cedes them evenly over the XCDs (NSTL_CEDE_CUS, one CU per XCD at 8;
+nstl_stream_cus then sizes the GEMM / attention grids to the CUs left, and
+the GEMM's stream-K tail keeps the cost near k / 256, tools/cu_mask_bench.py).
 """
 import os
 
@@ -58,6 +66,38 @@ def init_from_env(backend=None):
         else:
             dist.init_process_group(backend)
     return rank, world, local
+
+
+_CEDED = {}
+
+
+def cede_cus(k, device):
+    """Make the current stream of `device` a stream whose CU mask leaves out mask
+    bits 0 .. k-1 -- bit i is a CU of XCD i % 8 (tools/micro/cu_probe.hip), so k
+    a multiple of 8 cedes k / 8 CUs on every XCD -- for the collective kernels
+    that run during backward (NSTL_DP=zero1_overlap).  Returns the stream (kept
+    alive here); k <= 0 leaves the current stream."""
+    if k <= 0:
+        return torch.cuda.current_stream(device)
+    import ctypes
+    from . import _hip
+    key = (torch.device(device).index, k)
+    if key not in _CEDED:
+        fn = ctypes.CDLL(_hip.LIB_PATH).hipExtStreamCreateWithCUMask
+        fn.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+        n = torch.cuda.get_device_properties(device).multi_processor_count
+        words = (n + 31) // 32
+        mask = (ctypes.c_uint32 * words)()
+        for c in range(k, n):
+            mask[c // 32] |= 1 << (c % 32)
+        with torch.cuda.device(device):
+            st = ctypes.c_void_p()
+            if fn(ctypes.byref(st), words, mask) != 0:
+                raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+        _CEDED[key] = torch.cuda.ExternalStream(st.value, device=device)
+    s = _CEDED[key]
+    torch.cuda.set_stream(s)
+    return s
 
 
 def shard_batch_indices(num_batches, rank, world):
@@ -109,6 +149,45 @@ class GradAllReducer:
         self.reset()
 
 
+class GradShardReducer(GradAllReducer):
+    """ZeRO-1 with the reduction overlapped with backward: bucketed SUM reduce of
+    each final arena prefix onto the owning rank of `comm` (ShardComm), cut at
+    shard boundaries; [comm.numel, end) -- the replicated tail -- is left to
+    zero1_step.  After finish(), rank r's arena [comm.lo, comm.hi) holds the
+    summed gradients (what the reduce-scatter would have written)."""
+
+    def __init__(self, grads, comm, bucket_bytes=DEFAULT_BUCKET_BYTES, min_world=2):
+        self.comm = comm
+        super().__init__(grads, comm.group, bucket_bytes, min_world)
+
+    def ready(self, upto):
+        if not self.active:
+            return
+        upto = min(upto, self.comm.numel)
+        while self.sent < upto:
+            owner = self.sent // self.comm.shard
+            end = min((owner + 1) * self.comm.shard, self.sent + self.bucket)
+            if end > upto:
+                return
+            self._reduce(self.sent, end, owner)
+
+    def _reduce(self, lo, hi, owner):
+        dst = dist.get_global_rank(self.group, owner) if self.group is not None else owner
+        self.works.append(dist.reduce(self.g[lo:hi], dst=dst, op=dist.ReduceOp.SUM, group=self.group,
+                                      async_op=True))
+        self.sent = hi
+
+    def finish(self):
+        if not self.active:
+            return
+        while self.sent < self.comm.numel:
+            owner = self.sent // self.comm.shard
+            self._reduce(self.sent, min((owner + 1) * self.comm.shard, self.sent + self.bucket), owner)
+        for w in self.works:
+            w.wait()
+        self.reset()
+
+
 class ShardComm:
     """Equal contiguous shards of a flat arena over the ranks of `group`:
     reduce-scatter / all-gather of the arena (torch's tensor collectives, the
@@ -134,15 +213,19 @@ class ShardComm:
         dist.all_gather_into_tensor(full, full[self.lo:self.hi].clone(), group=self.group)
 
 
-def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=None):
+def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=None, reduced=False):
     """One sharded clip + Adam step (the FusedAdam kernels passed in as callables,
     so the orchestration is testable on CPU): reduce-scatter the gradients of
-    the shardable region [0, comm.numel), sum of squares of this shard, all-reduce
-    of the partial sums; `tail` = (lo, hi), a small replicated region (the f32
-    vectors), is all-reduced whole, its squares added once and updated on every
-    rank; Adam on this shard (+ tail), then all-gather each tensor of `gather`
-    over the shardable region."""
-    comm.reduce_scatter(g_full[:comm.numel], g_shard)
+    the shardable region [0, comm.numel) (``reduced``: GradShardReducer already
+    summed this rank's shard in place during backward), sum of squares of this
+    shard, all-reduce of the partial sums; `tail` = (lo, hi), a small replicated
+    region (the f32 vectors), is all-reduced whole, its squares added once and
+    updated on every rank; Adam on this shard (+ tail), then all-gather each
+    tensor of `gather` over the shardable region."""
+    if reduced:
+        g_shard.copy_(g_full[comm.lo:comm.hi])
+    else:
+        comm.reduce_scatter(g_full[:comm.numel], g_shard)
     sumsq_fn(g_shard, partial)
     dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=comm.group)
     if tail is not None and tail[1] > tail[0]:

@@ -199,8 +199,10 @@ class FusedAdam(torch.optim.Optimizer):
         from .. import parallel
         if max_norm is None:
             self.partial.zero_()
+        reduced = isinstance(eng.grad_reducer, parallel.GradShardReducer) and eng.grad_reducer.active
         parallel.zero1_step(self._comm, eng.g32, self._gs, self.partial, sumsq_fn, adam_fn,
-                            [eng.p16] if eng.p16 is not eng.p32 else [eng.p32], tail=(eng.n_shardable, eng.numel))
+                            [eng.p16] if eng.p16 is not eng.p32 else [eng.p32], tail=(eng.n_shardable, eng.numel),
+                            reduced=reduced)
         eng.master_stale = eng.p16 is not eng.p32
         self._moments_stale = True
         self._snapshot_norm(max_norm)

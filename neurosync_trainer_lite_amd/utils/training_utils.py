@@ -184,19 +184,27 @@ def rank_batches(dataloader, rank, world):
 
 def attach_data_parallel(model, optimizer, world):
     """Wire one rank's engine/optimizer for data parallelism (parallel.py): the
-    loss gradient pre-scaled by 1/world, per-rank dropout streams, and either the
-    sharded optimizer (NSTL_DP=zero1, default: no collective during backward) or
-    the bucketed gradient all-reduce overlapped with backward (NSTL_DP=allreduce)."""
+    loss gradient pre-scaled by 1/world, per-rank dropout streams, and one of
+    NSTL_DP=zero1 (default: the sharded optimizer, no collective during
+    backward), zero1_overlap (the same with each shard reduced onto its owner
+    bucket by bucket during backward, the compute stream ceding NSTL_CEDE_CUS
+    CUs, 8 by default, to the collectives) or allreduce (bucketed all-reduce
+    during backward, replicated optimizer)."""
     eng = _engine_of(model)
     if eng is None or world == 1 or eng.grad_scale_t is not None:
         return
     eng.grad_scale_t = torch.full((1,), 1.0 / world, device=eng.device)
     eng.seed_salt = dist.get_rank()
-    if os.environ.get("NSTL_DP", "zero1") == "allreduce" or not hasattr(optimizer, "shard"):
+    mode = os.environ.get("NSTL_DP", "zero1")
+    if mode == "allreduce" or not hasattr(optimizer, "shard"):
         from ..parallel import GradAllReducer
         eng.grad_reducer = GradAllReducer(eng.g32)
     else:
         optimizer.shard()
+        if mode == "zero1_overlap":
+            from ..parallel import GradShardReducer, cede_cus
+            cede_cus(int(os.environ.get("NSTL_CEDE_CUS", "8")), eng.device)
+            eng.grad_reducer = GradShardReducer(eng.g32, optimizer._comm)
 
 
 def train_one_epoch_multi_gpu(epoch, models, dataloader, criterion, optimizer, devices, clip, batch_step=0,

@@ -93,7 +93,7 @@ def test_data_parallel_gloo(tmp_path, monkeypatch):
         torch.testing.assert_close(a[k], v, rtol=1e-5, atol=1e-6)
 
 
-def _shard_worker(rank, port, out_dir, world=WORLD):
+def _shard_worker(rank, port, out_dir, world=WORLD, overlap=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -121,7 +121,14 @@ def _shard_worker(rank, port, out_dir, world=WORLD):
         v[lo:lo + k] = 0.999 * v[lo:lo + k] + 0.001 * gg * gg
         p[lo:lo + k] -= 1e-3 / 0.1 * m[lo:lo + k] / ((v[lo:lo + k] / 0.001).sqrt() + 1e-8)
 
-    parallel.zero1_step(comm, grads, gs, partial, sumsq_fn, adam_fn, [p], tail=(ns, n))
+    if overlap:
+        # backward's arena prefixes become final in uneven steps; buckets of 1000
+        # elements (cut at the shard boundaries) are reduced as they complete
+        red = parallel.GradShardReducer(grads, comm, bucket_bytes=4000)
+        for upto in (700, 2500, 2600, 9000, 30001, ns // 2 + 7, ns - 5, n):
+            red.ready(upto)
+        red.finish()
+    parallel.zero1_step(comm, grads, gs, partial, sumsq_fn, adam_fn, [p], tail=(ns, n), reduced=overlap)
     for t in (m, v):
         comm.all_gather(t[:ns])  # consolidate
     torch.save({"p": p, "m": m, "v": v}, os.path.join(out_dir, "s%d.pt" % rank))
@@ -151,3 +158,25 @@ def test_sharded_optimizer_step_gloo(tmp_path, world):
     torch.testing.assert_close(r0["p"], p, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(r0["m"], m, rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(r0["v"], v, rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_overlapped_shard_reduce_is_bit_identical_gloo(tmp_path, world):
+    """NSTL_DP=zero1_overlap (parallel.GradShardReducer): the gradient shards
+    reduced bucket by bucket onto their owners while backward runs give the same
+    parameters and moments as the post-backward reduce-scatter: bit for bit at
+    two ranks (one addition either way), to f32 rounding at four (the backend's
+    reduce and reduce-scatter may add the four contributions in different
+    orders)."""
+    for overlap, sub in ((False, "rs"), (True, "ov")):
+        d = tmp_path / sub
+        d.mkdir()
+        mp.spawn(_shard_worker, args=(_port(), str(d), world, overlap), nprocs=world, join=True)
+    for r in range(world):
+        a = torch.load(tmp_path / "rs" / ("s%d.pt" % r), weights_only=True)
+        b = torch.load(tmp_path / "ov" / ("s%d.pt" % r), weights_only=True)
+        for k in a:
+            if world == 2:
+                assert torch.equal(a[k], b[k]), (r, k)
+            else:
+                torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-7)

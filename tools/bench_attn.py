@@ -53,6 +53,11 @@ for p in [float(x) for x in os.environ.get("NSTL_BENCH_P", "0.3,0.0").split(",")
         a.dsum = dsum.data_ptr()
         if mask is not None:
             a.mask_bits = mask.data_ptr()
+        if os.environ.get("NSTL_BENCH_BIAS", "1") == "1":   # fused q|k|v bias column sums, as the step
+            rows = K.attn_bias_rows(a)
+            if rows:
+                extra["part"] = torch.empty(rows, 3 * D, device=dev)
+                a.dbias_part = extra["part"].data_ptr()
         return a
     a = args()
     tf = t(lambda: K.attn_fwd(a))
