@@ -1421,18 +1421,6 @@ int launch(K kern, dim3 grid, size_t lds, hipStream_t st, const AttnParams& p, c
   return 0;
 }
 
-// compute units of the current device (the persistent grid's size)
-int cu_count() {
-  static int n[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (n[dev] == 0) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    n[dev] = v;
-  }
-  return n[dev];
-}
 
 // the persistent forward (bf16, T = 128, enough heads to fill the grid);
 // NSTL_ATTN_FWD=oneshot selects the one-workgroup-per-head kernel (A/B; read per call)
@@ -1469,7 +1457,7 @@ extern "C" int nstl_attn_fwd(const nstl_attn_args* a, void* stream) {
   nstl::count(NSTL_K_ATTN_FWD);
   if (use_persist_fwd(a)) {
     const int nitems = a->B * a->H;
-    const int G = std::min(nitems, 2 * cu_count());
+    const int G = std::min(nitems, std::max(2, 2 * nstl::stream_cus(st)));  // two workgroups per CU the stream may use
     const size_t lds = PF_LDS;
     if (p.thresh && p.mask)
       return launch(attn_fwd_persist_kernel<true>, dim3(G), lds, st, p, "nstl_attn_fwd persistent", FWD_NT, nitems);

@@ -1,11 +1,13 @@
 """Step time of the 228M training step on a compute stream that excludes k CUs
 (hipExtStreamCreateWithCUMask): what ceding CUs to RCCL's channel workgroups
-during backward would cost the step (the decision behind NSTL_DP, DESIGN.md
-section 5).  The excluded CUs are spread over the mask's bit positions (one
-per 256/k).  Every kernel of the step runs on the masked stream, so the ring
-GEMMs' single-round grids (256 tiles) take two rounds on 256 - k CUs; with
---persist-cus the persistent GEMM grid is sized to the CUs left.
-  python tools/cu_mask_bench.py [k ...]"""
+during backward costs the step (NSTL_DP=zero1_overlap).
+Mask bit i is a CU of XCD i % 8 (tools/micro/cu_probe.hip); pattern "first"
+(default) clears bits 0 .. k-1, i.e. ceil(k / 8) CUs on the first min(k, 8)
+XCDs -- one per XCD at k = 8.  The persistent grids take 8 x the fewest CUs left
+on one XCD (nstl_stream_cus) and the GEMM deals what does not divide into them
+stream-K.  "spread" clears one bit per 256 / k: all of them on XCD 0 (the
+round-3 table's pattern).
+  python tools/cu_mask_bench.py [k ...] [--pattern first|spread|last]"""
 import argparse
 import ctypes
 import json
@@ -41,7 +43,7 @@ def main():
     ap.add_argument("ks", nargs="*", type=int, default=[0, 2, 4, 8, 16, 32])
     ap.add_argument("--steps", type=int, default=15)
     ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--pattern", default="spread", choices=["spread", "first", "last"],
+    ap.add_argument("--pattern", default="first", choices=["spread", "first", "last"],
                     help="which mask bits are cleared: one per n/k (spread), the first k, or the last k")
     args = ap.parse_args()
     from neurosync_trainer_lite_amd.config import training_config
