@@ -376,18 +376,26 @@ NSTL_DEV void add_acc(f32x4& x, const f32x4 y) {
 struct Seg {
   int t, ks, ke;
 };
+// The tail's unit ranges go to the workgroups in XCD-contiguous order (rank =
+// xcd_remap(w)): the workgroups of one XCD take consecutive tiles, which
+// tile_coords lays out as a patch sharing A and B panels in that XCD's L2 (dealt
+// in workgroup order, an XCD's tiles were scattered over the whole output and
+// the GEMM ran 40-70 % slower).  Slab slots and the hand-off partner go by rank.
 struct Walker {
   int t_dp, G, dp_tiles, U;
+  int rank;      // position of this workgroup's range in the tail
   int pos, end;  // units: at most 2 G tiles x 64 (K = 16384) in the tail
   NSTL_DEV void init(const GroupParams& gp, int T, int w, int G_, bool sk) {
     G = G_;
     t_dp = w;
+    rank = w;
     if (sk) {
       dp_tiles = gp.sk.dp_tiles;
       U = gp.sk.units;
+      if (G % 8 == 0) rank = xcd_remap(w, G);
       const int I = (T - dp_tiles) * U;
-      pos = w * I / G;
-      end = (w + 1) * I / G;
+      pos = rank * I / G;
+      end = (rank + 1) * I / G;
     } else {
       dp_tiles = T;
       U = 1;
@@ -416,13 +424,13 @@ struct Walker {
 // finishes the block: a whole tile, or the second contributor (its accumulators
 // then hold the sum); the first contributor's epilogue runs with its stores off
 // (it zeroes the accumulators for the next segment).  The tile's head [0, ks)
-// belongs to the previous workgroup's range (its last segment, slot
-// 2 (w - 1) + 1), its tail to the next one's (first segment, slot 2 (w + 1)).
+// belongs to the previous range's workgroup (its last segment, slot
+// 2 (w - 1) + 1; w: the range's rank), its tail to the next one's (first
+// segment, slot 2 (w + 1)).
 // One straight-line pass whatever the case -- a branch over the accumulators
 // splits their live ranges and spills: stores and loads that do not apply go
 // through an empty buffer range (dropped; loads return 0).
-NSTL_DEV bool sk_handoff(const StreamK& sk, f32x4 (&acc)[8][8], const Seg& s, int wave, int lane) {
-  const int w = blockIdx.x;
+NSTL_DEV bool sk_handoff(const StreamK& sk, f32x4 (&acc)[8][8], const Seg& s, int w, int wave, int lane) {
   const bool part = !(s.ke < 0 || (s.ks == 0 && s.ke == sk.units));
   const bool tail = s.ks > 0;
   const uint32_t mine = (uint32_t)(tail ? 2 * w : 2 * w + 1), other = (uint32_t)(tail ? 2 * w - 1 : 2 * w + 2);
@@ -694,7 +702,10 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     const int first = prob ? gp.tile_end[prob - 1] : 0;
     const Params& q = gp.g[prob];
     lt = tt - first;
-    tile_coords(xcd_remap(lt, gp.tile_end[prob] - first), q.tiles_m, q.tiles_n, m0, n0);
+    // whole tiles: XCD-aware order over the problem's whole-tile part; the
+    // stream-K tail is XCD-contiguous by construction (Walker), in tile order
+    const int ndp = (SK ? min(gp.tile_end[prob], gp.sk.dp_tiles) : gp.tile_end[prob]) - first;
+    tile_coords(lt < ndp ? xcd_remap(lt, ndp) : lt, q.tiles_m, q.tiles_n, m0, n0);
   };
   int prob, m0, n0, lt;
   locate(sg.t, prob, m0, n0, lt);
@@ -781,7 +792,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
       }
     }
     bool fin = true;
-    if constexpr (SK) fin = sk_handoff(gp.sk, acc, sg, wave, lane);
+    if constexpr (SK) fin = sk_handoff(gp.sk, acc, sg, wk.rank, wave, lane);
     epilogue<EM>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, fin);
     if (!has_next) break;
     sg = ns;
