@@ -555,6 +555,10 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
 #pragma unroll
       for (int bp = 0; bp < 8; bp += 2) {
         f32x4 uv[2] = {rd_acc(acc[a][bp]), rd_acc(acc[a][bp + 1])};
+        if (!fin) {  // a stream-K first contributor: only the zeroing reads above
+          G4_SB();
+          continue;
+        }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const int b = bp + s;
@@ -609,7 +613,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
         const uint32_t y0 = pack_bf16x2(uv[1][0], uv[1][1]), y1 = pack_bf16x2(uv[1][2], uv[1][3]);
         const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-        if (fin) *(uint4*)(crow + 16 * (bp + odd) + 4 * (g - odd)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        *(uint4*)(crow + 16 * (bp + odd) + 4 * (g - odd)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         G4_SB();  // one (a, bp) group at a time: hoisting the accumulator reads spills
       }
     }

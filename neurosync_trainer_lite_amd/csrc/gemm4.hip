@@ -22,10 +22,14 @@ int gemm4_env() {
   return e ? atoi(e) : 1;
 }
 
-// NSTL_GEMM4_SK=0: no stream-K tail (a partial last round of whole tiles instead)
+// NSTL_GEMM4_SK=1: a stream-K tail when the grid does not divide the tiles
+// (default 0: a partial last round of whole tiles, measured faster on every
+// shape but the long-K weight gradients, profiles/r4_sk_bench_v2.txt); 2: the
+// stream-K instantiation also when the grid divides the tiles (every tail range
+// one whole tile: its cost without hand-offs; timing only)
 int sk_env() {
   const char* e = getenv("NSTL_GEMM4_SK");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }
 
 // the stream-K slabs and tickets, per (device, stream): launches on different
@@ -66,7 +70,8 @@ bool sk_space(hipStream_t st, int G, g4::StreamK& sk) {
 void plan_sk(g4::GroupParams& gp, int G, hipStream_t st) {
   memset(&gp.sk, 0, sizeof(gp.sk));
   const int T = gp.tile_end[gp.n - 1];
-  if (T <= G || T % G == 0 || !sk_env()) return;
+  const int mode = sk_env();  // 2: the stream-K instantiation even when G divides T (timing only)
+  if (T < G || !mode || (T % G == 0 && mode != 2)) return;
   const int K = gp.g[0].K;
   for (int i = 0; i < gp.n; ++i)
     if (gp.g[i].K != K) return;

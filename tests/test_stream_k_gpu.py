@@ -6,7 +6,9 @@ leaves on one XCD.  When that grid does not divide the tile count, the last
 G + T % G tiles are dealt stream-K (csrc/gemm4.h StreamK): every workgroup a
 contiguous, equal range of 256-deep K units, a split tile's two partials summed
 by its second contributor.  NSTL_PERSIST_CUS caps the grid so the tail runs on
-an unmasked stream too.  Split tiles add two f32 partials (x + y, the same
+an unmasked stream too (NSTL_GEMM4_SK=1 turns the tail on: it is off by
+default, measured slower than a partial round of whole tiles on most shapes,
+DESIGN.md section 5).  Split tiles add two f32 partials (x + y, the same
 whichever arrives last), so f32 outputs agree with the whole-tile run to f32
 rounding and bf16 outputs to one rounding step in rare elements; both are held
 to float64.
@@ -43,6 +45,7 @@ def rel_err(got, ref):
 
 def sk_and_whole(monkeypatch, fn, cus):
     """fn() on a grid capped to `cus` workgroups (stream-K tail), then on the full grid."""
+    monkeypatch.setenv("NSTL_GEMM4_SK", "1")
     monkeypatch.setenv("NSTL_PERSIST_CUS", str(cus))
     K.kernel_counts_reset()
     a = fn()
@@ -210,6 +213,8 @@ def test_masked_stream_grid_and_gemm():
     """A stream that cedes one CU per XCD (mask bits 0..7) runs 8 fewer persistent
     workgroups; one ceding two CUs of XCD 0 (bits 0 and 8) runs 8 fewer too (the
     fewest per XCD, times 8); the GEMM on it takes the stream-K tail."""
+    import os
+    os.environ["NSTL_GEMM4_SK"] = "1"
     s1, n = masked_stream(set(range(8)))
     s2, _ = masked_stream({0, 8})
     assert K.stream_cus(torch.cuda.current_stream().cuda_stream) == n
@@ -224,5 +229,6 @@ def test_masked_stream_grid_and_gemm():
         K.gemm(X, W, C, M, N, Kd)
     s1.synchronize()
     c = K.kernel_counts()
+    del os.environ["NSTL_GEMM4_SK"]
     assert c["gemm4"] == 1 and c["gemm4_sk"] == 1, c
     assert rel_err(C, f64(X) @ f64(W).T) < 1e-5

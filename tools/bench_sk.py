@@ -1,6 +1,9 @@
-"""GEMM time against the persistent grid size (NSTL_PERSIST_CUS caps it; read
-per call): whole-tile rounds at 256 workgroups, the stream-K tail below.
-The step's shapes (M = 16,384 tokens).  python tools/bench_sk.py [cus ...]"""
+"""GEMM time against the persistent grid size: the step's shapes (M = 16,384
+tokens) on 256 workgroups, on fewer (NSTL_PERSIST_CUS caps the grid; read per
+call) with the stream-K tail (NSTL_GEMM4_SK=1) or whole-tile rounds
+(NSTL_GEMM4_SK=0), and on a CU-masked stream ceding 8 CUs (one per XCD).
+  python tools/bench_sk.py [cus ...]"""
+import ctypes
 import os
 import sys
 
@@ -14,14 +17,27 @@ bf = torch.bfloat16
 M = 16384
 
 
-def t(fn, reps=20):
-    for _ in range(3):
-        fn()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for a, b in ev:
-        a.record()
-        fn()
-        b.record()
+def masked_stream(k):
+    fn = ctypes.CDLL(K.LIB_PATH).hipExtStreamCreateWithCUMask
+    fn.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    n = torch.cuda.get_device_properties(0).multi_processor_count
+    mask = (ctypes.c_uint32 * ((n + 31) // 32))()
+    for c in range(k, n):
+        mask[c // 32] |= 1 << (c % 32)
+    st = ctypes.c_void_p()
+    assert fn(ctypes.byref(st), (n + 31) // 32, mask) == 0
+    return torch.cuda.ExternalStream(st.value, device=dev)
+
+
+def t(fn, stream, reps=20):
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in ev:
+            a.record()
+            fn()
+            b.record()
     torch.cuda.synchronize()
     ts = sorted(a.elapsed_time(b) for a, b in ev)
     return ts[len(ts) // 2] * 1e3
@@ -32,18 +48,27 @@ for name, n, k in [("fwd ffn2", 1024, 4096), ("fwd ffn1", 4096, 1024), ("fwd qkv
     X = torch.randn(M, k, device=dev).to(bf)
     W = (torch.randn(n, k, device=dev) * 0.05).to(bf)
     C = torch.empty(M, n, dtype=bf, device=dev)
-    cases.append((name, 2.0 * M * n * k, lambda X=X, W=W, C=C, n=n, k=k: K.gemm(X, W, C, M, n, k)))
+    cases.append((name, lambda X=X, W=W, C=C, n=n, k=k: K.gemm(X, W, C, M, n, k)))
 dY = torch.randn(M, 4096, device=dev).to(bf)
 Xa = torch.randn(M, 4096, device=dev).to(bf)
 G = torch.empty(4096, 4096, device=dev)
-cases.append(("dW 4096^2", 2.0 * M * 4096 * 4096,
-              lambda: K.gemm(dY, Xa, G, 4096, 4096, M, a_kmajor=False, b_kmajor=False)))
-cus = [int(x) for x in sys.argv[1:]] or [256, 248, 240, 224]
-print("%-10s" % "" + "".join("%14s" % ("%d WGs" % c) for c in cus))
-for name, fl, fn in cases:
+cases.append(("dW 4096^2", lambda: K.gemm(dY, Xa, G, 4096, 4096, M, a_kmajor=False, b_kmajor=False)))
+main = torch.cuda.current_stream()
+m8 = masked_stream(8)
+arms = [("256", main, {}), ("256 SK inst", main, {"NSTL_GEMM4_SK": "2"}), ("248 SK", main, {"NSTL_PERSIST_CUS": "248", "NSTL_GEMM4_SK": "1"}),
+        ("248 whole", main, {"NSTL_PERSIST_CUS": "248", "NSTL_GEMM4_SK": "0"}),
+        ("mask8 SK", m8, {"NSTL_GEMM4_SK": "1"}), ("mask8 whole", m8, {"NSTL_GEMM4_SK": "0"}),
+        ("mask8 G240", m8, {"NSTL_PERSIST_CUS": "240"}), ("mask8 G224", m8, {"NSTL_PERSIST_CUS": "224"}),
+        ("mask8 G256", m8, {"NSTL_PERSIST_CUS": "256"})]
+print("stream_cus: main %d, mask8 %d" % (K.stream_cus(main.cuda_stream), K.stream_cus(m8.cuda_stream)))
+print("%-10s" % "" + "".join("%16s" % a[0] for a in arms))
+for name, fn in cases:
     row = []
-    for c in cus:
-        os.environ["NSTL_PERSIST_CUS"] = str(c)
-        row.append(t(fn))
-    os.environ.pop("NSTL_PERSIST_CUS", None)
-    print("%-10s" % name + "".join("%8.1f us %+4.0f%%" % (x, 100 * (x / row[0] - 1)) for x in row))
+    for _, st, env in arms:
+        for kk in ("NSTL_PERSIST_CUS", "NSTL_GEMM4_SK"):
+            os.environ.pop(kk, None)
+        os.environ.update(env)
+        row.append(t(fn, st))
+    for kk in ("NSTL_PERSIST_CUS", "NSTL_GEMM4_SK"):
+        os.environ.pop(kk, None)
+    print("%-10s" % name + "".join("%9.1f %+5.0f%%" % (x, 100 * (x / row[0] - 1)) for x in row))
