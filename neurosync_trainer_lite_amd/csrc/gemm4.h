@@ -545,6 +545,17 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
 #pragma unroll
       for (int e = 0; e < 4; ++e) csum[b][e] = 0.f;
     const int rope_rb = p.rope_dim * 4;  // bytes per table row in LDS
+    // RoPE: the lane's table chunk per column block (col % rope_dim) / 4, once
+    // per tile (a power-of-two rope_dim, the production case: a mask)
+    int rchunk[8];
+    if constexpr (EM == EM_ROPE) {
+      const bool pow2 = (p.rope_dim & (p.rope_dim - 1)) == 0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int col = col0 + 16 * b + 4 * g;
+        rchunk[b] = (pow2 ? col & (p.rope_dim - 1) : col % p.rope_dim) >> 2;
+      }
+    }
     bf16* const cbase = (bf16*)p.C + (int64_t)(row0 + c) * p.ldc + col0;
 #pragma unroll
     for (int a = 0; a < 8; ++a) {
@@ -552,6 +563,13 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       bf16* crow = cbase + (int64_t)(16 * a) * p.ldc;
       // position of the row (a power-of-two T, the production case: a mask)
       const int t = EM != EM_ROPE ? 0 : ((p.rope_T & (p.rope_T - 1)) == 0 ? row & (p.rope_T - 1) : row % p.rope_T);
+      // RoPE: the row's 8 table reads issued together (one at the point of use
+      // exposed an LDS round trip per 4 outputs)
+      f32x4 rcs[8];
+      if constexpr (EM == EM_ROPE) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) rcs[b] = *(const f32x4*)(rope_lds + rope_off(t, rchunk[b], rope_rb));
+      }
 #pragma unroll
       for (int bp = 0; bp < 8; bp += 2) {
         f32x4 uv[2] = {rd_acc(acc[a][bp]), rd_acc(acc[a][bp + 1])};
@@ -591,7 +609,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
 #pragma clang fp contract(off)
             if (col < p.rope_cols) {
               // pairs (col, col + 1), (col + 2, col + 3): chunk (col % rope_dim) / 4
-              const f32x4 cs = *(const f32x4*)(rope_lds + rope_off(t, (col % p.rope_dim) >> 2, rope_rb));
+              const f32x4 cs = rcs[b];
               const float x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
               v[0] = x0 * cs[0] - x1 * cs[1];
               v[1] = x0 * cs[1] + x1 * cs[0];

@@ -104,7 +104,7 @@ int g4_mode(const nstl_gemm_args* a) {
     case NSTL_EPI_BIAS_RELU_DROP:
       return bf_out && (a->N & 1) == 0 ? g4::EM_RELU_DROP : 0;
     case NSTL_EPI_BIAS_ROPE:
-      return bf_out && a->rope_dim % 4 == 0 && a->rope_cols % 16 == 0 &&
+      return bf_out && a->b_kmajor && a->rope_dim % 4 == 0 && a->rope_cols % 16 == 0 &&
                      (int64_t)a->rope_T * a->rope_dim * 4 <= g4::ROPE_LDS
                  ? g4::EM_ROPE
                  : 0;
@@ -160,7 +160,9 @@ void launch_em(int em, dim3 grid, hipStream_t st, const g4::GroupParams& gp) {
     case g4::EM_RELU_DROP:
       hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_RELU_DROP, GROUPED, 0, SK>), grid, block, 0, st, gp);
       break;
-    case g4::EM_ROPE: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_ROPE, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
+    case g4::EM_ROPE:  // the q|k|v forward (TT) only: g4_mode takes RoPE with a K-major B
+      if constexpr (BKM) hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_ROPE, GROUPED, 0, SK>), grid, block, 0, st, gp);
+      break;
     case g4::EM_DRELU: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_DRELU, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
     default: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_F32, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
   }
