@@ -1828,18 +1828,6 @@ int getenv_pq() {
   return v;
 }
 
-// CUs of the current device (the persistent grid: one workgroup per CU)
-int device_cus() {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cus[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    cus[dev] = n;
-  }
-  return cus[dev];
-}
 
 // the persistent kernel's split-tile slots: one 256 KB f32 slot per workgroup,
 // owned by the library per (device, stream) so launches on different streams
@@ -1847,11 +1835,11 @@ int device_cus() {
 f32x4* persist_slots(hipStream_t st, int G) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, std::pair<f32x4*, int>> slots;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  const int dev = nstl::stream_device(st);  // the stream's device, not the current one
   std::lock_guard<std::mutex> lk(mu);
   auto& e = slots[{dev, st}];
   if (e.second < G) {
+    nstl::DeviceGuard on(dev);
     if (e.first) (void)hipFree(e.first);
     e.first = nullptr;
     e.second = 0;
@@ -1891,7 +1879,7 @@ int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t s
     const int hmode = getenv_gemm_h();
     if (hmode && splits == 1 && a->a_kmajor) {
       const int nth = ((a->M + H_BM - 1) / H_BM) * ((a->N + BIG - 1) / BIG);
-      const int G = 2 * device_cus();
+      const int G = 2 * nstl::stream_cus(st);
       const bool multi = em != EM_GENERIC && em != EM_WS && G > 0 && nth % G == 0 && nth / G >= 2 &&
                          a->K % (4 * R_BK) == 0;
       if (hmode == 1 || multi) {
@@ -1913,7 +1901,7 @@ int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t s
     // NSTL_GEMM_PQ=1: multi-round bf16 problems with the plain (bias) epilogue on
     // full tiles run on the persistent cross-tile pipelined kernel
     {
-      const int G = device_cus();
+      const int G = nstl::stream_cus(st);
       if (getenv_pq() && splits == 1 && em == EM_BF16 && p.direct_epi && a->M % BIG == 0 && a->N % BIG == 0 &&
           G > 0 && nt % G == 0 && nt / G >= (getenv_pq() == 2 ? 1 : 2) && a->K % R_BK == 0 && a->K / R_BK >= 6 &&
           a->a_kmajor && p.debug_skip_epilogue == 0) {
@@ -1927,7 +1915,7 @@ int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t s
       }
     }
     // multi-round problems with a lean epilogue: the persistent XCD-phased kernel
-    const int G = device_cus();
+    const int G = nstl::stream_cus(st);
     const bool lean = em == EM_BF16 || em == EM_RELU_DROP || em == EM_ROPE || em == EM_DRELU || em == EM_F32;
     if (getenv_persist() && splits == 1 && lean && (a->a_kmajor || !a->b_kmajor) && G > 0 && nt % G == 0 &&
         nt / G >= 2 && a->K % (8 * R_BK) == 0) {

@@ -43,11 +43,11 @@ struct SkSpace {
 bool sk_space(hipStream_t st, int G, g4::StreamK& sk) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, SkSpace> spaces;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
+  const int dev = nstl::stream_device(st);  // the stream's device, not the current one
   std::lock_guard<std::mutex> lk(mu);
   SkSpace& s = spaces[{dev, st}];
   if (s.G < G) {
+    nstl::DeviceGuard on(dev);
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
     if (hipStreamSynchronize(st) != hipSuccess) return false;  // the old space may be in use

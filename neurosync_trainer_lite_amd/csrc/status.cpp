@@ -28,10 +28,18 @@ void count(int which, long long n) {
   if (which >= 0 && which < NSTL_K_COUNT) g_counts[which].fetch_add(n, std::memory_order_relaxed);
 }
 
+int stream_device(hipStream_t st) {
+  int dev = 0;
+  if (st != nullptr && hipStreamGetDevice(st, &dev) == hipSuccess) return dev;
+  (void)hipGetLastError();
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  return dev;
+}
+
 int stream_cus(hipStream_t st) {
   static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  const int dev = stream_device(st);
+  if (dev < 0 || dev >= 64) return 0;
   if (cus[dev] == 0) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 0;

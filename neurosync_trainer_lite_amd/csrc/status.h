@@ -15,6 +15,21 @@ void count(int which, long long n = 1);  // nstl_kernel_counts (NSTL_K_*)
 // round-robin, so an XCD with fewer CUs than its share would run a second
 // round).  NSTL_PERSIST_CUS=<n> caps it (tests of the stream-K tail).
 int stream_cus(hipStream_t st);
+// The device a stream belongs to (hipStreamGetDevice; the current device for
+// the null stream or on failure): per-device workspaces are keyed and allocated
+// on it, not on whatever device is current when a call is made.
+int stream_device(hipStream_t st);
+// makes `dev` current for its scope (allocations for another device's stream)
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 }  // namespace nstl
 
 #define NSTL_CHECK_ARG(cond, ...)                                         \
