@@ -715,19 +715,24 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     __syncthreads();
   }
 
-  // tile index -> (problem, m0, n0); XCD-aware order within each problem
-  // (and the tile's index within its problem: sq_part is per problem)
+  // tile index -> (problem, m0, n0) and the tile's index within its problem
+  // (sq_part is per problem).  The XCD-aware remap runs over the launch's whole
+  // list of whole tiles, problems concatenated: XCD x's concurrent tiles are
+  // consecutive ids, i.e. one or two problems in compact patches (tile_coords).
+  // Remapped per problem instead, every problem was spread over all 8 XCDs, each
+  // taking a thin slice that needed most of the problem's A panels: the grouped
+  // weight gradients fetched 2.6x their algorithmic bytes.  The stream-K tail is
+  // XCD-contiguous by construction (Walker), in tile order.
+  const int ndp_all = SK ? gp.sk.dp_tiles : T;
   auto locate = [&](int tt, int& prob, int& m0, int& n0, int& lt) {
+    const int gt = tt < ndp_all ? xcd_remap(tt, ndp_all) : tt;
     prob = 0;
     if (GROUPED)
-      while (prob + 1 < gp.n && tt >= gp.tile_end[prob]) ++prob;
+      while (prob + 1 < gp.n && gt >= gp.tile_end[prob]) ++prob;
     const int first = prob ? gp.tile_end[prob - 1] : 0;
     const Params& q = gp.g[prob];
-    lt = tt - first;
-    // whole tiles: XCD-aware order over the problem's whole-tile part; the
-    // stream-K tail is XCD-contiguous by construction (Walker), in tile order
-    const int ndp = (SK ? min(gp.tile_end[prob], gp.sk.dp_tiles) : gp.tile_end[prob]) - first;
-    tile_coords(lt < ndp ? xcd_remap(lt, ndp) : lt, q.tiles_m, q.tiles_n, m0, n0);
+    lt = gt - first;
+    tile_coords(lt, q.tiles_m, q.tiles_n, m0, n0);
   };
   int prob, m0, n0, lt;
   locate(sg.t, prob, m0, n0, lt);
