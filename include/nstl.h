@@ -354,9 +354,10 @@ enum {
   NSTL_K_COUNT
 };
 /* Workgroups a persistent one-per-CU grid launches on `stream` (the GEMM and
- * attention-forward grids): 8 x the fewest CUs the stream's CU mask leaves on one
- * XCD (mask bit i = a CU of XCD i % 8).  A compute stream that cedes CUs to the
- * gradient collectives should cede them evenly over the XCDs. */
+ * attention-forward grids): 32 x the fewest CUs the stream's CU mask leaves on
+ * one (XCD, shader engine) pair (mask bit i = a CU of XCD i % 8, SE (i / 8) % 4).
+ * A compute stream that cedes CUs to the gradient collectives should cede them
+ * evenly over the 32 pairs (multiples of 32 mask bits from bit 0). */
 int nstl_stream_cus(void* stream);
 /* Copies min(n, NSTL_K_COUNT) counters to out; returns NSTL_K_COUNT. */
 int nstl_kernel_counts(int64_t* out, int n);

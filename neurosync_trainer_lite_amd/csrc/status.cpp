@@ -49,12 +49,15 @@ int stream_cus(hipStream_t st) {
   int g = ncu;
   uint32_t m[32] = {0};
   const int words = (ncu + 31) / 32;
-  if (ncu % 8 == 0 && words <= 32 && hipExtStreamGetCUMask(st, (uint32_t)words, m) == hipSuccess) {
-    int per[8] = {0};
-    for (int i = 0; i < ncu; ++i) per[i % 8] += (m[i / 32] >> (i % 32)) & 1;
+  if (ncu % 32 == 0 && words <= 32 && hipExtStreamGetCUMask(st, (uint32_t)words, m) == hipSuccess) {
+    // mask bit i: XCD i % 8, shader engine (i / 8) % 4 (tools/micro/cu_probe.hip);
+    // workgroups are dealt round-robin over the XCDs and, inside one, over its 4
+    // shader engines, so the grid is 32 x the fewest CUs of any (XCD, SE)
+    int per[32] = {0};
+    for (int i = 0; i < ncu; ++i) per[(i % 8) * 4 + (i / 8) % 4] += (m[i / 32] >> (i % 32)) & 1;
     int lo = per[0];
-    for (int x = 1; x < 8; ++x) lo = per[x] < lo ? per[x] : lo;
-    if (lo > 0) g = 8 * lo;
+    for (int x = 1; x < 32; ++x) lo = per[x] < lo ? per[x] : lo;
+    if (lo > 0) g = 32 * lo;
   } else {
     (void)hipGetLastError();  // no mask (or not queryable): every CU
   }

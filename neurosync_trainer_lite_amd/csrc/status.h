@@ -9,11 +9,12 @@ namespace nstl {
 void set_error(const std::string& msg);
 int fail(int code, const char* fmt, ...);
 void count(int which, long long n = 1);  // nstl_kernel_counts (NSTL_K_*)
-// Workgroups a persistent one-per-CU grid may launch on stream `st`: 8 x the
-// fewest CUs the stream's CU mask leaves on any of the 8 XCDs (mask bit i is a
-// CU of XCD i % 8, tools/micro/cu_probe.hip; workgroups are dealt to the XCDs
-// round-robin, so an XCD with fewer CUs than its share would run a second
-// round).  NSTL_PERSIST_CUS=<n> caps it (tests of the stream-K tail).
+// Workgroups a persistent one-per-CU grid may launch on stream `st`: 32 x the
+// fewest CUs the stream's CU mask leaves on any (XCD, shader engine) pair (mask
+// bit i is a CU of XCD i % 8, SE (i / 8) % 4, tools/micro/cu_probe.hip;
+// workgroups are dealt round-robin over the XCDs and their SEs, so one with
+// fewer CUs than its share would run a second round).  NSTL_PERSIST_CUS=<n>
+// caps it (tests of the stream-K tail).
 int stream_cus(hipStream_t st);
 // The device a stream belongs to (hipStreamGetDevice; the current device for
 // the null stream or on failure): per-device workspaces are keyed and allocated

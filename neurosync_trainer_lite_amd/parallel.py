@@ -32,9 +32,9 @@ shard holds it, on RCCL's stream, so the reduce-scatter leaves the critical
 path; buckets never straddle a shard boundary, and the post-backward step skips
 its reduce-scatter.  A collective kernel resident during backward holds CUs the
 step's persistent grids would otherwise use: run the compute stream on a CU
-mask that cedes them evenly over the XCDs (NSTL_CEDE_CUS, one CU per XCD at 8;
-nstl_stream_cus then sizes the GEMM / attention grids to the CUs left, and
-the GEMM's stream-K tail keeps the cost near k / 256, tools/cu_mask_bench.py).
+mask that cedes them evenly over the XCD shader engines (NSTL_CEDE_CUS, one CU per (XCD, SE) at 32;
+nstl_stream_cus then sizes the GEMM / attention grids to the CUs left;
+tools/cu_mask_bench.py measures what that costs).
 """
 import os
 
@@ -73,10 +73,11 @@ _CEDED = {}
 
 def cede_cus(k, device):
     """Make the current stream of `device` a stream whose CU mask leaves out mask
-    bits 0 .. k-1 -- bit i is a CU of XCD i % 8 (tools/micro/cu_probe.hip), so k
-    a multiple of 8 cedes k / 8 CUs on every XCD -- for the collective kernels
-    that run during backward (NSTL_DP=zero1_overlap).  Returns the stream (kept
-    alive here); k <= 0 leaves the current stream."""
+    bits 0 .. k-1 -- bit i is a CU of XCD i % 8, shader engine (i / 8) % 4
+    (tools/micro/cu_probe.hip), so k a multiple of 32 cedes k / 32 CUs of every
+    (XCD, SE) pair, the only balanced choices -- for the collective kernels that
+    run during backward (NSTL_DP=zero1_overlap).  Returns the stream (kept alive
+    here); k <= 0 leaves the current stream."""
     if k <= 0:
         return torch.cuda.current_stream(device)
     import ctypes

@@ -188,7 +188,7 @@ def attach_data_parallel(model, optimizer, world):
     NSTL_DP=zero1 (default: the sharded optimizer, no collective during
     backward), zero1_overlap (the same with each shard reduced onto its owner
     bucket by bucket during backward, the compute stream ceding NSTL_CEDE_CUS
-    CUs, 8 by default, to the collectives) or allreduce (bucketed all-reduce
+    CUs, 32 by default (one per XCD shader engine), to the collectives) or allreduce (bucketed all-reduce
     during backward, replicated optimizer)."""
     eng = _engine_of(model)
     if eng is None or world == 1 or eng.grad_scale_t is not None:
@@ -203,7 +203,7 @@ def attach_data_parallel(model, optimizer, world):
         optimizer.shard()
         if mode == "zero1_overlap":
             from ..parallel import GradShardReducer, cede_cus
-            cede_cus(int(os.environ.get("NSTL_CEDE_CUS", "8")), eng.device)
+            cede_cus(int(os.environ.get("NSTL_CEDE_CUS", "32")), eng.device)
             eng.grad_reducer = GradShardReducer(eng.g32, optimizer._comm)
 
 

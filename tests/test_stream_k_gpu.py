@@ -210,16 +210,17 @@ def masked_stream(excluded):
 
 
 def test_masked_stream_grid_and_gemm():
-    """A stream that cedes one CU per XCD (mask bits 0..7) runs 8 fewer persistent
-    workgroups; one ceding two CUs of XCD 0 (bits 0 and 8) runs 8 fewer too (the
-    fewest per XCD, times 8); the GEMM on it takes the stream-K tail."""
+    """Mask bit i is a CU of XCD i % 8, shader engine (i / 8) % 4: a stream ceding
+    one CU of every (XCD, SE) pair (bits 0..31) runs 32 fewer persistent
+    workgroups, and so does one ceding a single CU (bit 0: that SE's share
+    sets the grid); the GEMM on it takes the stream-K tail."""
     import os
     os.environ["NSTL_GEMM4_SK"] = "1"
-    s1, n = masked_stream(set(range(8)))
-    s2, _ = masked_stream({0, 8})
+    s1, n = masked_stream(set(range(32)))
+    s2, _ = masked_stream({0})
     assert K.stream_cus(torch.cuda.current_stream().cuda_stream) == n
-    assert K.stream_cus(s1.cuda_stream) == n - 8
-    assert K.stream_cus(s2.cuda_stream) == n - 16
+    assert K.stream_cus(s1.cuda_stream) == n - 32
+    assert K.stream_cus(s2.cuda_stream) == n - 32
     M, N, Kd = 4096, 4096, 1024
     X, W = rnd(M, Kd, dtype=bf, seed=50), rnd(N, Kd, dtype=bf, scale=0.05, seed=51)
     C = torch.empty(M, N, dtype=torch.float32, device=DEV)
