@@ -244,6 +244,37 @@ int main(int argc, char** argv) {
       printf("  abl dW 4096^2 K=16384 dbg %d %-20s %8.1f us  %7.1f TF/s\n", a.dbg, a.what, us, fl / us * 1e-6);
     }
   }
+  {  // dW 4096^2 (K = 15360 tokens) with padded operand row strides: do power-of-two
+     // strides of the MN-major operands (the token rows) cost DMA intake?  timing only
+    const int Mt = 15360, n = 4096, k = 4096;
+    float* Cf;
+    CK(hipMalloc(&Cf, (size_t)n * k * 4));
+    for (int pad : {0, 64, 128, 256}) {
+      // both operands live in maxA-element buffers: a padded stride must still fit
+      // (a range past the allocation reads unmapped memory and faults the card)
+      if ((int64_t)Mt * (std::max(n, k) + pad) > maxA) continue;
+      g4::GroupParams gp{};
+      g4::Params& p = gp.g[0];
+      p.A = (const char*)A; p.lda = n + pad; p.B = (const char*)B; p.ldb = k + pad;
+      p.C = (char*)Cf; p.ldc = k; p.M = n; p.N = k; p.K = Mt; p.alpha = 1.f;
+      p.a_bytes = (uint32_t)((int64_t)Mt * (n + pad) * 2); p.b_bytes = (uint32_t)((int64_t)Mt * (k + pad) * 2);
+      p.tiles_m = n / 256; p.tiles_n = k / 256;
+      gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
+      auto run = [&]() {
+        hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 0>), dim3(256), dim3(g4::NT), 0, st, gp);
+      };
+      for (int w = 0; w < 3; ++w) run();
+      std::vector<float> ts;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0, st)); run(); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+      }
+      std::sort(ts.begin(), ts.end());
+      const double us = ts[reps / 2] * 1e3, fl = 2.0 * n * k * Mt;
+      printf("  dW 4096^2 K=15360 operand stride +%3d elements %8.1f us  %7.1f TF/s\n", pad, us, fl / us * 1e-6);
+      fflush(stdout);
+    }
+  }
   {  // early DMA on the forward / dX shapes
     for (int bkm = 1; bkm >= 0; --bkm)
       for (int dbg : {0, 16}) {
