@@ -359,6 +359,10 @@ enum {
  * A compute stream that cedes CUs to the gradient collectives should cede them
  * evenly over the 32 pairs (multiples of 32 mask bits from bit 0). */
 int nstl_stream_cus(void* stream);
+/* The rule nstl_stream_cus applies to a CU mask of `ncu` bits (host only, no
+ * device needed): 32 x the fewest set bits of any (XCD, SE) pair; 0 when ncu is
+ * not a multiple of 32. */
+int nstl_mask_grid(const uint32_t* mask, int ncu);
 /* Copies min(n, NSTL_K_COUNT) counters to out; returns NSTL_K_COUNT. */
 int nstl_kernel_counts(int64_t* out, int n);
 void nstl_kernel_counts_reset(void);

@@ -118,7 +118,7 @@ EXPORTS = [
     "nstl_loss_fwd_bwd", "nstl_sumsq", "nstl_adam_step", "nstl_clip_coef", "nstl_cast", "nstl_copy2d", "nstl_autocorr",
     "nstl_features", "nstl_stft_mel", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
     "nstl_version", "nstl_fp8_quant_rows", "nstl_fp8_quant_cols", "nstl_kernel_counts", "nstl_kernel_counts_reset",
-    "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs", "nstl_transpose_bf16", "nstl_stream_cus",
+    "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs", "nstl_transpose_bf16", "nstl_stream_cus", "nstl_mask_grid",
 ]
 
 # nstl_kernel_counts order (NSTL_K_* in include/nstl.h)
@@ -184,6 +184,8 @@ def lib():
         L.nstl_kernel_counts_reset.restype = None
         L.nstl_stream_cus.argtypes = [_vp]
         L.nstl_stream_cus.restype = _i32
+        L.nstl_mask_grid.argtypes = [_vp, _i32]
+        L.nstl_mask_grid.restype = _i32
         _lib = L
     return _lib
 
@@ -221,6 +223,16 @@ def kernel_counts():
 
 def kernel_counts_reset():
     lib().nstl_kernel_counts_reset()
+
+
+def mask_grid(excluded, ncu=256):
+    """nstl_mask_grid: the persistent grid a CU mask clearing `excluded` bits allows."""
+    words = (ncu + 31) // 32
+    m = (ctypes.c_uint32 * words)()
+    for c in range(ncu):
+        if c not in excluded:
+            m[c // 32] |= 1 << (c % 32)
+    return lib().nstl_mask_grid(m, ncu)
 
 
 def stream_cus(stream=None):

@@ -28,6 +28,21 @@ void count(int which, long long n) {
   if (which >= 0 && which < NSTL_K_COUNT) g_counts[which].fetch_add(n, std::memory_order_relaxed);
 }
 
+}  // namespace nstl
+
+// mask bit i: XCD i % 8, shader engine (i / 8) % 4 (tools/micro/cu_probe.hip);
+// workgroups are dealt round-robin over the XCDs and, inside one, over its 4
+// shader engines, so a one-per-CU grid is 32 x the fewest CUs of any (XCD, SE)
+extern "C" int nstl_mask_grid(const uint32_t* mask, int ncu) {
+  if (mask == nullptr || ncu <= 0 || ncu % 32) return 0;
+  int per[32] = {0};
+  for (int i = 0; i < ncu; ++i) per[(i % 8) * 4 + (i / 8) % 4] += (mask[i / 32] >> (i % 32)) & 1;
+  int lo = per[0];
+  for (int x = 1; x < 32; ++x) lo = per[x] < lo ? per[x] : lo;
+  return 32 * lo;
+}
+
+namespace nstl {
 int stream_device(hipStream_t st) {
   int dev = 0;
   if (st != nullptr && hipStreamGetDevice(st, &dev) == hipSuccess) return dev;
@@ -50,14 +65,8 @@ int stream_cus(hipStream_t st) {
   uint32_t m[32] = {0};
   const int words = (ncu + 31) / 32;
   if (ncu % 32 == 0 && words <= 32 && hipExtStreamGetCUMask(st, (uint32_t)words, m) == hipSuccess) {
-    // mask bit i: XCD i % 8, shader engine (i / 8) % 4 (tools/micro/cu_probe.hip);
-    // workgroups are dealt round-robin over the XCDs and, inside one, over its 4
-    // shader engines, so the grid is 32 x the fewest CUs of any (XCD, SE)
-    int per[32] = {0};
-    for (int i = 0; i < ncu; ++i) per[(i % 8) * 4 + (i / 8) % 4] += (m[i / 32] >> (i % 32)) & 1;
-    int lo = per[0];
-    for (int x = 1; x < 32; ++x) lo = per[x] < lo ? per[x] : lo;
-    if (lo > 0) g = 32 * lo;
+    const int mg = nstl_mask_grid(m, ncu);
+    if (mg > 0) g = mg;
   } else {
     (void)hipGetLastError();  // no mask (or not queryable): every CU
   }
