@@ -275,6 +275,38 @@ int main(int argc, char** argv) {
       fflush(stdout);
     }
   }
+  {  // dW at K = 16384 vs 15360 and 3840^2 vs 4096^2: is the K = 16384 slowdown the
+     // operands' size (256 MB, the Infinity Cache) or the K extent?  timing only
+    struct DS { int n, Mt; };
+    const DS ds[] = {{4096, 16384}, {4096, 15360}, {3840, 16384}, {3840, 15360}, {4096, 8192}};
+    float* Cf;
+    CK(hipMalloc(&Cf, (size_t)4096 * 4096 * 4));
+    for (const DS& d : ds) {
+      if ((int64_t)d.Mt * d.n > maxA) continue;  // both operands live in maxA-element buffers
+      g4::GroupParams gp{};
+      g4::Params& p = gp.g[0];
+      p.A = (const char*)A; p.lda = d.n; p.B = (const char*)B; p.ldb = d.n;
+      p.C = (char*)Cf; p.ldc = d.n; p.M = d.n; p.N = d.n; p.K = d.Mt; p.alpha = 1.f;
+      p.a_bytes = (uint32_t)((int64_t)d.Mt * d.n * 2); p.b_bytes = p.a_bytes;
+      p.tiles_m = d.n / 256; p.tiles_n = d.n / 256;
+      gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
+      const int grid = std::min(256, gp.tile_end[0]);
+      auto run = [&]() {
+        hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 0>), dim3(grid), dim3(g4::NT), 0, st, gp);
+      };
+      for (int w = 0; w < 3; ++w) run();
+      std::vector<float> ts;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0, st)); run(); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+      }
+      std::sort(ts.begin(), ts.end());
+      const double us = ts[reps / 2] * 1e3, fl = 2.0 * d.n * d.n * d.Mt;
+      printf("  dW %dx%d K=%d (operands %.0f MB)  %8.1f us  %7.1f TF/s\n", d.n, d.n, d.Mt,
+             2.0 * d.Mt * d.n * 2 / 1048576.0, us, fl / us * 1e-6);
+      fflush(stdout);
+    }
+  }
   {  // early DMA on the forward / dX shapes
     for (int bkm = 1; bkm >= 0; --bkm)
       for (int dbg : {0, 16}) {
