@@ -271,42 +271,76 @@ NSTL_DEV void fwd_queries(const AttnParams& p, const char* Kimg, const char* Vim
   }
   const float c2 = p.scale * LOG2E;
   float m = -INFINITY;
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt)
-    if (kt < nkt) m = fmaxf(fmaxf(fmaxf(m, s[kt][0]), fmaxf(s[kt][1], s[kt][2])), s[kt][3]);
-  m = max_xor16(m);
-  m = max_xor32(m);
-  // bf16: 2^(s*c2 - m*c2), one FMA per score instead of a subtract and a multiply.
-  // f32 (parity mode) keeps (s - m)*c2: s - m is exact near the max, where the
-  // rounded m*c2 of the FMA form would cancel (the fp32 gradient norm moved by 1e-4)
-  const float mc = m * c2;
   float sum = 0.f;
+  if constexpr (sizeof(T) == 2) {
+    // bf16: the max as two v_max3 per key tile; 2^(s*c2 - m*c2) as packed FMAs
+    // (one per two scores, instead of a subtract and a multiply per score) and
+    // the row sum as packed adds over two partial sums
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt)
-    if (kt < nkt) {
+    for (int kt = 0; kt < NKT; ++kt)
+      if (kt < nkt) m = fmaxf(fmaxf(m, fmaxf(fmaxf(s[kt][0], s[kt][1]), s[kt][2])), s[kt][3]);
+    m = max_xor16(m);
+    m = max_xor32(m);
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 c2v = {c2, c2}, nmc = {-m * c2, -m * c2};
+    f32x2 sum2 = {0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = fast_exp2(sizeof(T) == 2 ? fmaf(s[kt][r], c2, -mc) : (s[kt][r] - m) * c2);
-        s[kt][r] = e;
-        sum += e;
+    for (int kt = 0; kt < NKT; ++kt)
+      if (kt < nkt) {
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 x = __builtin_elementwise_fma((f32x2){s[kt][r], s[kt][r + 1]}, c2v, nmc);
+          const f32x2 e = {fast_exp2(x[0]), fast_exp2(x[1])};
+          s[kt][r] = e[0];
+          s[kt][r + 1] = e[1];
+          sum2 += e;
+        }
       }
-    }
+    sum = sum2[0] + sum2[1];
+  } else {
+    // f32 (parity mode) keeps (s - m)*c2: s - m is exact near the max, where the
+    // rounded m*c2 of the FMA form would cancel (the fp32 gradient norm moved by 1e-4)
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+      if (kt < nkt) m = fmaxf(fmaxf(fmaxf(m, s[kt][0]), fmaxf(s[kt][1], s[kt][2])), s[kt][3]);
+    m = max_xor16(m);
+    m = max_xor32(m);
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+      if (kt < nkt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = fast_exp2((s[kt][r] - m) * c2);
+          s[kt][r] = e;
+          sum += e;
+        }
+      }
+  }
   sum = sum_xor16(sum);
   sum = sum_xor32(sum);
   if (p.thresh) {
     // dropout on P: keys (r, r+1) of this lane's query share one hash.  The keep
     // compare is an SGPR lane mask already -- the ballot of (kt, r) -- and lane
     // kt*4 + r takes it by v_writelane (the select-by-lane-index form cost ~7
-    // vector instructions per ballot).
+    // vector instructions per ballot).  The hashes go first, all of them (their
+    // multiplies interleave); then one key tile's compares, selects and ballots
+    // at a time (sched_barrier): left free, the compiler formed all 32 ballot
+    // masks before the first v_writelane and spilled SGPRs into VGPR lanes.
     const int q = q0 + c;
     // pair index of drop_idx(bh, T, q, 4g) (even): 32-bit, checked by the launcher
     const uint32_t pair0 = ((uint32_t)bh * T_ + q) * (uint32_t)(T_ >> 1) + 2 * g;
     const uint32_t st = nstl_seed_term(p.seed);
+    uint32_t hs[NKT][2];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      hs[kt][0] = nstl_pair_hash32(st, pair0 + kt * 8);
+      hs[kt][1] = nstl_pair_hash32(st, pair0 + kt * 8 + 1);
+    }
     uint32_t mlo = 0, mhi = 0;  // lane kt*4 + r: keep bits of (kt, r)
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
       if (kt < nkt) {
-        const uint32_t h0 = nstl_pair_hash32(st, pair0 + kt * 8), h1 = nstl_pair_hash32(st, pair0 + kt * 8 + 1);
+        const uint32_t h0 = hs[kt][0], h1 = hs[kt][1];
         const bool k[4] = {(h0 & 0xFFFFu) >= p.thresh, (h0 >> 16) >= p.thresh, (h1 & 0xFFFFu) >= p.thresh,
                            (h1 >> 16) >= p.thresh};
 #pragma unroll
@@ -318,6 +352,7 @@ NSTL_DEV void fwd_queries(const AttnParams& p, const char* Kimg, const char* Vim
           mlo = nstl_writelane_i32((int)(uint32_t)bal, kt * 4 + r, (int)mlo);
           mhi = nstl_writelane_i32((int)(uint32_t)(bal >> 32), kt * 4 + r, (int)mhi);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     if (p.mask && lane < nkt * 4) p.mask[mask_word(bh, nkt, q0 >> 4, 0, 0) + lane] = ((uint64_t)mhi << 32) | mlo;
@@ -526,17 +561,21 @@ NSTL_DEV void rope_apply(float (&v)[4][4], const float (&tc)[4][4], const float 
 // the hardware sin / cos (v_sin_f32 / v_cos_f32 on angle / 2pi).  Against the
 // f32 tables the error is ~1e-6 absolute, far below the bf16 rounding of the
 // dQ / dK it rotates.
+// The angle goes to v_sin / v_cos in revolutions, t * (inv_freq / 2pi), with the
+// lane's sign folded into the factor (sin is odd, cos even): one multiply per
+// angle instead of three (angle, 1/2pi for each of sin and cos, the sign).
 NSTL_DEV void rope_tab_fast(float (&tc)[4][4], float (&ts)[4][4], int row0, int c) {
-  const float sgn = (c & 1) ? -1.f : 1.f;
+  const float sgn_rev = ((c & 1) ? -1.f : 1.f) * 0.15915494309189535f;  // +-1/(2pi)
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
     const float two_i = (float)(2 * (dt * 8 + (c >> 1)));
     const float inv_freq = __expf(-9.21034049987793f * two_i / (float)DH);  // f32(ln 10000)
+    const float f = inv_freq * sgn_rev;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float a = (float)(row0 + r) * inv_freq;
-      ts[dt][r] = sgn * __sinf(a);
-      tc[dt][r] = __cosf(a);
+      const float a = (float)(row0 + r) * f;
+      ts[dt][r] = __builtin_amdgcn_sinf(a);
+      tc[dt][r] = __builtin_amdgcn_cosf(a);
     }
   }
 }
@@ -898,16 +937,70 @@ NSTL_DEV uint4 rope_chunk(const AttnParams& p, int idx, int nchunk) {
   return *src;
 }
 
+// rows [tok0, tok0 + T) of a head's 64 columns (h * DH) of a bf16 [*, ld] operand
+// as a buffer resource (host-checked: T * ld * 2 < 2^31)
+NSTL_DEV __amdgpu_buffer_rsrc_t head_rsrc(const char* base, int64_t ld, int64_t tok0, int h, int T) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (tok0 * ld + h * DH) * 2), 0, (int)((uint32_t)T * ld * 2),
+                                           0x00020000);
+}
+// dma_rows (ImgK<128>, bf16) from a head buffer: 8 rows per 1 KB wave instruction
+template <int NW>
+NSTL_DEV void dma_rows_buf(char* img, __amdgpu_buffer_rsrc_t r, uint32_t ld_bytes, int nrows, int wave, int lane) {
+  const int ninst = nrows / 8;
+  for (int q = wave; q < ninst; q += NW) {
+    const int row = q * 8 + (lane >> 3), lc = (lane & 7) ^ ((row >> 1) & 7);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(img + q * 1024), 16,
+                                             (uint32_t)row * ld_bytes + lc * 16, 0, 0, 0);
+  }
+}
+typedef int i32x4b __attribute__((ext_vector_type(4)));
+// store_tile16x64<bf16> into a head buffer (head_rsrc of the output), the tile's
+// first row at byte offset off0: 32-bit offsets instead of 64-bit addresses
+NSTL_DEV void store_tile16x64_buf(const float (&v)[4][4], char* scr, __amdgpu_buffer_rsrc_t r, uint32_t off0,
+                                  uint32_t ld_bytes, int lane) {
+  constexpr int RB = DH * 2, CPR = RB / 16;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) *(bf16*)(scr + (4 * g + rr) * RB + (dt * 16 + (lane & 15)) * 2) = (bf16)v[dt][rr];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int c = lane; c < 16 * CPR; c += 64) {
+    const int row = c / CPR, ch = c % CPR;
+    __builtin_amdgcn_raw_buffer_store_b128(*(const i32x4b*)(scr + row * RB + ch * 16), r,
+                                           off0 + (uint32_t)row * ld_bytes + ch * 16, 0, 0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+NSTL_DEV bf16x8 buf_frag(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+// D's row part: sum_e a[e] b[e] over one fragment pair, two products per
+// v_dot2_f32_bf16 (unpacked, each product cost two conversions and an FMA)
+NSTL_DEV float dot8_bf16(const bf16x8& a, const bf16x8& b, float acc) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int e = 0; e < 8; e += 2)
+    acc = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){a[e], a[e + 1]}, (bf16x2){b[e], b[e + 1]}, acc, false);
+  return acc;
+}
+// stored keep bit r of a nibble as an all-ones / zero lane mask (one v_bfe_i32):
+// P_drop and dP_drop then take it by AND instead of a compare and two selects
+NSTL_DEV uint32_t keep_mask(uint32_t nib, int r) { return (uint32_t)((int)(nib << (31 - r)) >> 31); }
+NSTL_DEV float and_mask(float x, uint32_t m) { return __uint_as_float(__float_as_uint(x) & m); }
+
 // DM: dropout mode, fixed per launch so the per-element loop carries no branch:
 // 0 none, 1 the forward's stored keep bits, 2 re-hashed (seed, element)
-template <int DM>
+// TC: T as a compile-time constant (the production T = 128; 0: p.T)
+template <int DM, int TC = 0>
 __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p) {
   typedef bf16x8 Frag;
   constexpr int RBK = DH * 2;
   typedef ImgK<RBK> Img;
   constexpr int NW = BWD_NT / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int T_ = p.T, nkt = T_ / 16;
+  const int T_ = TC ? TC : p.T, nkt = T_ / 16;
   char* Qimg = smem;                                           // [128][128 B]
   char* Dimg = Qimg + FUSED_MAX_T * RBK;                       // [128][128 B]
   char* DSimg = smem;                                          // over Q | dO after phase 1
@@ -925,23 +1018,26 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
   const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int64_t tok0 = (int64_t)b * T_;
   const int k0 = w * 16;     // this wave's keys (phase 1) and queries (D, phase 2)
-  const bool act = k0 < T_;
-  dma_rows<RBK, NW>(Qimg, p.q + (tok0 * p.q_ld + h * DH) * 2, p.q_ld * 2, T_, w, lane);
-  dma_rows<RBK, NW>(Dimg, p.dout + (tok0 * p.dout_ld + h * DH) * 2, p.dout_ld * 2, T_, w, lane);
-  dma_rows<RBK, NW>(Kimg, p.k + (tok0 * p.k_ld + h * DH) * 2, p.k_ld * 2, T_, w, lane);
+  const bool act = TC == FUSED_MAX_T || k0 < T_;
+  // the head's rows of each operand as a buffer (base in SGPRs, per-lane 32-bit
+  // offsets; 64-bit per-lane addresses were ~100 of the wave's vector instructions)
+  const __amdgpu_buffer_rsrc_t rq = head_rsrc(p.q, p.q_ld, tok0, h, T_), rd = head_rsrc(p.dout, p.dout_ld, tok0, h, T_),
+                               rk = head_rsrc(p.k, p.k_ld, tok0, h, T_), rv = head_rsrc(p.v, p.v_ld, tok0, h, T_),
+                               ro = head_rsrc(p.o, p.o_ld, tok0, h, T_);
+  dma_rows_buf<NW>(Qimg, rq, (uint32_t)p.q_ld * 2, T_, w, lane);
+  dma_rows_buf<NW>(Dimg, rd, (uint32_t)p.dout_ld * 2, T_, w, lane);
+  dma_rows_buf<NW>(Kimg, rk, (uint32_t)p.k_ld * 2, T_, w, lane);
   for (int i = tid; i < T_; i += BWD_NT) lse_s[i] = p.lse[(int64_t)bh * T_ + i] * LOG2E;
   if (tid == 0) *arrived = 0u;
   Frag fk[2], fv[2], oo[2];
   if (act) {
-    const int r = k0 + c;
-    const bf16* krow = (const bf16*)p.k + (tok0 + r) * p.k_ld + h * DH;
-    const bf16* vrow = (const bf16*)p.v + (tok0 + r) * p.v_ld + h * DH;
-    const bf16* orow = (const bf16*)p.o + (tok0 + r) * p.o_ld + h * DH;
+    const uint32_t r = (uint32_t)(k0 + c);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      gload_frag<bf16>(fk[u], krow, 32 * u + 8 * g);
-      gload_frag<bf16>(fv[u], vrow, 32 * u + 8 * g);
-      gload_frag<bf16>(oo[u], orow, 32 * u + 8 * g);
+      const uint32_t col = (uint32_t)(32 * u + 8 * g) * 2;
+      fk[u] = buf_frag(rk, r * (uint32_t)p.k_ld * 2 + col);
+      fv[u] = buf_frag(rv, r * (uint32_t)p.v_ld * 2 + col);
+      oo[u] = buf_frag(ro, r * (uint32_t)p.o_ld * 2 + col);
     }
   }
   // stored keep bits for this wave's 16 keys: lane 4*qt + r holds word (qt, k0/16, r)
@@ -955,8 +1051,7 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
     for (int u = 0; u < 2; ++u) {
       Frag fo;
       frag_row<Img>(fo, Dimg, k0 + c, 32 * u + 8 * g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dpart += (float)fo[e] * (float)oo[u][e];
+      dpart = dot8_bf16(fo, oo[u], dpart);
     }
     dpart = sum_xor16(dpart);
     dpart = sum_xor32(dpart);
@@ -995,8 +1090,12 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
             const int q = qt * 16 + 4 * g + r;
             const float pv = fast_exp2(st[r] * c2 - lse_s[q]);
             float pdr = pv, dpd = dpt[r];
-            if constexpr (DM != 0) {  // P_drop's 1/(1-p) goes onto dV at the end
-              const bool keep = DM == 1 ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
+            if constexpr (DM == 1) {  // P_drop's 1/(1-p) goes onto dV at the end
+              const uint32_t km = keep_mask(nib, r);
+              pdr = and_mask(pv, km);
+              dpd = and_mask(dpd * p.inv_keep, km);
+            } else if constexpr (DM == 2) {
+              const bool keep = nstl_keep(p.seed, drop_idx(bh, T_, q, k0 + c), p.thresh);
               pdr = keep ? pv : 0.f;
               dpd = keep ? dpd * p.inv_keep : 0.f;
             }
@@ -1096,10 +1195,9 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
       if (p.rope_k) rope_apply(vk, tc, ts);
     }
     char* scr = scratch + w * 16 * RBK;
-    const int64_t r0 = tok0 + k0;
-    store_tile16x64<bf16>(vq, scr, p.dq + (r0 * p.dq_ld + h * DH) * 2, p.dq_ld, lane);
-    store_tile16x64<bf16>(vk, scr, p.dk + (r0 * p.dk_ld + h * DH) * 2, p.dk_ld, lane);
-    store_tile16x64<bf16>(vv, scr, p.dv + (r0 * p.dv_ld + h * DH) * 2, p.dv_ld, lane);
+    store_tile16x64_buf(vq, scr, head_rsrc(p.dq, p.dq_ld, tok0, h, T_), (uint32_t)k0 * p.dq_ld * 2, p.dq_ld * 2, lane);
+    store_tile16x64_buf(vk, scr, head_rsrc(p.dk, p.dk_ld, tok0, h, T_), (uint32_t)k0 * p.dk_ld * 2, p.dk_ld * 2, lane);
+    store_tile16x64_buf(vv, scr, head_rsrc(p.dv, p.dv_ld, tok0, h, T_), (uint32_t)k0 * p.dv_ld * 2, p.dv_ld * 2, lane);
   }
   if (bias_row) {
     if (act) {
@@ -1242,8 +1340,7 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_persist_kernel(AttnParams 
       for (int u = 0; u < 2; ++u) {
         Frag fo;
         frag_row<Img>(fo, Dimg, k0 + c, 32 * u + 8 * g);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dpart += (float)fo[e] * (float)oo[u][e];
+        dpart = dot8_bf16(fo, oo[u], dpart);
       }
       dpart = sum_xor16(dpart);
       dpart = sum_xor32(dpart);
@@ -1277,8 +1374,12 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_persist_kernel(AttnParams 
           const int q = qt * 16 + 4 * g + r;
           const float pv = fast_exp2(st[r] * c2 - lse_s[q]);
           float pdr = pv, dpd = dpt[r];
-          if constexpr (DM != 0) {
-            const bool keep = DM == 1 ? ((nib >> r) & 1) : nstl_keep(p.seed, drop_idx(it, T_, q, k0 + c), p.thresh);
+          if constexpr (DM == 1) {
+            const uint32_t km = keep_mask(nib, r);
+            pdr = and_mask(pv, km);
+            dpd = and_mask(dpd * p.inv_keep, km);
+          } else if constexpr (DM == 2) {
+            const bool keep = nstl_keep(p.seed, drop_idx(it, T_, q, k0 + c), p.thresh);
             pdr = keep ? pv : 0.f;
             dpd = keep ? dpd * p.inv_keep : 0.f;
           }
@@ -1748,6 +1849,10 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
   if (use_fused_bwd(a)) {
     NSTL_CHECK_ARG(!(a->rope_q || a->rope_k) || ((((uintptr_t)a->rope_cos) | ((uintptr_t)a->rope_sin)) & 15) == 0,
                    "nstl_attn_bwd: RoPE tables must be 16-byte aligned");
+    // head_rsrc: T rows of each operand as one buffer (32-bit extent)
+    const int64_t ld_max = std::max(std::max(std::max(a->q_ld, a->k_ld), std::max(std::max(a->v_ld, a->o_ld), a->dout_ld)),
+                                    std::max(std::max(a->dq_ld, a->dk_ld), a->dv_ld));
+    NSTL_CHECK_ARG((int64_t)a->T * ld_max * 2 < (1ll << 31), "nstl_attn_bwd: T x row stride past 2^31 bytes");
     nstl::count(NSTL_K_ATTN_BWD_FUSED);
     if (use_persist_bwd(a, p)) {
       const int nitems = a->B * a->H;
@@ -1759,6 +1864,11 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
       return launch(attn_bwd_persist_kernel<2>, grid, PB_LDS, st, p, "nstl_attn_bwd persistent", BWD_NT, nitems);
     }
     const dim3 grid(1, a->B * a->H);
+    if (a->T == FUSED_MAX_T) {  // the production shape: T a compile-time constant
+      if (!p.thresh) return launch(attn_bwd_fused_kernel<0, FUSED_MAX_T>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
+      if (p.mask) return launch(attn_bwd_fused_kernel<1, FUSED_MAX_T>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
+      return launch(attn_bwd_fused_kernel<2, FUSED_MAX_T>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
+    }
     if (!p.thresh) return launch(attn_bwd_fused_kernel<0>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
     if (p.mask) return launch(attn_bwd_fused_kernel<1>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
     return launch(attn_bwd_fused_kernel<2>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);
