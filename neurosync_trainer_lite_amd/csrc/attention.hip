@@ -58,8 +58,27 @@ NSTL_DEV void vmcnt_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// The 128-byte-row (bf16) K / V / Q / dO images of this file: 16-byte chunk c
+// of row r at c ^ att_x(r).  They are read both ways: by rows (ds_read_b128, 16
+// rows at one chunk per lane group) and transposed (ds_read_b64_tr_b16, 8 rows x
+// 32 bytes per 32-lane group).  ImgK<128>'s x = (r >> 1) & 7 serves the row reads
+// but puts rows r and r + 2 of a transposed read on the same banks (2 LDS cycles
+// per 32-lane group instead of 1: the backward's largest bank-conflict term).
+// This x -- row bit 1 to chunk bit 2, row bit 2 to chunk bit 1 -- is
+// conflict-free for both (checked for every read pattern of the kernels below by
+// a bank simulation of the ds_read_b128 / ds_read_b64_tr_b16 lane groups).
+// 256-byte rows (f32) keep ImgK<256>.
+NSTL_DEV int att_x(int row) { return (((row >> 2) & 1) << 1) | (((row >> 1) & 1) << 2); }
+template <int RB> struct ImgAtt {
+  static NSTL_DEV int off(int row, int byte) {
+    const int chunk = byte >> 4;
+    const int x = RB == 128 ? att_x(row) : (row & 15);
+    return row * RB + (((chunk ^ x) << 4) | (byte & 15));
+  }
+};
+
 // LDS-DMA rows [0, nrows) of a (b, h) slice (64 elements per row) into an
-// ImgK<RB> image.  One wave instruction moves 1 KB = 1024/RB rows; the image
+// ImgAtt<RB> image.  One wave instruction moves 1 KB = 1024/RB rows; the image
 // swizzle is applied to the per-lane source chunk.
 template <int RB, int NW = NT / 64>
 NSTL_DEV void dma_rows(char* img, const char* g, int64_t ld_bytes, int nrows, int wave, int lane) {
@@ -67,7 +86,7 @@ NSTL_DEV void dma_rows(char* img, const char* g, int64_t ld_bytes, int nrows, in
   const int ninst = nrows / RPK;
   for (int q = wave; q < ninst; q += NW) {
     const int row = q * RPK + lane / CPR, pc = lane % CPR;
-    const int x = RB == 128 ? ((row >> 1) & 7) : (row & 15);
+    const int x = RB == 128 ? att_x(row) : (row & 15);
     const int lc = pc ^ x;
     const char* src = g + row * ld_bytes + lc * 16;
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
@@ -192,7 +211,7 @@ constexpr int FWD_NT = 512, FWD_QB = 16 * FWD_NT / 64;
 // One wave's 16 queries q0 .. q0+15 of head bh (tokens from tok0, head column
 // h*DH) against all keys of the K / V images: scores, exact softmax, dropout
 // (keep bits to p.mask), O and the LSE.  fq: the wave's Q fragments.
-// ImgK<128> fragment reads as inline asm (bf16): with a prefetch DMA in flight
+// ImgAtt<128> fragment reads as inline asm (bf16): with a prefetch DMA in flight
 // into the other buffer the compiler would put vmcnt(0) in front of its own LDS
 // reads (it cannot tell the images apart), draining the prefetch; the caller
 // orders them with an explicit lgkmcnt(0) + sched_barrier before the MFMAs.
@@ -201,15 +220,15 @@ typedef int i32x4a __attribute__((ext_vector_type(4)));
 typedef int i32x2a __attribute__((ext_vector_type(2)));
 NSTL_DEV void asm_row128(bf16x8& f, const char* img, int row, int r) {
   i32x4a v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(img + ImgK<128>::off(row, r * 2))));
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(img + ImgAtt<128>::off(row, r * 2))));
   f = __builtin_bit_cast(bf16x8, v);
 }
-NSTL_DEV void asm_col2_128(bf16x8& f, const char* img, int col16, int r0, int lane) {  // frag_col2<ImgK<128>>
+NSTL_DEV void asm_col2_128(bf16x8& f, const char* img, int col16, int r0, int lane) {  // frag_col2<ImgAtt<128>>
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   const int byte = (col16 + 4 * pp) * 2;
   i32x2a v0, v1;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v0) : "v"(lds_addr(img + ImgK<128>::off(r0 + 4 * g + q, byte))));
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v1) : "v"(lds_addr(img + ImgK<128>::off(r0 + 16 + 4 * g + q, byte))));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v0) : "v"(lds_addr(img + ImgAtt<128>::off(r0 + 4 * g + q, byte))));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v1) : "v"(lds_addr(img + ImgAtt<128>::off(r0 + 16 + 4 * g + q, byte))));
   const bf16x4 b0 = __builtin_bit_cast(bf16x4, v0), b1 = __builtin_bit_cast(bf16x4, v1);
   f = (bf16x8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
 }
@@ -222,7 +241,7 @@ struct NoHook {
   NSTL_DEV void operator()() const {}
 };
 
-// AR: the Q fragments come from the wave's 16-row Q image Qw (ImgK<128>) and
+// AR: the Q fragments come from the wave's 16-row Q image Qw (ImgAtt<128>) and
 // every K / V / Q fragment read is inline asm (bf16 only; the persistent kernel);
 // after_qk() runs once the wave is done with its Q image (the S products)
 template <typename T, int NKT, bool AR = false, typename Hook = NoHook>
@@ -231,7 +250,7 @@ NSTL_DEV void fwd_queries(const AttnParams& p, const char* Kimg, const char* Vim
                           int q0, int lane, Hook after_qk = Hook()) {
   typedef typename FragT<T>::type Frag;
   constexpr int RBK = DH * (int)sizeof(T);
-  typedef ImgK<RBK> Img;
+  typedef ImgAtt<RBK> Img;
   constexpr int nkt = NKT;
   const int T_ = p.T, g = lane >> 4, c = lane & 15;
   // s[kt][r] = score(query q0 + c, key 16kt + 4g + r)
@@ -463,16 +482,16 @@ __global__ __launch_bounds__(FWD_NT, 4) void attn_fwd_persist_kernel(AttnParams 
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = gridDim.x;
   char* const Qw = smem + 4 * PF_IMG + w * 2048;
-  // per-lane byte offsets inside a head's slab, once (ImgK<128> swizzle on the
+  // per-lane byte offsets inside a head's slab, once (ImgAtt<128> swizzle on the
   // source chunk, as dma_rows): the wave's two 1 KB pieces of the K and V
   // images (rows 8(w + 8u) ..) and of its own Q rows (16w + 8u ..)
   uint32_t offk[2], offv[2], offq[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int row = (w + 8 * u) * 8 + (lane >> 3), lc = (lane & 7) ^ ((row >> 1) & 7);
+    const int row = (w + 8 * u) * 8 + (lane >> 3), lc = (lane & 7) ^ att_x(row);
     offk[u] = (uint32_t)(row * p.k_ld * 2 + lc * 16);
     offv[u] = (uint32_t)(row * p.v_ld * 2 + lc * 16);
-    const int qr = 8 * u + (lane >> 3), qc = (lane & 7) ^ ((qr >> 1) & 7);
+    const int qr = 8 * u + (lane >> 3), qc = (lane & 7) ^ att_x(qr);
     offq[u] = (uint32_t)((w * 16 + qr) * p.q_ld * 2 + qc * 16);
   }
   auto head = [&](int it, const char* base, int64_t ld) {
@@ -652,7 +671,7 @@ __global__ __launch_bounds__(BWD_NT, 6) void attn_bwd_dq_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
   constexpr int ESZ = (int)sizeof(T);
   constexpr int RBK = DH * ESZ;
-  typedef ImgK<RBK> Img;
+  typedef ImgAtt<RBK> Img;
   constexpr int NW = BWD_NT / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int T_ = p.T, nkt = T_ / 16;
@@ -777,7 +796,7 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
   typedef typename FragT<T>::type Frag;
   constexpr int ESZ = (int)sizeof(T);
   constexpr int RBK = DH * ESZ;
-  typedef ImgK<RBK> Img;
+  typedef ImgAtt<RBK> Img;
   constexpr int NW = BWD_NT / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int T_ = p.T, nkt = T_ / 16;
@@ -943,12 +962,12 @@ NSTL_DEV __amdgpu_buffer_rsrc_t head_rsrc(const char* base, int64_t ld, int64_t 
   return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (tok0 * ld + h * DH) * 2), 0, (int)((uint32_t)T * ld * 2),
                                            0x00020000);
 }
-// dma_rows (ImgK<128>, bf16) from a head buffer: 8 rows per 1 KB wave instruction
+// dma_rows (ImgAtt<128>, bf16) from a head buffer: 8 rows per 1 KB wave instruction
 template <int NW>
 NSTL_DEV void dma_rows_buf(char* img, __amdgpu_buffer_rsrc_t r, uint32_t ld_bytes, int nrows, int wave, int lane) {
   const int ninst = nrows / 8;
   for (int q = wave; q < ninst; q += NW) {
-    const int row = q * 8 + (lane >> 3), lc = (lane & 7) ^ ((row >> 1) & 7);
+    const int row = q * 8 + (lane >> 3), lc = (lane & 7) ^ att_x(row);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(img + q * 1024), 16,
                                              (uint32_t)row * ld_bytes + lc * 16, 0, 0, 0);
   }
@@ -997,7 +1016,7 @@ template <int DM, int TC = 0>
 __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p) {
   typedef bf16x8 Frag;
   constexpr int RBK = DH * 2;
-  typedef ImgK<RBK> Img;
+  typedef ImgAtt<RBK> Img;
   constexpr int NW = BWD_NT / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int T_ = TC ? TC : p.T, nkt = T_ / 16;
@@ -1246,7 +1265,7 @@ constexpr size_t PB_LDS = PB_CNT + 16;
 template <int DM>
 __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_persist_kernel(AttnParams p, int nitems) {
   typedef bf16x8 Frag;
-  typedef ImgK<128> Img;
+  typedef ImgAtt<128> Img;
   constexpr int NW = BWD_NT / 64;
   constexpr int T_ = PF_T, nkt = PF_T / 16;
   extern __shared__ __attribute__((aligned(16))) char smem_pb[];
@@ -1270,7 +1289,7 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_persist_kernel(AttnParams 
     const int b = item / p.H, h = item % p.H;
     return base + ((int64_t)b * PF_T * ld + h * DH) * 2;
   };
-  // the wave's two 1 KB pieces of each image (rows 8 (w + 8 u) .., ImgK<128>
+  // the wave's two 1 KB pieces of each image (rows 8 (w + 8 u) .., ImgAtt<128>
   // swizzle on the source chunk, as the forward); the per-lane offsets are
   // recomputed per head (registers are the binding budget at 4 waves per SIMD)
   auto issue_images = [&](int item, int lane) {
@@ -1279,7 +1298,7 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_persist_kernel(AttnParams 
     const char* kb = head(item, p.k, p.k_ld);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int row = (w + 8 * u) * 8 + (lane >> 3), lc = (lane & 7) ^ ((row >> 1) & 7);
+      const int row = (w + 8 * u) * 8 + (lane >> 3), lc = (lane & 7) ^ att_x(row);
       dma1k(qb + (row * p.q_ld * 2 + lc * 16), Qimg + (w + 8 * u) * 1024);
       dma1k(db + (row * p.dout_ld * 2 + lc * 16), Dimg + (w + 8 * u) * 1024);
       dma1k(kb + (row * p.k_ld * 2 + lc * 16), Kimg + (w + 8 * u) * 1024);
