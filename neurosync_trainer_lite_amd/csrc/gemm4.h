@@ -275,11 +275,20 @@ NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 
     if constexpr (!(DBG & 8)) mma16(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
     G4_SB();
     if constexpr (RD && !(DBG & 2)) rd_after<AK, BKM, RSO, RH, I, 0>(na, nb, ra, rb);
-    // the 16 DMA pieces: after MFMAs 2, 6, ..., 62, or (DBG & 16, an experiment) after
-    // MFMAs 0 .. 15, issued as early in h = 1 as possible
-    constexpr bool DMA_HERE = (DBG & 16) ? I < 16 : (I & 3) == 2;
+    // the 16 DMA pieces: after MFMAs 2, 6, ..., 62, or (experiments) after MFMAs
+    // 0 .. 15 (DBG & 16) / 0, 2, ..., 30 (DBG & 32): issued earlier in h = 1; after
+    // MFMAs 32, 34, ..., 62 (DBG & 64) / 47 .. 62 (DBG & 128): later
+    constexpr bool DMA_HERE = (DBG & 16)    ? I < 16
+                              : (DBG & 32)  ? (I < 32 && (I & 1) == 0)
+                              : (DBG & 64)  ? (I >= 32 && (I & 1) == 0)
+                              : (DBG & 128) ? (I >= 47 && I < 63)
+                                            : (I & 3) == 2;
     if constexpr (DMA && !(DBG & 1) && DMA_HERE) {
-      constexpr int q = (DBG & 16) ? I : I >> 2;
+      constexpr int q = (DBG & 16)    ? I
+                        : (DBG & 32)  ? I >> 1
+                        : (DBG & 64)  ? (I - 32) >> 1
+                        : (DBG & 128) ? I - 47
+                                      : I >> 2;
       if constexpr (q < 8) dma16(d.ra, adst + q * 1024, d.va[q], d.ta + sa);
       else dma16(d.rb, bdst + (q - 8) * 1024, d.vb[q - 8], d.tb + sb);
       G4_SB();

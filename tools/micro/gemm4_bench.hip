@@ -75,6 +75,57 @@ __global__ __launch_bounds__(256, 1) void store_tile(bf16* C, int N, int ldc) {
     for (int bp = 0; bp < 8; bp += 2) *(uint4*)(cbase + (int64_t)(16 * a) * ldc + 16 * (bp + odd) + 4 * (g - odd)) = v;
 }
 
+// G4_DMA_AB=1: DMA piece placement arms (DBG 0 / 64 / 128; 16 and 32 measured
+// slower, profiles/r4_gemm4_dma_placement.txt) alternated over three
+// shapes after a warm-up block (the first blocks of a process run slow)
+template <bool AK, bool BKM, int EM, int DBG>
+void launch_any(const g4::GroupParams& gp, hipStream_t st) {
+  hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, EM, false, DBG>), dim3(256), dim3(g4::NT), 0, st, gp);
+}
+int dma_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
+  struct Case { const char* name; int M, N, K; int kind; };  // kind 0 TT, 1 TN, 2 NN f32 (dW)
+  const Case cs[] = {{"fwd ffn2 16384x1024x4096", 16384, 1024, 4096, 0},
+                     {"dX  ffn2 16384x1024x4096", 16384, 1024, 4096, 1},
+                     {"dW  4096^2 K=16384     ", 4096, 4096, 16384, 2}};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  typedef void (*F)(const g4::GroupParams&, hipStream_t);
+  const int dbgs[3] = {0, 64, 128};
+  const F fs[3][3] = {{launch_any<true, true, g4::EM_BF16, 0>, launch_any<true, true, g4::EM_BF16, 64>, launch_any<true, true, g4::EM_BF16, 128>},
+                      {launch_any<true, false, g4::EM_BF16, 0>, launch_any<true, false, g4::EM_BF16, 64>, launch_any<true, false, g4::EM_BF16, 128>},
+                      {launch_any<false, false, g4::EM_F32, 0>, launch_any<false, false, g4::EM_F32, 64>, launch_any<false, false, g4::EM_F32, 128>}};
+  for (int round = 0; round < 4; ++round)
+    for (const Case& c : cs) {
+      g4::GroupParams gp{};
+      g4::Params& p = gp.g[0];
+      p.M = c.M; p.N = c.N; p.K = c.K; p.alpha = 1.f;
+      if (c.kind == 2) {  // dW = A^T B, A [K][M], B [K][N] (MN-major)
+        p.A = (const char*)A; p.lda = c.M; p.B = (const char*)B; p.ldb = c.N; p.C = (char*)Cf; p.ldc = c.N;
+        p.a_bytes = (uint32_t)((int64_t)c.K * c.M * 2); p.b_bytes = (uint32_t)((int64_t)c.K * c.N * 2);
+      } else {
+        p.A = (const char*)A; p.lda = c.K; p.B = (const char*)B; p.ldb = c.kind == 0 ? c.K : c.N; p.C = (char*)C; p.ldc = c.N;
+        p.a_bytes = (uint32_t)((int64_t)c.M * c.K * 2); p.b_bytes = (uint32_t)((int64_t)c.N * c.K * 2);
+      }
+      p.tiles_m = c.M / 256; p.tiles_n = c.N / 256;
+      gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
+      for (int arm = 0; arm < 3; ++arm) {
+        const F f = fs[c.kind][arm];
+        for (int w = 0; w < 3; ++w) f(gp, st);
+        std::vector<float> ts;
+        for (int r = 0; r < 15; ++r) {
+          CK(hipEventRecord(e0, st)); f(gp, st); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+          float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        if (round > 0)
+          printf("round %d  %s  dbg %2d  %8.1f us\n", round, c.name, dbgs[arm], ts[7] * 1e3);
+        fflush(stdout);
+      }
+    }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   struct Shape { const char* name; int M, N, K, bkm; };
   const Shape shapes[] = {
@@ -99,6 +150,11 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&R, maxC * 4));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, st, A, maxA, 1u);
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, st, B, maxA, 2u);
+  if (getenv("G4_DMA_AB")) {
+    float* Cf;
+    CK(hipMalloc(&Cf, 4096LL * 4096 * 4));
+    return dma_ab(A, B, C, Cf, st);
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
