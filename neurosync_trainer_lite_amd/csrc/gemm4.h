@@ -254,16 +254,18 @@ NSTL_DEV void rd_all(bf16x8 (&fa)[8], bf16x8 (&fb)[8], const RdAddr<AK>& ra, con
 // lgkmcnt(0)); if DMA, the 16 pieces follow MFMAs 2, 6, ..., 62 (A pieces to adst,
 // B pieces to bdst, stage offsets sa / sb).  RSO: the read slot's byte offset.
 // DBG (timing experiments only, wrong results): 1 no DMA, 2 no reads, 8 no MFMA.
-template <bool AK, bool BKM, int RSO, int RH, int I, int R>
+// (experiments, profiles/r4_gemm4_read_spread.txt: DBG & 256 spreads the reads over
+// MFMAs 1 .. 56, DBG & 512 over 1 .. 32, DBG & 1024 over 1 .. 24)
+template <bool AK, bool BKM, int RSO, int RH, int I, int R, int SPAN = 46>
 NSTL_DEV void rd_after(bf16x8 (&na)[8], bf16x8 (&nb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb) {
   constexpr int NR = n_reads<AK, BKM>();
   if constexpr (R < NR) {
-    if constexpr (1 + (46 * R) / NR == I) {
+    if constexpr (1 + (SPAN * R) / NR == I) {
       rd_slot<AK, BKM, RSO, RH, R>(na, nb, ra, rb);
       G4_SB();
-      rd_after<AK, BKM, RSO, RH, I, R + 1>(na, nb, ra, rb);
-    } else if constexpr (1 + (46 * R) / NR < I) {
-      rd_after<AK, BKM, RSO, RH, I, R + 1>(na, nb, ra, rb);
+      rd_after<AK, BKM, RSO, RH, I, R + 1, SPAN>(na, nb, ra, rb);
+    } else if constexpr (1 + (SPAN * R) / NR < I) {
+      rd_after<AK, BKM, RSO, RH, I, R + 1, SPAN>(na, nb, ra, rb);
     }
   }
 }
@@ -274,7 +276,8 @@ NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 
   if constexpr (I < 64) {
     if constexpr (!(DBG & 8)) mma16(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
     G4_SB();
-    if constexpr (RD && !(DBG & 2)) rd_after<AK, BKM, RSO, RH, I, 0>(na, nb, ra, rb);
+    if constexpr (RD && !(DBG & 2))
+      rd_after<AK, BKM, RSO, RH, I, 0, (DBG & 256) ? 56 : (DBG & 512) ? 32 : (DBG & 1024) ? 24 : 46>(na, nb, ra, rb);
     // the 16 DMA pieces: after MFMAs 2, 6, ..., 62, or (experiments) after MFMAs
     // 0 .. 15 (DBG & 16) / 0, 2, ..., 30 (DBG & 32): issued earlier in h = 1; after
     // MFMAs 32, 34, ..., 62 (DBG & 64) / 47 .. 62 (DBG & 128): later

@@ -75,8 +75,9 @@ __global__ __launch_bounds__(256, 1) void store_tile(bf16* C, int N, int ldc) {
     for (int bp = 0; bp < 8; bp += 2) *(uint4*)(cbase + (int64_t)(16 * a) * ldc + 16 * (bp + odd) + 4 * (g - odd)) = v;
 }
 
-// G4_DMA_AB=1: DMA piece placement arms (DBG 0 / 64 / 128; 16 and 32 measured
-// slower, profiles/r4_gemm4_dma_placement.txt) alternated over three
+// G4_DMA_AB=1: K-loop placement arms (now DBG 0 / 256 / 512, the read spread; the DMA
+// placements 16, 32, 64, 128 measured slower, profiles/r4_gemm4_dma_placement.txt)
+// alternated over three
 // shapes after a warm-up block (the first blocks of a process run slow)
 template <bool AK, bool BKM, int EM, int DBG>
 void launch_any(const g4::GroupParams& gp, hipStream_t st) {
@@ -91,11 +92,11 @@ int dma_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   typedef void (*F)(const g4::GroupParams&, hipStream_t);
-  const int dbgs[3] = {0, 64, 128};
-  const F fs[3][3] = {{launch_any<true, true, g4::EM_BF16, 0>, launch_any<true, true, g4::EM_BF16, 64>, launch_any<true, true, g4::EM_BF16, 128>},
-                      {launch_any<true, false, g4::EM_BF16, 0>, launch_any<true, false, g4::EM_BF16, 64>, launch_any<true, false, g4::EM_BF16, 128>},
-                      {launch_any<false, false, g4::EM_F32, 0>, launch_any<false, false, g4::EM_F32, 64>, launch_any<false, false, g4::EM_F32, 128>}};
-  for (int round = 0; round < 4; ++round)
+  const int dbgs[3] = {0, 512, 1024};
+  const F fs[3][3] = {{launch_any<true, true, g4::EM_BF16, 0>, launch_any<true, true, g4::EM_BF16, 512>, launch_any<true, true, g4::EM_BF16, 1024>},
+                      {launch_any<true, false, g4::EM_BF16, 0>, launch_any<true, false, g4::EM_BF16, 512>, launch_any<true, false, g4::EM_BF16, 1024>},
+                      {launch_any<false, false, g4::EM_F32, 0>, launch_any<false, false, g4::EM_F32, 512>, launch_any<false, false, g4::EM_F32, 1024>}};
+  for (int round = 0; round < 6; ++round)
     for (const Case& c : cs) {
       g4::GroupParams gp{};
       g4::Params& p = gp.g[0];
