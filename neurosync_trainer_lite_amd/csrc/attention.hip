@@ -237,6 +237,12 @@ NSTL_DEV void lgkm_fence() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// rows [tok0, tok0 + T) of a head's 64 columns (h * DH) of a bf16 [*, ld] operand
+// as a buffer resource (host-checked: T * ld * 2 < 2^31)
+NSTL_DEV __amdgpu_buffer_rsrc_t head_rsrc(const char* base, int64_t ld, int64_t tok0, int h, int T) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (tok0 * ld + h * DH) * 2), 0, (int)((uint32_t)T * ld * 2),
+                                           0x00020000);
+}
 struct NoHook {
   NSTL_DEV void operator()() const {}
 };
@@ -404,9 +410,20 @@ NSTL_DEV void fwd_queries(const AttnParams& p, const char* Kimg, const char* Vim
   }
   // normalise (dropout's 1/(1-p) applied to O instead of P) and store
   const float inv = (p.thresh ? p.inv_keep : 1.f) * __builtin_amdgcn_rcpf(sum);
-  T* orow = (T*)p.o + (tok0 + q0 + c) * p.o_ld + h * DH + 4 * g;
+  if constexpr (AR) {  // the head's O rows as a buffer: 32-bit offsets (one store per dt, as store4)
+    const __amdgpu_buffer_rsrc_t ro = head_rsrc(p.o, p.o_ld, tok0, h, T_);
+    const uint32_t ob = ((uint32_t)(q0 + c) * (uint32_t)p.o_ld + 4 * g) * 2;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) store4<T>(orow + 16 * dt, o[dt] * inv);
+    for (int dt = 0; dt < 4; ++dt) {
+      const f32x4 x = o[dt] * inv;
+      const bf16x4 b = {(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2a, b), ro, ob + 32 * dt, 0, 0);
+    }
+  } else {
+    T* orow = (T*)p.o + (tok0 + q0 + c) * p.o_ld + h * DH + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) store4<T>(orow + 16 * dt, o[dt] * inv);
+  }
   if (g == 0) p.lse[(int64_t)bh * T_ + q0 + c] = m * p.scale + logf(sum);
 }
 
@@ -498,20 +515,27 @@ __global__ __launch_bounds__(FWD_NT, 4) void attn_fwd_persist_kernel(AttnParams 
     const int b = it / p.H, h = it % p.H;
     return base + ((int64_t)b * PF_T * ld + h * DH) * 2;
   };
+  // heads as buffer resources (base in SGPRs, the per-lane offsets above as 32-bit
+  // voffsets: no 64-bit address per piece)
+  auto hbuf = [&](int it, const char* base, int64_t ld) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)head(it, base, ld), 0, (int)((uint32_t)PF_T * ld * 2), 0x00020000);
+  };
+  auto dma_buf = [](__amdgpu_buffer_rsrc_t r, uint32_t off, char* dst) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, off, 0, 0, 0);
+  };
   auto issue_kv = [&](int it, int buf) {
-    const char* kb = head(it, p.k, p.k_ld);
-    const char* vb = head(it, p.v, p.v_ld);
+    const __amdgpu_buffer_rsrc_t rk = hbuf(it, p.k, p.k_ld), rv = hbuf(it, p.v, p.v_ld);
     char* img = smem + buf * 2 * PF_IMG;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      dma1k(kb + offk[u], img + (w + 8 * u) * 1024);
-      dma1k(vb + offv[u], img + PF_IMG + (w + 8 * u) * 1024);
+      dma_buf(rk, offk[u], img + (w + 8 * u) * 1024);
+      dma_buf(rv, offv[u], img + PF_IMG + (w + 8 * u) * 1024);
     }
   };
   auto issue_q = [&](int it) {
-    const char* qb = head(it, p.q, p.q_ld);
+    const __amdgpu_buffer_rsrc_t rq = hbuf(it, p.q, p.q_ld);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) dma1k(qb + offq[u], Qw + u * 1024);
+    for (int u = 0; u < 2; ++u) dma_buf(rq, offq[u], Qw + u * 1024);
   };
   int it = blockIdx.x;
   if (it >= nitems) return;
@@ -956,12 +980,6 @@ NSTL_DEV uint4 rope_chunk(const AttnParams& p, int idx, int nchunk) {
   return *src;
 }
 
-// rows [tok0, tok0 + T) of a head's 64 columns (h * DH) of a bf16 [*, ld] operand
-// as a buffer resource (host-checked: T * ld * 2 < 2^31)
-NSTL_DEV __amdgpu_buffer_rsrc_t head_rsrc(const char* base, int64_t ld, int64_t tok0, int h, int T) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (tok0 * ld + h * DH) * 2), 0, (int)((uint32_t)T * ld * 2),
-                                           0x00020000);
-}
 // dma_rows (ImgAtt<128>, bf16) from a head buffer: 8 rows per 1 KB wave instruction
 template <int NW>
 NSTL_DEV void dma_rows_buf(char* img, __amdgpu_buffer_rsrc_t r, uint32_t ld_bytes, int nrows, int wave, int lane) {
@@ -1826,6 +1844,9 @@ extern "C" int nstl_attn_fwd(const nstl_attn_args* a, void* stream) {
   }
   nstl::count(NSTL_K_ATTN_FWD);
   if (use_persist_fwd(a)) {
+    // head buffers (q, k, v, o): T rows of each as one 32-bit extent
+    NSTL_CHECK_ARG((int64_t)a->T * std::max(std::max(a->q_ld, a->k_ld), std::max(a->v_ld, a->o_ld)) * 2 < (1ll << 31),
+                   "nstl_attn_fwd: T x row stride past 2^31 bytes");
     const int nitems = a->B * a->H;
     const int G = std::min(nitems, std::max(2, 2 * nstl::stream_cus(st)));  // two workgroups per CU the stream may use
     const size_t lds = PF_LDS;
