@@ -970,7 +970,18 @@ constexpr int FUSED_ROPE_OFF = 8 * 16 * DH * 2 + 3 * 8 * 64 * 4;
 constexpr int FUSED_RS = DH / 2 + 4;  // padded table row (floats): 144 B, 16-byte aligned
 constexpr int FUSED_ARRIVED_OFF = FUSED_ROPE_OFF + 2 * FUSED_MAX_T * FUSED_RS * 4;
 constexpr int FUSED_DS_RB = FUSED_MAX_T * 2;  // dS^T image row: 128 queries (bf16)
-typedef ImgMN<FUSED_DS_RB> DsImg;
+// The dS^T image: written by rows (ds_write_b64, 16 lanes on 16 consecutive rows at one
+// column) and read transposed (frag_col2: 8 consecutive rows x 32 bytes per 32-lane
+// group).  16-byte chunk c of row r at c ^ x, x = (r & 7) << 1 | (r >> 3) & 1: the
+// transposed reads are conflict-free and the writes 2-way (16-byte chunk swizzles
+// cannot place 16 rows' 8-byte halves on distinct banks).  ImgMN<256>, made for
+// frag_col's row pattern, cost 4-way writes and 2-way reads here.
+struct DsImg {
+  static NSTL_DEV int off(int row, int byte) {
+    const int x = ((row & 7) << 1) | ((row >> 3) & 1);
+    return row * FUSED_DS_RB + ((((byte >> 4) ^ x) << 4) | (byte & 15));
+  }
+};
 
 // 16-byte chunk idx of the concatenated cos | sin tables (nchunk chunks each);
 // past the end it re-reads the last chunk (the caller does not store it)
