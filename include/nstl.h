@@ -351,6 +351,7 @@ enum {
   NSTL_K_GEMM4,              /* 4-wave persistent 256x256 GEMM launches (csrc/gemm4.h) */
   NSTL_K_GEMM4_TILES,        /*   ... their 256x256 output tiles */
   NSTL_K_GEMM4_SK,           /*   ... launches with a stream-K tail (grid not dividing the tiles) */
+  NSTL_K_GEMM_FP8_ROPE,      /* fp8 GEMM launches with the RoPE epilogue (C5 q|k|v, cross q, cross k|v) */
   NSTL_K_COUNT
 };
 /* Workgroups a persistent one-per-CU grid launches on `stream` (the GEMM and

@@ -124,7 +124,7 @@ EXPORTS = [
 # nstl_kernel_counts order (NSTL_K_* in include/nstl.h)
 KERNEL_COUNT_NAMES = ["gemm128", "gemm_ring", "gemm_ring_tiles", "gemm_group", "gemm_group_tiles",
                       "gemm_splitk_reduce", "gemm_fp8", "attn_fwd", "attn_fwd_generic", "attn_bwd_fused",
-                      "attn_bwd_split", "attn_bwd_generic", "gemm4", "gemm4_tiles", "gemm4_sk"]
+                      "attn_bwd_split", "attn_bwd_generic", "gemm4", "gemm4_tiles", "gemm4_sk", "gemm_fp8_rope"]
 
 _lib = None
 
@@ -291,10 +291,65 @@ def gemm_grouped(problems, stream=None):
           "nstl_gemm_grouped")
 
 
+# ---------------------------------------------------------------------------
+# operand extents: every tensor handed to a kernel must hold the last element
+# the call addresses (the kernels take plain pointers and strides and do not
+# know the allocation: an oversize M, K or ld would read or write past it)
+# ---------------------------------------------------------------------------
+def _room(t):
+    """Bytes from t.data_ptr() to the end of its storage."""
+    st = t.untyped_storage()
+    return st.data_ptr() + st.nbytes() - t.data_ptr()
+
+
+def _need(t, last, what):
+    """t must hold element index `last` (in t's element size) past its first."""
+    if t is None or last < 0:
+        return
+    if (last + 1) * t.element_size() > _room(t):
+        raise ValueError("%s: the call addresses element %d but the tensor's storage holds %d from its start"
+                         % (what, last, _room(t) // t.element_size()))
+
+
+def _need_mat(t, rows, cols, ld, what):
+    """A row-major [rows][cols] operand with row stride ld (elements)."""
+    if rows > 0 and cols > 0:
+        if ld < cols:
+            raise ValueError("%s: row stride %d < %d columns" % (what, ld, cols))
+        _need(t, (rows - 1) * ld + cols - 1, what)
+
+
+def _ceil(x, m):
+    return (x + m - 1) // m * m
+
+
+def gemm_check(A, B, C, M, N, K, a):
+    """Extents of every operand of one nstl_gemm call (a: the filled GemmArgs)."""
+    if M <= 0 or N <= 0 or K <= 0:
+        raise ValueError("nstl_gemm: empty problem %dx%dx%d" % (M, N, K))
+    vec = 16 // A.element_size()  # K-major rows are read in 16-byte chunks
+    if a.a_kmajor:
+        _need_mat(A, M, _ceil(K, vec), a.lda, "nstl_gemm A [M][K]")
+    else:
+        _need_mat(A, K, _ceil(M, vec), a.lda, "nstl_gemm A [K][M]")
+    if a.b_kmajor:
+        _need_mat(B, N, _ceil(K, vec), a.ldb, "nstl_gemm B [N][K]")
+    else:
+        _need_mat(B, K, _ceil(N, vec), a.ldb, "nstl_gemm B [K][N]")
+    _need_mat(C, M, N, a.ldc, "nstl_gemm C [M][N]")
+
+
+def _check_side(t, n, what):
+    if t is not None:
+        _need(t, n - 1, what)
+
+
 def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=None, ldc=None,
               alpha=1.0, beta=0.0, epilogue=EPI_NONE, bias=None, aux=None, ld_aux=0, p_drop=0.0, seed=0,
               rope=None, rope_cols=0, split_k=1, workspace=None, colsum_part=None, relu_mask=None,
               a_scale=None, b_scale=None, sq_part=None):
+    """The GemmArgs of one call, with every operand's extent checked against the
+    tensor's storage (ValueError before anything is launched)."""
     a = GemmArgs()
     a.dtype = dtype_code(A.dtype)
     a.c_dtype = dtype_code(C.dtype)
@@ -323,6 +378,18 @@ def gemm_args(A, B, C, M, N, K, *, a_kmajor=True, b_kmajor=True, lda=None, ldb=N
     a.relu_mask = ptr(relu_mask)
     a.a_scale, a.b_scale = ptr(a_scale), ptr(b_scale)
     a.sq_part = ptr(sq_part)
+    gemm_check(A, B, C, M, N, K, a)
+    _check_side(bias, N, "nstl_gemm bias [N]")
+    if aux is not None:
+        _need_mat(aux, M, N, ld_aux, "nstl_gemm aux [M][ld_aux]")
+    if rope is not None:
+        _check_side(rope[0], rT * (rdim // 2), "nstl_gemm rope_cos [T][dim/2]")
+        _check_side(rope[1], rT * (rdim // 2), "nstl_gemm rope_sin [T][dim/2]")
+    _check_side(relu_mask, ((M + 63) // 64) * 8 * ((N + 7) // 8), "nstl_gemm relu_mask words")
+    _check_side(colsum_part, ((M + 127) // 128) * N, "nstl_gemm colsum_part [M/128][N]")
+    _check_side(sq_part, ((M + 255) // 256) * ((N + 255) // 256) * 8, "nstl_gemm sq_part [tiles][8]")
+    _check_side(a_scale, M, "nstl_gemm a_scale [M]")
+    _check_side(b_scale, N, "nstl_gemm b_scale [N]")
     return a
 
 
@@ -375,6 +442,35 @@ def attn_args(dtype, B, T, H, q, q_ld, k, k_ld, v, v_ld, o, o_ld, lse, p_drop, s
     a.q, a.q_ld, a.k, a.k_ld, a.v, a.v_ld = q, q_ld, k, k_ld, v, v_ld
     a.o, a.o_ld, a.lse = o, o_ld, lse
     a.p_drop, a.seed = p_drop, seed & 0xFFFFFFFFFFFFFFFF
+    return a
+
+
+def attn_set(a, **ops):
+    """Point the AttnArgs `a` (attn_args) at tensors, each checked against the
+    extent the call addresses: q, k, v, o, dout, dq, dk, dv (row stride from the
+    tensor, B*T rows of H*dh), lse / dsum ([B*H*T] f32), mask_bits ([B*H*T*T/64]
+    words), rope_cos / rope_sin ([T][dh/2] f32), dbias_part ([rows][3*H*dh] f32,
+    rows = attn_bias_rows)."""
+    rows, cols = a.B * a.T, a.H * a.dh
+    for name, t in ops.items():
+        if t is None:
+            setattr(a, name, None)
+            continue
+        if name in ("q", "k", "v", "o", "dout", "dq", "dk", "dv"):
+            ld = t.stride(0)
+            _need_mat(t, rows, cols, ld, "nstl_attn %s [B*T][H*dh]" % name)
+            setattr(a, name + "_ld", ld)
+        elif name in ("lse", "dsum"):
+            _check_side(t, a.B * a.H * a.T, "nstl_attn %s [B*H*T]" % name)
+        elif name == "mask_bits":
+            _check_side(t, a.B * a.H * a.T * a.T // 64, "nstl_attn mask_bits [B*H*T*T/64]")
+        elif name in ("rope_cos", "rope_sin"):
+            _check_side(t, a.T * (a.dh // 2), "nstl_attn %s [T][dh/2]" % name)
+        elif name == "dbias_part":
+            _check_side(t, attn_bias_rows(a) * 3 * cols, "nstl_attn dbias_part [rows][3*H*dh]")
+        else:
+            raise TypeError("attn_set: unknown operand %r" % name)
+        setattr(a, name, t.data_ptr())
     return a
 
 

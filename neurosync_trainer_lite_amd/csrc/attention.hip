@@ -1268,249 +1268,6 @@ static_assert(FUSED_ARRIVED_OFF >= 3 * FUSED_MAX_T * DH * 2 + 2 * FUSED_MAX_T * 
 static_assert(FUSED_ROPE_OFF % 16 == 0, "16-byte table chunks");
 static_assert(8 * 16 * DH * 2 + 3 * 8 * 64 * 4 <= 3 * FUSED_MAX_T * DH * 2, "staging must fit in the images");
 
-// ---------------------------------------------------------------------------
-// Persistent fused backward (bf16, T = 128, RoPE^T recomputed or absent): the
-// fused kernel's per-head work, with 2 workgroups per CU walking the heads
-// (item = blockIdx.x + i G).  In the one-shot grid every workgroup loads its
-// Q / dO / K images, waits, computes and stores, so a head's load latency is
-// hidden only by the CU's other workgroup.  Here the next head's images (and
-// its LSE) are issued as soon as phase 2 is done with the current ones, and land
-// while the current head's epilogue (RoPE^T, the three tile stores, the bias
-// partials) runs: the staging, bias partials, LSE and D have LDS regions of
-// their own.  A wave's own K rows come from the K image; its V and O rows (the
-// dP operand and D) are the only loads a head waits for.
-// LDS: Q | dO | K images (48 KB; dS^T over Q | dO after phase 1), output
-// staging [8 waves][16 rows][128 B], bias partials [3][8][64] f32, LSE and D
-// [128] f32, the arrival counter: 71 KB, two workgroups per CU.
-constexpr int PB_IMG = PF_T * DH * 2;
-constexpr int PB_STAGE = 3 * PB_IMG;
-constexpr int PB_RED = PB_STAGE + 8 * 16 * DH * 2;
-constexpr int PB_LSE = PB_RED + 3 * 8 * 64 * 4;
-constexpr int PB_D = PB_LSE + PF_T * 4;
-constexpr int PB_LSEN = PB_D + PF_T * 4;  // the next head's LSE (natural log, LDS-DMA)
-constexpr int PB_CNT = PB_LSEN + PF_T * 4;
-constexpr size_t PB_LDS = PB_CNT + 16;
-
-template <int DM>
-__global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_persist_kernel(AttnParams p, int nitems) {
-  typedef bf16x8 Frag;
-  typedef ImgAtt<128> Img;
-  constexpr int NW = BWD_NT / 64;
-  constexpr int T_ = PF_T, nkt = PF_T / 16;
-  extern __shared__ __attribute__((aligned(16))) char smem_pb[];
-  // LDS pointers from a per-head opaque base (below): otherwise the compiler
-  // hoists every fragment-read address of the head out of the head loop, and the
-  // loop-carried addresses spill
-  char* smem = smem_pb;
-  char* Qimg = smem;
-  char* Dimg = smem + PB_IMG;
-  char* Kimg = smem + 2 * PB_IMG;
-  float* lse_s = (float*)(smem + PB_LSE);
-  unsigned* arrived = (unsigned*)(smem + PB_CNT);
-
-  const int tid = threadIdx.x, lane0 = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int G = gridDim.x;
-  const int k0 = w * 16;  // this wave's keys (phase 1) and queries (D, phase 2)
-  int it = blockIdx.x;
-  if (it >= nitems) return;
-  auto head = [&](int item, const char* base, int64_t ld) {
-    const int b = item / p.H, h = item % p.H;
-    return base + ((int64_t)b * PF_T * ld + h * DH) * 2;
-  };
-  // the wave's two 1 KB pieces of each image (rows 8 (w + 8 u) .., ImgAtt<128>
-  // swizzle on the source chunk, as the forward); the per-lane offsets are
-  // recomputed per head (registers are the binding budget at 4 waves per SIMD)
-  auto issue_images = [&](int item, int lane) {
-    const char* qb = head(item, p.q, p.q_ld);
-    const char* db = head(item, p.dout, p.dout_ld);
-    const char* kb = head(item, p.k, p.k_ld);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int row = (w + 8 * u) * 8 + (lane >> 3), lc = (lane & 7) ^ att_x(row);
-      dma1k(qb + (row * p.q_ld * 2 + lc * 16), Qimg + (w + 8 * u) * 1024);
-      dma1k(db + (row * p.dout_ld * 2 + lc * 16), Dimg + (w + 8 * u) * 1024);
-      dma1k(kb + (row * p.k_ld * 2 + lc * 16), Kimg + (w + 8 * u) * 1024);
-    }
-  };
-  // a head's LSE: 512 bytes by LDS-DMA (waves 0, 1), scaled to log2 units at the head's start
-  auto issue_lse = [&](int item, int lane) {
-    if (w < 2)
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(p.lse + (int64_t)item * PF_T +
-                                                                                        w * 64 + lane),
-                                       (void __attribute__((address_space(3)))*)(smem_pb + PB_LSEN + w * 256), 4, 0, 0);
-  };
-  issue_images(it, lane0);
-  issue_lse(it, lane0);
-  if (tid == 0) *arrived = 0u;
-  const float c2 = p.scale * LOG2E;
-  const bool rope = p.rope_q || p.rope_k;
-  for (;;) {
-    // an opaque zero per head: every lane-dependent address, swizzle and RoPE
-    // angle is recomputed per head instead of hoisted out of the loop (the
-    // hoisted values stayed live across the whole head and spilled)
-    int z;
-    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-    smem = smem_pb + z;
-    const int lane = lane0 + z, g = lane >> 4, c = lane & 15;
-    Qimg = smem;
-    Dimg = smem + PB_IMG;
-    Kimg = smem + 2 * PB_IMG;
-    char* DSimg = smem;
-    char* scratch = smem + PB_STAGE;
-    float* red = (float*)(smem + PB_RED);
-    lse_s = (float*)(smem + PB_LSE);
-    float* d_s = (float*)(smem + PB_D);
-    arrived = (unsigned*)(smem + PB_CNT);
-    const int b = it / p.H, h = it % p.H;
-    const int64_t tok0 = (int64_t)b * T_;
-    Frag fv[2], oo[2];
-    {
-      const bf16* vrow = (const bf16*)p.v + (tok0 + k0 + c) * p.v_ld + h * DH;
-      const bf16* orow = (const bf16*)p.o + (tok0 + k0 + c) * p.o_ld + h * DH;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        gload_frag<bf16>(fv[u], vrow, 32 * u + 8 * g);
-        gload_frag<bf16>(oo[u], orow, 32 * u + 8 * g);
-      }
-    }
-    uint64_t mword = 0;
-    if (DM == 1 && (lane >> 2) < nkt) mword = p.mask[mask_word(it, nkt, lane >> 2, k0 >> 4, lane & 3)];
-    vmcnt_wait<0>();  // this head's images and LSE (issued a head ago), V / O rows
-    __syncthreads();
-    if (tid < PF_T) lse_s[tid] = ((const float*)(smem + PB_LSEN))[tid] * LOG2E;  // read before the barrier below
-    Frag fk[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) frag_row<Img>(fk[u], Kimg, k0 + c, 32 * u + 8 * g);
-    {  // D of queries k0 + c (dO from its image, O from registers)
-      float dpart = 0.f;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        Frag fo;
-        frag_row<Img>(fo, Dimg, k0 + c, 32 * u + 8 * g);
-        dpart = dot8_bf16(fo, oo[u], dpart);
-      }
-      dpart = sum_xor16(dpart);
-      dpart = sum_xor32(dpart);
-      if (g == 0) d_s[k0 + c] = dpart;
-    }
-    __syncthreads();
-    f32x4 dk[4], dv[4];
-    Frag dsf[nkt / 2];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < nkt / 2; ++j) {  // 32-query chunks
-      f32x4 pdv[2], dsv[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int qt = 2 * j + u;
-        f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
-        Frag fb;
-        frag_row<Img>(fb, Qimg, qt * 16 + c, 8 * g);
-        mma16(st, fb, fk[0]);
-        frag_row<Img>(fb, Qimg, qt * 16 + c, 32 + 8 * g);
-        mma16(st, fb, fk[1]);
-        frag_row<Img>(fb, Dimg, qt * 16 + c, 8 * g);
-        mma16(dpt, fb, fv[0]);
-        frag_row<Img>(fb, Dimg, qt * 16 + c, 32 + 8 * g);
-        mma16(dpt, fb, fv[1]);
-        uint32_t nib = 0;
-        if (DM == 1) nib = (uint32_t)(shfl64(mword, 4 * qt + (lane & 3)) >> (16 * (c >> 2) + 4 * g));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = qt * 16 + 4 * g + r;
-          const float pv = fast_exp2(st[r] * c2 - lse_s[q]);
-          float pdr = pv, dpd = dpt[r];
-          if constexpr (DM == 1) {
-            const uint32_t km = keep_mask(nib, r);
-            pdr = and_mask(pv, km);
-            dpd = and_mask(dpd * p.inv_keep, km);
-          } else if constexpr (DM == 2) {
-            const bool keep = nstl_keep(p.seed, drop_idx(it, T_, q, k0 + c), p.thresh);
-            pdr = keep ? pv : 0.f;
-            dpd = keep ? dpd * p.inv_keep : 0.f;
-          }
-          pdv[u][r] = pdr;
-          dsv[u][r] = pv * (dpd - d_s[q]);
-        }
-      }
-      const Frag fa1 = acc_frag<bf16>(pdv[0], pdv[1]);
-      dsf[j] = acc_frag<bf16>(dsv[0], dsv[1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        Frag fb;
-        frag_col2<Img>(fb, Dimg, dt * 16, 32 * j, lane);
-        mma16(dv[dt], fa1, fb);
-        frag_col2<Img>(fb, Qimg, dt * 16, 32 * j, lane);
-        mma16(dk[dt], dsf[j], fb);
-      }
-    }
-    __syncthreads();  // every wave is done with the Q / dO images
-#pragma unroll
-    for (int j = 0; j < nkt / 2; ++j) {
-      const bf16x8 f = dsf[j];
-      *(bf16x4*)(DSimg + DsImg::off(k0 + c, (32 * j + 4 * g) * 2)) = (bf16x4){f[0], f[1], f[2], f[3]};
-      *(bf16x4*)(DSimg + DsImg::off(k0 + c, (32 * j + 16 + 4 * g) * 2)) = (bf16x4){f[4], f[5], f[6], f[7]};
-    }
-    __syncthreads();
-    f32x4 dq[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < nkt / 2; ++j) {
-      Frag fa;
-      frag_col2<DsImg>(fa, DSimg, k0, 32 * j, lane);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        Frag fb;
-        frag_col2<Img>(fb, Kimg, dt * 16, 32 * j, lane);
-        mma16(dq[dt], fa, fb);
-      }
-    }
-    __syncthreads();  // every wave is done with the dS^T and K images
-    const int nxt = it + G;
-    const bool has_next = nxt < nitems;
-    if (has_next) {
-      issue_images(nxt, lane);
-      issue_lse(nxt, lane);
-    }
-    float vq[4][4], vk[4][4], vv[4][4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        vq[dt][r] = dq[dt][r] * p.scale;
-        vk[dt][r] = dk[dt][r] * p.scale;
-        vv[dt][r] = DM != 0 ? dv[dt][r] * p.inv_keep : dv[dt][r];
-      }
-    if (rope) {  // dQ and dK rows are the same 16
-      float tc[4][4], ts[4][4];
-      rope_tab_fast(tc, ts, k0 + 4 * g, c);
-      if (p.rope_q) rope_apply(vq, tc, ts);
-      if (p.rope_k) rope_apply(vk, tc, ts);
-    }
-    char* scr = scratch + w * 16 * DH * 2;
-    const int64_t r0 = tok0 + k0;
-    store_tile16x64<bf16>(vq, scr, p.dq + (r0 * p.dq_ld + h * DH) * 2, p.dq_ld, lane);
-    store_tile16x64<bf16>(vk, scr, p.dk + (r0 * p.dk_ld + h * DH) * 2, p.dk_ld, lane);
-    store_tile16x64<bf16>(vv, scr, p.dv + (r0 * p.dv_ld + h * DH) * 2, p.dv_ld, lane);
-    if (p.dbias) {
-      float* bias_row = p.dbias + (int64_t)b * 3 * p.H * DH;
-      wave_colsum16x64<bf16>(vq, red, w, lane);
-      wave_colsum16x64<bf16>(vk, red + NW * 64, w, lane);
-      wave_colsum16x64<bf16>(vv, red + 2 * NW * 64, w, lane);
-      if (last_to_arrive(arrived, NW, lane)) {
-#pragma unroll
-        for (int m = 0; m < 3; ++m) wave_sum_out(red + m * NW * 64, NW, bias_row + m * p.H * DH + h * DH, lane);
-        if (lane == 0) *arrived = 0u;  // for the next head: every wave passes its barriers after this
-      }
-    }
-    if (!has_next) break;
-    it = nxt;
-  }
-}
-static_assert(PB_LDS <= 80 * 1024, "two workgroups per CU");
 
 size_t fwd_lds_bytes(int T, int esz) {  // K, V images (the output leaves from registers)
   return (size_t)2 * T * DH * esz;
@@ -1749,15 +1506,6 @@ bool use_fused_bwd(const nstl_attn_args* a) {
   return use_fast(a) && a->dtype == NSTL_BF16 && a->T <= FUSED_MAX_T;
 }
 
-// the persistent fused backward (NSTL_ATTN_BWD=persist; T = 128 with RoPE^T
-// recomputed or absent): measured 81 vs 74 us for the one-workgroup-per-head
-// fused kernel at the step's shape (profiles/r4_attn_bwd_persist_ab.txt), off
-bool use_persist_bwd(const nstl_attn_args* a, const AttnParams& p) {
-  const char* e = getenv("NSTL_ATTN_BWD");
-  if (!(e && e[0] == 'p')) return false;
-  return a->T == PF_T && (!(p.rope_q || p.rope_k) || p.rope_fast);
-}
-
 int fill(AttnParams& p, const nstl_attn_args* a, bool bwd) {
   NSTL_CHECK_ARG(a != nullptr, "nstl_attn: null args");
   NSTL_CHECK_ARG(a->dtype == NSTL_F32 || a->dtype == NSTL_BF16, "nstl_attn: bad dtype");
@@ -1905,15 +1653,6 @@ extern "C" int nstl_attn_bwd(const nstl_attn_args* a, void* stream) {
                                     std::max(std::max(a->dq_ld, a->dk_ld), a->dv_ld));
     NSTL_CHECK_ARG((int64_t)a->T * ld_max * 2 < (1ll << 31), "nstl_attn_bwd: T x row stride past 2^31 bytes");
     nstl::count(NSTL_K_ATTN_BWD_FUSED);
-    if (use_persist_bwd(a, p)) {
-      const int nitems = a->B * a->H;
-      const dim3 grid(std::min(nitems, std::max(2, 2 * nstl::stream_cus(st))));
-      if (!p.thresh)
-        return launch(attn_bwd_persist_kernel<0>, grid, PB_LDS, st, p, "nstl_attn_bwd persistent", BWD_NT, nitems);
-      if (p.mask)
-        return launch(attn_bwd_persist_kernel<1>, grid, PB_LDS, st, p, "nstl_attn_bwd persistent", BWD_NT, nitems);
-      return launch(attn_bwd_persist_kernel<2>, grid, PB_LDS, st, p, "nstl_attn_bwd persistent", BWD_NT, nitems);
-    }
     const dim3 grid(1, a->B * a->H);
     if (a->T == FUSED_MAX_T) {  // the production shape: T a compile-time constant
       if (!p.thresh) return launch(attn_bwd_fused_kernel<0, FUSED_MAX_T>, grid, FUSED_LDS, st, p, "nstl_attn_bwd fused", BWD_NT);

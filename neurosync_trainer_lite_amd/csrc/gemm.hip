@@ -302,126 +302,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(GemmParams p) {
 }
 
 
-// ===========================================================================
-// 256x256 tile, 8 waves (2 x 4, each 128 x 64), BK = 64 bf16, LDS-DMA
-// (global_load_lds_dwordx4) staging into two 64 KB buffers, one barrier per K
-// tile.  A 128^2 tile moves (128+128)*2 B per 2*128^2 FLOP = 64 FLOP/B through
-// L2, which at the MFMA rate needs ~39 TB/s (> the ~34.5 TB/s aggregate L2);
-// 256^2 halves that.  The DMA writes LDS lane-linearly (1 KB per wave
-// instruction), so the bank swizzle is applied to the per-lane SOURCE address
-// and undone by the same ImgK / ImgMN read mapping.
-// Preconditions (checked on the host): bf16, K % 64 == 0, 16-byte aligned rows.
-constexpr int BIG = 256, BIG_NT = 512, BIG_TILE = 32768;
-
-template <bool KMAJ, int RB>
-NSTL_DEV void glds_stage(char* img, const char* base, int64_t ld, int row0, int rows_total, int k0, int wave,
-                         int lane) {
-  // 32 wave-instructions of 1 KB per 32 KB tile, 4 per wave
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int q = wave * 4 + s;
-    const char* src;
-    if (KMAJ) {  // 128-byte rows: 8 rows per KB
-      const int row = 8 * q + (lane >> 3), pc = lane & 7;
-      const int lc = pc ^ ((row >> 1) & 7);
-      const int gi = min(row0 + row, rows_total - 1);
-      src = base + ((int64_t)gi * ld + k0 + lc * 8) * 2;
-    } else {     // RB-byte rows (512): 2 rows per KB
-      constexpr int CPR = RB / 16;
-      constexpr int RPK = 1024 / RB;
-      const int row = RPK * q + lane / CPR, pc = lane % CPR;
-      const int x = (row & 3) | (((row >> 3) & 1) << 2);
-      const int lc = pc ^ (x << 1);
-      const int gi = min(row0 + lc * 8, ((rows_total - 1) / 8) * 8);
-      src = base + ((int64_t)(k0 + row) * ld + gi) * 2;
-    }
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                     (void __attribute__((address_space(3)))*)(img + q * 1024), 16, 0, 0);
-  }
-}
-
-template <bool AK, bool BKM>
-__global__ __launch_bounds__(BIG_NT, 2) void gemm256_kernel(GemmParams p) {
-  constexpr int BK = 64;
-  constexpr int MN_RB = BIG * 2;  // 512-byte rows for MN-major images
-  constexpr int A_RB = AK ? 128 : MN_RB;
-  constexpr int B_RB = BKM ? 128 : MN_RB;
-  constexpr int SMEM = 8 * 64 * EPI_LD * 4 > 4 * BIG_TILE ? 8 * 64 * EPI_LD * 4 : 4 * BIG_TILE;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int nt_m = (p.M + BIG - 1) / BIG, nt_n = (p.N + BIG - 1) / BIG;
-  // XCD-contiguous id ranges, then grouped order (GROUP_M row tiles per group,
-  // column-fastest inside): an XCD's 32 co-resident blocks cover ~4 x 8 tiles,
-  // sharing 4 A panels and 8 B panels in its L2.
-  const int id = xcd_remap(blockIdx.x, nt_m * nt_n);
-  constexpr int GROUP_M = 4;
-  const int per_group = GROUP_M * nt_n;
-  const int first_m = (id / per_group) * GROUP_M;
-  const int gm = min(nt_m - first_m, GROUP_M);
-  const int in_g = id % per_group;
-  const int tm = first_m + in_g % gm, tn = in_g / gm;
-  const int m0 = tm * BIG, n0 = tn * BIG;
-  const int kz0 = blockIdx.y * p.k_chunk;
-  const int kz1 = min(p.K, kz0 + p.k_chunk);
-  const int nk = (kz1 - kz0) / BK;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  if (nk > 0) {
-    glds_stage<AK, A_RB>(smem, p.A, p.lda, m0, p.M, kz0, wave, lane);
-    glds_stage<BKM, B_RB>(smem + BIG_TILE, p.B, p.ldb, n0, p.N, kz0, wave, lane);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      const int k1 = kz0 + (kt + 1) * BK;
-      glds_stage<AK, A_RB>(smem + (cur ^ 1) * 2 * BIG_TILE, p.A, p.lda, m0, p.M, k1, wave, lane);
-      glds_stage<BKM, B_RB>(smem + (cur ^ 1) * 2 * BIG_TILE + BIG_TILE, p.B, p.ldb, n0, p.N, k1, wave, lane);
-    }
-    const char* Ai = smem + cur * 2 * BIG_TILE;
-    const char* Bi = Ai + BIG_TILE;
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 fb[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (BKM)
-          frag_row<ImgK<128>>(fb[t], Bi, wn * 64 + t * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4));
-        else
-          frag_col<ImgMN<B_RB>>(fb[t], Bi, wn * 64 + t * 16, kk * 32, lane);
-      }
-      // A fragments double-buffered in registers: the read of fragment a+1 is
-      // issued before the 4 MFMAs of fragment a
-      bf16x8 fa[2];
-      if (AK)
-        frag_row<ImgK<128>>(fa[0], Ai, wm * 128 + (lane & 15), kk * 32 + 8 * (lane >> 4));
-      else
-        frag_col<ImgMN<A_RB>>(fa[0], Ai, wm * 128, kk * 32, lane);
-#pragma unroll
-      for (int a = 0; a < 8; ++a) {
-        if (a + 1 < 8) {
-          if (AK)
-            frag_row<ImgK<128>>(fa[(a + 1) & 1], Ai, wm * 128 + (a + 1) * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4));
-          else
-            frag_col<ImgMN<A_RB>>(fa[(a + 1) & 1], Ai, wm * 128 + (a + 1) * 16, kk * 32, lane);
-        }
-#pragma unroll
-        for (int b = 0; b < 4; ++b) mma16(acc[a][b], fa[a & 1], fb[b]);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  gemm_epilogue<8, 4>(p, acc, m0 + wm * 128, n0 + wn * 64, lane, (float*)&smem[0] + wave * 64 * EPI_LD);
-}
+// 256x256 tiles (the ring kernels below).  A 128^2 tile moves (128+128)*2 B per
+// 2*128^2 FLOP = 64 FLOP/B through L2, which at the MFMA rate needs ~39 TB/s (>
+// the ~34.5 TB/s aggregate L2); 256^2 halves that.  The LDS-DMA writes LDS
+// lane-linearly (1 KB per wave instruction), so the bank swizzle is applied to
+// the per-lane SOURCE address and undone by the same read mapping.
+constexpr int BIG = 256, BIG_NT = 512;
 
 // ===========================================================================
 // 256x256 tile, 8 waves (2 x 4, each 128 x 64), BK = 32, a ring of FIVE 32 KB
@@ -969,15 +855,8 @@ NSTL_DEV unsigned long long rt_stamp() {
 
 // One 256 x 256 output tile of p: `id` is the tile's linear index in p's grid
 // (already XCD-remapped by the caller), `kz` its split-K chunk.
-// Flags of a persistent kernel's split tile (RT_*): the first piece of a tile
-// leaves its f32 accumulators in the workgroup's private slot `part` (lane-
-// linear: register g of thread t at part[g * 512 + t], 1 KB per wave store)
-// instead of an epilogue; the second piece starts from them.
-enum { RT_RESTORE = 1, RT_SAVE = 2 };
-
 template <bool AK, bool BKM, int EM>
-NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz0, int kz1, char* smem, int flags = 0,
-                        f32x4* part = nullptr) {
+NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz0, int kz1, char* smem) {
   NSTL_STAMP(st_entry);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -997,10 +876,6 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz0, int kz1, char* sme
   const RingSrc rs = ring_src<AK, BKM>(p, m0, n0, wave, lane);
 
   f32x4 acc[8][4];
-  // the parked slot through a buffer descriptor: one lane offset (tid * 16) and
-  // a scalar offset per register (global immediates reach only +-4 KB)
-  __amdgpu_buffer_rsrc_t prs;
-  if (flags) prs = __builtin_amdgcn_make_buffer_rsrc(part, 0, BIG * BIG * 4, 0x00020000);
 #pragma unroll
   for (int a = 0; a < 8; ++a)
 #pragma unroll
@@ -1078,37 +953,7 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz0, int kz1, char* sme
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger
   NSTL_STAMP(st_kloop);
-  if (flags & RT_RESTORE) {
-    // add the parked first piece (acc = second + first: f32 rounding differs
-    // from one chain by ~1 ulp).  Loaded one 16-VGPR group ahead: acc starting
-    // from the slot would keep 128 more VGPRs live through the prologue (spills).
-    f32x4 nx[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      nx[b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, tid * 16, b * BIG_NT * 16, 0));
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      f32x4 cur[4];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) cur[b] = nx[b];
-      if (a + 1 < 8) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          nx[b] = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, tid * 16, ((a + 1) * 4 + b) * BIG_NT * 16, 0));
-      }
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] += cur[b];
-    }
-  }
-  if (flags & RT_SAVE) {
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, acc[a][b]), prs, tid * 16,
-                                               (a * 4 + b) * BIG_NT * 16, 0);
-  } else if (p.debug_skip_epilogue == 1) {  // timing experiments only (NSTL_GEMM_DEBUG=skip_epi)
+  if (p.debug_skip_epilogue == 1) {  // timing experiments only (NSTL_GEMM_DEBUG=skip_epi)
 #pragma unroll
     for (int a = 0; a < 8; ++a)
 #pragma unroll
@@ -1132,7 +977,7 @@ NSTL_DEV void ring_tile(const GemmParams& p, int id, int kz0, int kz1, char* sme
     s[0] = st_entry; s[1] = st_prologue; s[2] = st_kloop; s[3] = st_epi;
     s[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
     s[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    s[6] = id | ((unsigned long long)flags << 32); s[7] = nk;
+    s[6] = id; s[7] = nk;
   }
 #endif
 }
@@ -1143,448 +988,6 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm256r_kernel(GemmParams p) {
   const int nt = ((p.M + BIG - 1) / BIG) * ((p.N + BIG - 1) / BIG);
   const int kb = blockIdx.y * p.k_chunk;
   ring_tile<AK, BKM, EM>(p, xcd_remap(blockIdx.x, nt), kb, min(p.K, kb + p.k_chunk), smem);
-}
-
-// Persistent form for multi-round problems (tiles = rounds x gridDim.x): workgroup
-// w runs the tiles of blocks w, w + G, w + 2G, ... of the one-shot grid (same
-// XCD-aware tile order).  In the one-shot grid every CU finishes a round at the
-// same moment, so all 256 write their 32 MB of output at once (HBM-bound, the
-// MFMAs idle) and then wait for the next round's dispatch.  Here the eight XCDs
-// run out of phase: on XCD x (read from XCC_ID; placement only affects speed)
-// the first tile is cut at K-step x*nk/8, its first piece parked in the
-// workgroup's private f32 slot and finished last, so XCD x's tile boundaries
-// (epilogue bursts, prologue fills) fall x/8 of a tile later than XCD 0's.
-template <bool AK, bool BKM, int EM>
-__global__ __launch_bounds__(BIG_NT, 1) void gemm256p_kernel(GemmParams p, int rounds, f32x4* parts) {
-  __shared__ __attribute__((aligned(16))) char smem[R_SMEM];
-  const int G = gridDim.x, w = blockIdx.x;
-  const int nt = rounds * G;
-  const int nk = p.K / R_BK;
-  const int xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7;
-  const int cut = p.debug_skip_epilogue == 3 ? 0 : ((xcc * nk) >> 3) * R_BK;  // K index of the cut (0: none)
-  f32x4* part = parts + (int64_t)w * (BIG * BIG / 4);
-  // segments: [tile 0 to the cut, parked] tiles 1..rounds-1 [tile 0 from the cut]
-  // (one ring_tile call site: inlining it per segment kind spills registers)
-  const int nseg = rounds + (cut > 0 ? 1 : 0);
-  for (int sg = 0; sg < nseg; ++sg) {
-    const int j = sg < rounds ? sg : 0;
-    int kb = 0, ke = p.K, flags = 0;
-    if (cut > 0 && sg == 0) { ke = cut; flags = RT_SAVE; }
-    if (cut > 0 && sg == rounds) { kb = cut; flags = RT_RESTORE; }
-    if (sg > 0) __syncthreads();  // the previous tile's epilogue scratch is free
-    ring_tile<AK, BKM, EM>(p, xcd_remap(w + j * G, nt), kb, ke, smem, flags, part);
-  }
-}
-
-// Persistent, cross-tile pipelined form (r3, NSTL_GEMM_PQ=1; bf16 output without
-// beta on full tiles, the register-direct epilogue).  One workgroup per CU runs
-// its tiles (w, w + G, ...: the one-shot grid's XCD-aware order) as ONE
-// continuous stream of K-steps: the last three K-steps of tile i stage tile
-// i + 1's first three, so the ring never drains and there is no prologue or
-// workgroup dispatch between tiles.  The epilogue writes straight from the
-// accumulators (no LDS, no barrier), so each wave group does it between its own
-// M(last) and R(first) of the next tile; its 16 stores per wave sit in vmcnt
-// between the next tile's stages 2 and 3, and the first two K-steps of the next
-// tile count them (vmcnt(24) instead of 8): the stores retire under those
-// K-steps instead of holding the next loads.  The first K-step of a tile starts
-// its accumulators from the MFMA's zero operand.
-constexpr int PQ_ST = 16;  // global stores per wave of ring_epi_bf16_direct_b (checked in the ISA)
-
-NSTL_DEV void pq_tile(const GemmParams& p, int id, int& m0, int& n0) {
-  const int nt_n = (p.N + BIG - 1) / BIG, nt_m = (p.M + BIG - 1) / BIG;
-  constexpr int GROUP_M = 4;
-  const int per_group = GROUP_M * nt_n;
-  const int first_m = (id / per_group) * GROUP_M;
-  const int gm = min(nt_m - first_m, GROUP_M);
-  const int in_g = id % per_group;
-  m0 = (first_m + in_g % gm) * BIG;
-  n0 = (in_g / gm) * BIG;
-}
-
-template <bool AK, bool BKM>
-__global__ __launch_bounds__(BIG_NT, 1) void gemm256q_kernel(GemmParams p, int rounds) {
-  __shared__ __attribute__((aligned(16))) char smem[R_SMEM];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int G = gridDim.x, w = blockIdx.x;
-  const int nt = rounds * G;
-  const int nk = p.K / R_BK;
-  const uint32_t smem_u32 = lds_u32(smem);
-  int m0, n0, nm0 = 0, nn0 = 0;
-  pq_tile(p, xcd_remap(w, nt), m0, n0);
-  RingSrc rs = ring_src<AK, BKM>(p, m0, n0, wave, lane), rn = rs;
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) ring_stage(smem + s * R_SLOT, rs, s * R_BK, wave);
-  NSTL_VMCNT(0);  // all three landed: the head steps' vmcnt(24) then holds for tile 0 too
-  __builtin_amdgcn_s_barrier();
-  if (wm == 1) __builtin_amdgcn_s_barrier();  // the stagger (kept across tiles)
-  int slot = 0;
-  // stage: 0 none, 1 this tile's K-step kt + 3, 2 the next tile's K-step kt + 3 - nk.
-  // W: the wait count (a compile-time constant at each call site: a runtime
-  // choice between s_waitcnt immediates costs taken branches every K-step).
-  auto step = [&](int kt, int stage, auto W) {
-    constexpr int wait = decltype(W)::value;
-    const uint32_t Ai = smem_u32 + slot * R_SLOT;
-    const uint32_t Bi = Ai + R_SLOT / 2;
-    bf16x8 fb[4], fa[8];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (BKM) asm_frag_k64(fb[t], Bi, wn * 64 + t * 16 + (lane & 15), 8 * (lane >> 4));
-      else asm_frag_mn512(fb[t], Bi, wn * 64 + t * 16, lane);
-    }
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      if (AK) asm_frag_k64(fa[a], Ai, wm * 128 + a * 16 + (lane & 15), 8 * (lane >> 4));
-      else asm_frag_mn512(fa[a], Ai, wm * 128 + a * 16, lane);
-    }
-    if (stage) {
-      int s3 = slot + 3;
-      if (s3 >= R_STAGES) s3 -= R_STAGES;
-      if (stage == 1) ring_stage(smem + s3 * R_SLOT, rs, (kt + 3) * R_BK, wave);
-      else ring_stage(smem + s3 * R_SLOT, rn, (kt + 3 - nk) * R_BK, wave);
-    }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) mma16(acc[a][b], fb[b], fa[a]);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait) : "memory");
-    __builtin_amdgcn_s_barrier();
-    slot = slot + 1 == R_STAGES ? 0 : slot + 1;
-  };
-  using W8 = std::integral_constant<int, 8>;
-  using W24 = std::integral_constant<int, PQ_ST + 8>;
-  // three loops per tile (three step call sites, as the one-shot kernel's four:
-  // more sites gave the accumulators different registers per site and spilled)
-  for (int i = 0; i < rounds; ++i) {
-    const bool last = i + 1 == rounds;
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // K-steps 0, 1: the previous tile's 16 stores may still fly (counted: S(k+1)
-    // is retired with S(k+2), the stores and S(k+3) younger)
-    for (int kt = 0; kt < 2; ++kt) step(kt, 1, W24());
-    for (int kt = 2; kt < nk - 3; ++kt) step(kt, 1, W8());
-    // the next tile's sources (live for three K-steps); the last tile stages its
-    // own first three K-steps again into slots nobody reads (no drain variant of
-    // the step, so the accumulators keep one register assignment), retired by
-    // the vmcnt(0) before the workgroup ends
-    pq_tile(p, xcd_remap(w + (last ? i : i + 1) * G, nt), nm0, nn0);
-    rn = ring_src<AK, BKM>(p, nm0, nn0, wave, lane);
-    for (int kt = nk - 3; kt < nk; ++kt) step(kt, 2, W8());
-    // the epilogue from registers: the bias loads, then every older operation
-    // (the next tile's three staged K-steps) and the bias retire, then the 16
-    // stores go out behind them (no bias: no loads, and no wait at all)
-    if (p.bias != nullptr) {
-      float bs[4][4];
-      load_bias16(bs, p, n0 + wn * 64, lane);
-      NSTL_VMCNT(0);
-      ring_epi_bf16_direct_b(p, acc, bs, m0 + wm * 128, n0 + wn * 64, lane);
-    } else {  // a separate path: a merge with the loads above makes the compiler wait vmcnt(0)
-      const float bs[4][4] = {};
-      ring_epi_bf16_direct_b(p, acc, bs, m0 + wm * 128, n0 + wn * 64, lane);
-    }
-    m0 = nm0;
-    n0 = nn0;
-    rs = rn;
-  }
-  NSTL_VMCNT(0);  // the last tile's re-staged K-steps land before the workgroup ends
-  if (wm == 0) __builtin_amdgcn_s_barrier();  // close the stagger
-}
-
-// Grouped launch: independent problems of one kind back to back in one grid
-// (block b -> problem g with tile_end[g-1] <= b' < tile_end[g], b' XCD-remapped
-// over all tiles).  One launch of a decoder layer's ~256 weight-gradient tiles
-// fills the chip for one round with no split-K partials to reduce.
-struct GroupParams {
-  GemmParams g[NSTL_GEMM_GROUP_MAX];
-  int tile_end[NSTL_GEMM_GROUP_MAX];
-  int n;
-};
-
-template <bool AK, bool BKM, int EM>
-__global__ __launch_bounds__(BIG_NT, 1) void gemm256r_group_kernel(GroupParams gp) {
-  __shared__ __attribute__((aligned(16))) char smem[R_SMEM];
-  const int gid = xcd_remap(blockIdx.x, gp.tile_end[gp.n - 1]);
-  int g = 0;
-  while (g + 1 < gp.n && gid >= gp.tile_end[g]) ++g;
-  const GemmParams& p = gp.g[g];
-  ring_tile<AK, BKM, EM>(p, gid - (g > 0 ? gp.tile_end[g - 1] : 0), 0, p.K, smem);
-}
-
-// ===========================================================================
-// Two workgroups per CU (NSTL_GEMM_H): a 128 (M) x 256 (N) tile on 4 waves, one
-// per SIMD, each owning 128 x 64 -- the per-wave work of the 256^2 ring kernel
-// (8 A + 4 B fragments, 32 MFMAs per 32-deep K-step) -- with a ring of three
-// 24 KB LDS-DMA stages (A 128 x 32 + B 256 x 32 bf16: 72 KB), so two
-// workgroups fit on a CU (144 of 160 KB) and every SIMD runs one wave of each.
-// The workgroups are independent: one workgroup's epilogue, prologue and
-// dispatch gap run beside the other's K loop on the same CU, where the
-// one-workgroup 256^2 kernel leaves the matrix pipes idle for ~10 us per round
-// ("Where a GEMM round's fixed cost goes"), and the partner
-// wave on a SIMD fills the barrier and fragment-read gaps of this one (the role
-// the stagger plays inside the 8-wave kernel).
-// Step s: wait for this wave's share of stage s; barrier (stage s has landed for
-// every wave, and every wave has its fragments of stage s-1 in registers, so
-// its slot is free); stage s+2 into that slot; fragment reads of stage s; 32
-// MFMAs.  One barrier per K-step, two stages in flight.
-#ifndef NSTL_GEMMH_MODE
-#define NSTL_GEMMH_MODE 2
-#endif
-constexpr int H_BM = 128, H_NT = 256, H_SLOT = 24576, H_STAGES = 3, H_A = 8192;
-constexpr int H_SMEM = H_STAGES * H_SLOT;
-static_assert(4 * RING_EPI_WAVE <= H_SMEM, "epilogue scratch must fit in the ring");
-
-// per-lane LDS-DMA sources of wave-instructions q0 .. q0+NQ-1 of one operand image
-// (the glds_src32 layouts: K-major 64-byte rows with kswz, or ImgMN<512>)
-template <bool KMAJ, int NQ>
-NSTL_DEV void glds_src_q(const char* (&src)[NQ], const char* base, int64_t ld, int row0, int rows_total, int q0,
-                         int lane) {
-#pragma unroll
-  for (int s = 0; s < NQ; ++s) {
-    const int q = q0 + s;
-    if (KMAJ) {
-      const int row = 16 * q + (lane >> 2), ch = (lane & 3) ^ kswz(row);
-      const int gi = min(row0 + row, rows_total - 1);
-      src[s] = base + ((int64_t)gi * ld + ch * 8) * 2;
-    } else {
-      const int row = 2 * q + (lane >> 5), pc = lane & 31;
-      const int x = (row & 3) | (((row >> 3) & 1) << 2);
-      const int lc = pc ^ (x << 1);
-      const int gi = min(row0 + lc * 8, ((rows_total - 1) / 8) * 8);
-      src[s] = base + ((int64_t)row * ld + gi) * 2;
-    }
-  }
-}
-
-template <int NQ>
-NSTL_DEV void glds_issue_q(char* img, const char* const (&src)[NQ], int64_t off, int q0) {
-#pragma unroll
-  for (int s = 0; s < NQ; ++s)
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src[s] + off),
-                                     (void __attribute__((address_space(3)))*)(img + (q0 + s) * 1024), 16, 0, 0);
-}
-
-// One 128 x 256 tile of p over K range [kz0, kz1) (`id` already XCD-remapped).
-// flags (RT_*): RT_SAVE parks the f32 accumulators in the workgroup's private
-// slot `part` instead of an epilogue; RT_RESTORE adds the parked piece before it
-// (register g of thread t at part[g * 256 + t]).
-template <bool BKM, int EM>
-NSTL_DEV void h_tile(const GemmParams& p, int id, int kz0, int kz1, char* smem, int flags = 0,
-                     f32x4* part = nullptr) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nt_n = (p.N + BIG - 1) / BIG, nt_m = (p.M + H_BM - 1) / H_BM;
-  // grouped order over XCD-contiguous id ranges: an XCD's 64 co-resident
-  // workgroups cover ~8 x 8 tiles (8 A panels of 128 rows, 8 B panels of 256 columns)
-  constexpr int GROUP_M = 8;
-  const int per_group = GROUP_M * nt_n;
-  const int first_m = (id / per_group) * GROUP_M;
-  const int gm = min(nt_m - first_m, GROUP_M);
-  const int in_g = id % per_group;
-  const int tm = first_m + in_g % gm, tn = in_g / gm;
-  const int m0 = tm * H_BM, n0 = tn * BIG;
-  const int nk = (kz1 - kz0) / R_BK;
-  const uint32_t smem_u32 = lds_u32(smem);
-  const char* sa[2];
-  const char* sb[4];
-  glds_src_q<true, 2>(sa, p.A, p.lda, m0, p.M, wave * 2, lane);
-  glds_src_q<BKM, 4>(sb, p.B, p.ldb, n0, p.N, wave * 4, lane);
-  const int64_t b_kb = BKM ? 2 : 2 * p.ldb;
-  auto stage = [&](int slot, int k0) {
-    char* img = smem + slot * H_SLOT;
-    glds_issue_q<2>(img, sa, (int64_t)k0 * 2, wave * 2);
-    glds_issue_q<4>(img + H_A, sb, (int64_t)k0 * b_kb, wave * 4);
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  __amdgpu_buffer_rsrc_t prs;
-  if (flags) prs = __builtin_amdgcn_make_buffer_rsrc(part, 0, H_BM * BIG * 4, 0x00020000);
-
-  // NSTL_GEMMH_MODE (compile time, experiments): bit 0 progressive fragment waits
-  // (the MFMAs of A fragment a start once it has landed), bit 1 (default) the
-  // stage's six LDS-DMA pieces issued between the MFMA groups instead of ahead of
-  // the fragment reads, bit 2 static priority by the workgroup's slot on its CU
-  // (HW_ID TG_ID parity).  Measured (profiles/r3_gemmh_modes.txt): 2 is the
-  // fastest; 1 and 4 do not help.
-  constexpr int HM = NSTL_GEMMH_MODE;
-  bool prio_hi = false;
-  if (HM & 4) prio_hi = ((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 16) & 1) != 0;
-  if (prio_hi) __builtin_amdgcn_s_setprio(2);
-  stage(0, kz0);
-  if (nk > 1) stage(1, kz0 + R_BK);
-  int slot = 0;
-  // last: no stage is in flight behind this one (wait for all)
-  auto step = [&](int kt, bool stage2, bool last) {
-    if (last) NSTL_VMCNT(0);
-    else NSTL_VMCNT(6);
-    __builtin_amdgcn_s_barrier();
-    int s2 = slot + 2;
-    if (s2 >= H_STAGES) s2 -= H_STAGES;
-    char* const img2 = smem + s2 * H_SLOT;
-    const int64_t k2 = (int64_t)kz0 + (kt + 2) * R_BK;
-    if (stage2 && !(HM & 2)) stage(s2, (int)k2);
-    const uint32_t Ai = smem_u32 + slot * H_SLOT;
-    const uint32_t Bi = Ai + H_A;
-    bf16x8 fb[4], fa[8];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (BKM) asm_frag_k64(fb[t], Bi, wave * 64 + t * 16 + (lane & 15), 8 * (lane >> 4));
-      else asm_frag_mn512(fb[t], Bi, wave * 64 + t * 16, lane);
-    }
-#pragma unroll
-    for (int a = 0; a < 8; ++a) asm_frag_k64(fa[a], Ai, a * 16 + (lane & 15), 8 * (lane >> 4));
-    if (!(HM & 1)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (prio_hi) __builtin_amdgcn_s_setprio(3);
-    else __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      if (HM & 1) {
-        // LDS reads return in order: fragment a has landed once at most 7 - a
-        // (B: one ds_read_b128 per fragment, or two transpose reads, all issued
-        // before the A reads) are outstanding
-        if (a == 0) asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
-        else if (a == 1) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
-        else if (a == 2) asm volatile("s_waitcnt lgkmcnt(5)" ::: "memory");
-        else if (a == 3) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-        else if (a == 4) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
-        else if (a == 5) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-        else if (a == 6) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int b = 0; b < 4; ++b) mma16(acc[a][b], fb[b], fa[a]);
-      if ((HM & 2) && stage2 && a < 6) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (a < 2) glds_issue_q<1>(img2, *(const char* const(*)[1]) & sa[a], k2 * 2, wave * 2 + a);
-        else glds_issue_q<1>(img2 + H_A, *(const char* const(*)[1]) & sb[a - 2], k2 * b_kb, wave * 4 + a - 2);
-      }
-      if (HM & 3) __builtin_amdgcn_sched_barrier(0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (prio_hi) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(0);
-    slot = slot + 1 == H_STAGES ? 0 : slot + 1;
-  };
-  if (nk >= 2) {
-    for (int kt = 0; kt + 2 < nk; ++kt) step(kt, true, false);
-    step(nk - 2, false, false);
-    step(nk - 1, false, true);
-  } else if (nk == 1) {
-    step(0, false, true);
-  }
-  if (flags & RT_RESTORE) {
-    // the parked first piece, loaded one 16-VGPR group ahead (acc = second + first)
-    f32x4 nx[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      nx[b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, tid * 16, b * H_NT * 16, 0));
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      f32x4 cur[4];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) cur[b] = nx[b];
-      if (a + 1 < 8) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          nx[b] = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, tid * 16, ((a + 1) * 4 + b) * H_NT * 16, 0));
-      }
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] += cur[b];
-    }
-  }
-  const int col0 = n0 + wave * 64;
-  if (flags & RT_SAVE) {
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, acc[a][b]), prs, tid * 16,
-                                               (a * 4 + b) * H_NT * 16, 0);
-  } else if (p.debug_skip_epilogue == 1) {  // timing experiments only (NSTL_GEMM_DEBUG=skip_epi)
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(acc[a][b]));
-  } else if (EM == EM_BF16 && p.direct_epi && m0 + H_BM <= p.M && n0 + BIG <= p.N) {
-    ring_epi_bf16_direct(p, acc, m0, col0, lane);
-  } else {
-    __syncthreads();  // every wave is done with the ring: it becomes scratch
-    char* scr = smem + wave * RING_EPI_WAVE;
-    if (EM == EM_GENERIC) ring_epi_generic(p, acc, m0, col0, lane, scr);
-    else ring_epi<EM, false>(p, acc, m0, col0, lane, scr, 0);
-  }
-}
-
-template <bool BKM, int EM>
-__global__ __launch_bounds__(H_NT, 2) void gemmh_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[H_SMEM];
-  const int nt = ((p.M + H_BM - 1) / H_BM) * ((p.N + BIG - 1) / BIG);
-  h_tile<BKM, EM>(p, xcd_remap(blockIdx.x, nt), 0, p.K, smem);
-}
-
-// Persistent form (tiles = rounds x gridDim.x, grid = two workgroups per CU):
-// workgroup w runs the tiles of blocks w, w + G, ... of the one-shot grid.  Two
-// co-resident workgroups that start together run their tiles in lockstep, so
-// their epilogues and prologues coincide and nothing hides them (measured: the
-// one-shot grid hides no per-round cost).  One of the pair (HW_ID TG_ID odd:
-// its slot on the CU; placement only affects speed) therefore cuts its first
-// tile at half its K range: the first piece is parked in the workgroup's f32
-// slot and finished last, so its tile boundaries fall half a tile after its
-// partner's and each one's epilogue runs beside the other's K loop.
-template <bool BKM, int EM>
-__global__ __launch_bounds__(H_NT, 2) void gemmhp_kernel(GemmParams p, int rounds, f32x4* parts) {
-  __shared__ __attribute__((aligned(16))) char smem[H_SMEM];
-  const int G = gridDim.x, w = blockIdx.x;
-  const int nt = rounds * G;
-  const int nk = p.K / R_BK;
-  const bool odd = ((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 16) & 1) != 0 && p.debug_skip_epilogue != 3;
-  const int cut = odd ? (nk >> 1) * R_BK : 0;  // K index of the cut (0: none)
-  f32x4* part = parts + (int64_t)w * (H_BM * BIG / 4);
-  // segments: [tile 0 to the cut, parked] tiles 1..rounds-1 [tile 0 from the cut]
-  // (one h_tile call site: inlining it per segment kind spills registers)
-  const int nseg = rounds + (cut > 0 ? 1 : 0);
-  for (int sg = 0; sg < nseg; ++sg) {
-    const int j = sg < rounds ? sg : 0;
-    int kb = 0, ke = p.K, flags = 0;
-    if (cut > 0 && sg == 0) { ke = cut; flags = RT_SAVE; }
-    if (cut > 0 && sg == rounds) { kb = cut; flags = RT_RESTORE; }
-    if (sg > 0) __syncthreads();  // the previous tile's epilogue scratch / ring is free
-    h_tile<BKM, EM>(p, xcd_remap(w + j * G, nt), kb, ke, smem, flags, part);
-  }
-}
-
-template <bool BKM>
-void launch_h_em(int em, dim3 grid, hipStream_t st, const GemmParams& p, int rounds = 0, f32x4* parts = nullptr) {
-  dim3 block(H_NT);
-#define NSTL_H_LAUNCH(EMv)                                                                        \
-  if (rounds > 0) hipLaunchKernelGGL((gemmhp_kernel<BKM, EMv>), grid, block, 0, st, p, rounds, parts); \
-  else hipLaunchKernelGGL((gemmh_kernel<BKM, EMv>), grid, block, 0, st, p);
-  switch (em) {
-    case EM_BF16: NSTL_H_LAUNCH(EM_BF16) break;
-    case EM_RELU_DROP: NSTL_H_LAUNCH(EM_RELU_DROP) break;
-    case EM_ROPE: NSTL_H_LAUNCH(EM_ROPE) break;
-    case EM_DRELU: NSTL_H_LAUNCH(EM_DRELU) break;
-    case EM_F32: NSTL_H_LAUNCH(EM_F32) break;
-    default: hipLaunchKernelGGL((gemmh_kernel<BKM, EM_GENERIC>), grid, block, 0, st, p); break;
-  }
-#undef NSTL_H_LAUNCH
 }
 
 // ===========================================================================
@@ -1799,154 +1202,17 @@ __global__ void splitk_reduce(const float* ws, int splits, int M, int N, char* C
   }
 }
 
-// NSTL_GEMM_RING=0 selects the two-stage BK=64 kernel (A/B comparisons)
-bool getenv_ring() {
-  static const int v = [] {
-    const char* e = getenv("NSTL_GEMM_RING");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return v != 0;
-}
-
-// NSTL_GEMM_PERSIST=1 runs multi-round problems on the persistent XCD-phased
-// kernel (off: measured slower, DESIGN.md section 4 "Persistent, XCD-phased")
-bool getenv_persist() {
-  static const int v = [] {
-    const char* e = getenv("NSTL_GEMM_PERSIST");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v != 0;
-}
-
-// NSTL_GEMM_PQ=1: the persistent cross-tile pipelined kernel (gemm256q_kernel)
-// (2: also single-round problems -- a diagnostic of the per-K-step cost)
-int getenv_pq() {
-  static const int v = [] {
-    const char* e = getenv("NSTL_GEMM_PQ");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-
-// the persistent kernel's split-tile slots: one 256 KB f32 slot per workgroup,
-// owned by the library per (device, stream) so launches on different streams
-// never share one
-f32x4* persist_slots(hipStream_t st, int G) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, std::pair<f32x4*, int>> slots;
-  const int dev = nstl::stream_device(st);  // the stream's device, not the current one
-  std::lock_guard<std::mutex> lk(mu);
-  auto& e = slots[{dev, st}];
-  if (e.second < G) {
-    nstl::DeviceGuard on(dev);
-    if (e.first) (void)hipFree(e.first);
-    e.first = nullptr;
-    e.second = 0;
-    if (hipMalloc((void**)&e.first, (size_t)G * BIG * BIG * sizeof(float)) != hipSuccess) return nullptr;
-    e.second = G;
-  }
-  return e.first;
-}
-
-template <bool AK, bool BKM>
-void launch_persist_em(int em, int G, int rounds, hipStream_t st, const GemmParams& p, f32x4* parts) {
-  dim3 grid(G), block(BIG_NT);
-  switch (em) {
-    case EM_BF16: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_BF16>), grid, block, 0, st, p, rounds, parts); break;
-    case EM_RELU_DROP: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_RELU_DROP>), grid, block, 0, st, p, rounds, parts); break;
-    case EM_ROPE: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_ROPE>), grid, block, 0, st, p, rounds, parts); break;
-    case EM_DRELU: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_DRELU>), grid, block, 0, st, p, rounds, parts); break;
-    default: hipLaunchKernelGGL((gemm256p_kernel<AK, BKM, EM_F32>), grid, block, 0, st, p, rounds, parts); break;
-  }
-}
-
-// NSTL_GEMM_H: 1 runs K-major-A problems without split-K on the two-workgroups-
-// per-CU 128 x 256 kernel (gemmh_kernel); 0 keeps the 256^2 ring kernel
-int getenv_gemm_h() {
-  static const int v = [] {
-    const char* e = getenv("NSTL_GEMM_H");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 int launch_big(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t st) {
   const int nt = ((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
   dim3 grid(nt, splits), block(BIG_NT);
-  if (getenv_ring()) {
-    const int em = ring_epi_mode(a, p);
-    const int hmode = getenv_gemm_h();
-    if (hmode && splits == 1 && a->a_kmajor) {
-      const int nth = ((a->M + H_BM - 1) / H_BM) * ((a->N + BIG - 1) / BIG);
-      const int G = 2 * nstl::stream_cus(st);
-      const bool multi = em != EM_GENERIC && em != EM_WS && G > 0 && nth % G == 0 && nth / G >= 2 &&
-                         a->K % (4 * R_BK) == 0;
-      if (hmode == 1 || multi) {
-        f32x4* parts = nullptr;
-        if (hmode == 2) {
-          parts = persist_slots(st, G);  // 256 KB slots: the 128 x 256 tile needs half
-          NSTL_CHECK_ARG(parts != nullptr, "nstl_gemm: persistent slot allocation failed");
-        }
-        const dim3 grid(hmode == 2 ? G : nth);
-        const int rounds = hmode == 2 ? nth / G : 0;
-        if (a->b_kmajor) launch_h_em<true>(em, grid, st, p, rounds, parts);
-        else launch_h_em<false>(em, grid, st, p, rounds, parts);
-        NSTL_LAUNCH_CHECK("nstl_gemm (128x256 two per CU)");
-        nstl::count(NSTL_K_GEMM_RING);
-        nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt);
-        return 0;
-      }
-    }
-    // NSTL_GEMM_PQ=1: multi-round bf16 problems with the plain (bias) epilogue on
-    // full tiles run on the persistent cross-tile pipelined kernel
-    {
-      const int G = nstl::stream_cus(st);
-      if (getenv_pq() && splits == 1 && em == EM_BF16 && p.direct_epi && a->M % BIG == 0 && a->N % BIG == 0 &&
-          G > 0 && nt % G == 0 && nt / G >= (getenv_pq() == 2 ? 1 : 2) && a->K % R_BK == 0 && a->K / R_BK >= 6 &&
-          a->a_kmajor && p.debug_skip_epilogue == 0) {
-        dim3 g(G), b(BIG_NT);
-        if (a->a_kmajor && a->b_kmajor) hipLaunchKernelGGL((gemm256q_kernel<true, true>), g, b, 0, st, p, nt / G);
-        else hipLaunchKernelGGL((gemm256q_kernel<true, false>), g, b, 0, st, p, nt / G);
-        NSTL_LAUNCH_CHECK("nstl_gemm (256 cross-tile persistent)");
-        nstl::count(NSTL_K_GEMM_RING);
-        nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt);
-        return 0;
-      }
-    }
-    // multi-round problems with a lean epilogue: the persistent XCD-phased kernel
-    const int G = nstl::stream_cus(st);
-    const bool lean = em == EM_BF16 || em == EM_RELU_DROP || em == EM_ROPE || em == EM_DRELU || em == EM_F32;
-    if (getenv_persist() && splits == 1 && lean && (a->a_kmajor || !a->b_kmajor) && G > 0 && nt % G == 0 &&
-        nt / G >= 2 && a->K % (8 * R_BK) == 0) {
-      f32x4* parts = persist_slots(st, G);
-      NSTL_CHECK_ARG(parts != nullptr, "nstl_gemm: persistent slot allocation failed");
-      if (a->a_kmajor && a->b_kmajor) launch_persist_em<true, true>(em, G, nt / G, st, p, parts);
-      else if (a->a_kmajor) launch_persist_em<true, false>(em, G, nt / G, st, p, parts);
-      else launch_persist_em<false, false>(em, G, nt / G, st, p, parts);
-      NSTL_LAUNCH_CHECK("nstl_gemm (256 persistent)");
-      nstl::count(NSTL_K_GEMM_RING);
-      nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt);
-      return 0;
-    }
-    if (a->a_kmajor && a->b_kmajor) launch_ring_em<true, true>(em, grid, block, st, p);
-    else if (a->a_kmajor && !a->b_kmajor) launch_ring_em<true, false>(em, grid, block, st, p);
-    else if (!a->a_kmajor && !a->b_kmajor) launch_ring_em<false, false>(em, grid, block, st, p);
-    else launch_ring_em<false, true>(em, grid, block, st, p);
-    NSTL_LAUNCH_CHECK("nstl_gemm (256 ring)");
-    nstl::count(NSTL_K_GEMM_RING);
-    nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt * splits);
-    return 0;
-  }
-  if (a->a_kmajor && a->b_kmajor)
-    hipLaunchKernelGGL((gemm256_kernel<true, true>), grid, block, 0, st, p);
-  else if (a->a_kmajor && !a->b_kmajor)
-    hipLaunchKernelGGL((gemm256_kernel<true, false>), grid, block, 0, st, p);
-  else if (!a->a_kmajor && !a->b_kmajor)
-    hipLaunchKernelGGL((gemm256_kernel<false, false>), grid, block, 0, st, p);
-  else
-    hipLaunchKernelGGL((gemm256_kernel<false, true>), grid, block, 0, st, p);
-  NSTL_LAUNCH_CHECK("nstl_gemm (256)");
+  const int em = ring_epi_mode(a, p);
+  if (a->a_kmajor && a->b_kmajor) launch_ring_em<true, true>(em, grid, block, st, p);
+  else if (a->a_kmajor && !a->b_kmajor) launch_ring_em<true, false>(em, grid, block, st, p);
+  else if (!a->a_kmajor && !a->b_kmajor) launch_ring_em<false, false>(em, grid, block, st, p);
+  else launch_ring_em<false, true>(em, grid, block, st, p);
+  NSTL_LAUNCH_CHECK("nstl_gemm (256 ring)");
+  nstl::count(NSTL_K_GEMM_RING);
+  nstl::count(NSTL_K_GEMM_RING_TILES, (long long)nt * splits);
   return 0;
 }
 
@@ -1967,11 +1233,12 @@ int launch_typed(const nstl_gemm_args* a, GemmParams& p, int splits, hipStream_t
   return 0;
 }
 
-// NSTL_GEMM_DEBUG=skip_epi: the ring kernel stores nothing (timing experiments only)
+// NSTL_GEMM_DEBUG=skip_epi / skip_store: the ring kernel computes no epilogue /
+// stores nothing (timing experiments only: wrong results)
 int getenv_debug_skip_epi() {
   static const int v = [] {
     const char* e = getenv("NSTL_GEMM_DEBUG");
-    return !e ? 0 : std::string(e) == "skip_epi" ? 1 : std::string(e) == "skip_store" ? 2 : std::string(e) == "nocut" ? 3 : 0;
+    return !e ? 0 : std::string(e) == "skip_epi" ? 1 : std::string(e) == "skip_store" ? 2 : 0;
   }();
   return v;
 }
@@ -2085,6 +1352,7 @@ int gemm_f8(const nstl_gemm_args* a, GemmParams& p, hipStream_t st) {
   }
   NSTL_LAUNCH_CHECK("nstl_gemm (FP8)");
   nstl::count(NSTL_K_GEMM_FP8);
+  if (em == EM_ROPE) nstl::count(NSTL_K_GEMM_FP8_ROPE);
   return 0;
 }
 
@@ -2119,7 +1387,7 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
   // 256 kernel ties the 128 kernel split 8 ways: 60 vs 61 us, tools/bench_gemm_epi.py)
   const bool big = big_ok(a);
   NSTL_CHECK_ARG(!a->colsum_part || (big && a->epilogue == NSTL_EPI_DRELU_DROP && a->split_k <= 1 &&
-                                      ring_epi_mode(a, p) == EM_DRELU && getenv_ring()),
+                                      ring_epi_mode(a, p) == EM_DRELU),
                  "nstl_gemm: colsum_part needs the 256 kernel's dReLU epilogue (nstl_gemm_colsum_rows)");
   NSTL_CHECK_ARG(!a->relu_mask || nstl_gemm_relu_mask_words(a) > 0,
                  "nstl_gemm: relu_mask needs the 256 kernel's ReLU-dropout / dReLU epilogue (nstl_gemm_relu_mask_words)");
@@ -2156,12 +1424,10 @@ extern "C" int nstl_gemm(const nstl_gemm_args* a, void* stream) {
 extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream) {
   NSTL_CHECK_ARG(args != nullptr && n >= 1 && n <= NSTL_GEMM_GROUP_MAX, "nstl_gemm_grouped: 1..%d problems (got %d)",
                  NSTL_GEMM_GROUP_MAX, n);
-  GroupParams gp;
-  gp.n = n;
-  int tiles = 0;
   for (int g = 0; g < n; ++g) {
     const nstl_gemm_args* a = args + g;
-    if (int rc = make_params(a, gp.g[g])) return rc;
+    GemmParams p;
+    if (int rc = make_params(a, p)) return rc;
     NSTL_CHECK_ARG(a->dtype == NSTL_BF16 && a->K % 64 == 0 && a->M >= BIG && a->N >= BIG,
                    "nstl_gemm_grouped: problem %d is not a 256-kernel problem (bf16, M, N >= 256, K %% 64 == 0)", g);
     NSTL_CHECK_ARG(a->epilogue == NSTL_EPI_NONE && a->split_k <= 1 && !a->colsum_part && !a->relu_mask,
@@ -2169,32 +1435,24 @@ extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream
     NSTL_CHECK_ARG(a->a_kmajor == args[0].a_kmajor && a->b_kmajor == args[0].b_kmajor &&
                        a->c_dtype == args[0].c_dtype && (a->beta != 0.f) == (args[0].beta != 0.f),
                    "nstl_gemm_grouped: problem %d differs in layout, output type or beta use", g);
-    tiles += ((a->M + BIG - 1) / BIG) * ((a->N + BIG - 1) / BIG);
-    gp.tile_end[g] = tiles;
+    const int em = ring_epi_mode(a, p);
+    NSTL_CHECK_ARG(em == EM_F32 || em == EM_BF16, "nstl_gemm_grouped: f32 output, or bf16 without beta");
+    NSTL_CHECK_ARG(!a->sq_part || em == EM_F32, "nstl_gemm_grouped: sq_part needs f32 output");
   }
-  const int em = ring_epi_mode(args, gp.g[0]);
-  NSTL_CHECK_ARG(em == EM_F32 || em == EM_BF16, "nstl_gemm_grouped: f32 output, or bf16 without beta");
-  for (int g = 0; g < n; ++g)
-    NSTL_CHECK_ARG(!args[g].sq_part || em == EM_F32, "nstl_gemm_grouped: sq_part needs f32 output");
   hipStream_t st = (hipStream_t)stream;
-  {  // full tiles, beta 0: the 4-wave persistent kernel (gemm4.hip)
+  {  // full tiles, beta 0: one launch of the 4-wave persistent kernel (gemm4.hip)
     int handled = 0;
     if (int rc = nstl::gemm4_grouped(args, n, st, &handled)) return rc;
     if (handled) return 0;
   }
-  dim3 grid(tiles), block(BIG_NT);
-#define NSTL_GROUP_LAUNCH(AKv, BKv)                                                                        \
-  if (em == EM_F32) hipLaunchKernelGGL((gemm256r_group_kernel<AKv, BKv, EM_F32>), grid, block, 0, st, gp); \
-  else hipLaunchKernelGGL((gemm256r_group_kernel<AKv, BKv, EM_BF16>), grid, block, 0, st, gp);
-  const bool ak = args[0].a_kmajor, bk = args[0].b_kmajor;
-  if (ak && bk) { NSTL_GROUP_LAUNCH(true, true) }
-  else if (ak && !bk) { NSTL_GROUP_LAUNCH(true, false) }
-  else if (!ak && !bk) { NSTL_GROUP_LAUNCH(false, false) }
-  else { NSTL_GROUP_LAUNCH(false, true) }
-#undef NSTL_GROUP_LAUNCH
-  NSTL_LAUNCH_CHECK("nstl_gemm_grouped");
-  nstl::count(NSTL_K_GEMM_GROUP);
-  nstl::count(NSTL_K_GEMM_GROUP_TILES, tiles);
+  // anything else (partial tiles, beta != 0, K % 128 != 0, NSTL_GEMM4=0): one
+  // 8-wave ring launch per problem, in order, whatever its tile count (the ring
+  // epilogue writes sq_part, one slot per (tile, wave), as the grouped kernel did)
+  for (int g = 0; g < n; ++g) {
+    GemmParams p;
+    if (int rc = make_params(args + g, p)) return rc;
+    if (int rc = launch_big(args + g, p, 1, st)) return rc;
+  }
   return 0;
 }
 
@@ -2204,7 +1462,7 @@ extern "C" int nstl_gemm_colsum_rows(const nstl_gemm_args* a) {
   if (a->dtype == NSTL_FP8)  // the fp8 ring kernel's dReLU epilogue (same 128-row partial layout)
     return a->epilogue == NSTL_EPI_DRELU_DROP && a->split_k <= 1 && a->c_dtype == NSTL_BF16 &&
                    ring_epi_mode(a, p) == EM_DRELU ? (a->M + 127) / 128 : 0;
-  if (!big_ok(a) || a->epilogue != NSTL_EPI_DRELU_DROP || a->split_k > 1 || !getenv_ring()) return 0;
+  if (!big_ok(a) || a->epilogue != NSTL_EPI_DRELU_DROP || a->split_k > 1) return 0;
   if (ring_epi_mode(a, p) != EM_DRELU) return 0;
   return (a->M + 127) / 128;
 }
@@ -2217,7 +1475,7 @@ extern "C" int64_t nstl_gemm_relu_mask_words(const nstl_gemm_args* a) {
     if (a->split_k > 1 || a->c_dtype != NSTL_BF16 || (em != EM_RELU_DROP && em != EM_DRELU)) return 0;
     return (int64_t)((a->M + 63) / 64) * 8 * ((a->N + 7) / 8);
   }
-  if (!big_ok(a) || a->split_k > 1 || !getenv_ring() || a->dtype != NSTL_BF16 || a->c_dtype != NSTL_BF16) return 0;
+  if (!big_ok(a) || a->split_k > 1 || a->dtype != NSTL_BF16 || a->c_dtype != NSTL_BF16) return 0;
   const int em = ring_epi_mode(a, p);
   if (em != EM_RELU_DROP && em != EM_DRELU) return 0;
   return (int64_t)((a->M + 63) / 64) * 8 * ((a->N + 7) / 8);

@@ -326,9 +326,18 @@ NSTL_DEV int64_t mask_word(int N, int row, int col) {
 }
 
 // RoPE tables in LDS (EM_ROPE): row t holds rope_dim / 2 (cos, sin) pairs,
-// 16-byte chunk k (pairs 2k, 2k + 1) at k ^ (t & 15): the 16 lanes of a read
-// (16 consecutive positions, one chunk) hit 16 distinct bank slots
-NSTL_DEV int rope_off(int t, int chunk, int row_bytes) { return t * row_bytes + ((chunk ^ (t & 15)) << 4); }
+// 16-byte chunk k (pairs 2k, 2k + 1) at k ^ (t & m): the 16 lanes of a read
+// (16 consecutive positions, one chunk) hit 16 distinct bank slots when the row
+// has 16 or more chunks.  m (rope_swz) keeps the XOR inside the row: the low bit
+// of the chunk count, at most 16, minus one (rope_dim 64: 15; 32: 7; 96: 7; a
+// chunk count with bit 0 set: 0, no swizzle).  With m = 15 and fewer than 16
+// chunks, rows wrote into their neighbours' slots.
+NSTL_DEV int rope_swz(int rope_dim) {
+  const int chunks = rope_dim >> 2;
+  const int low = chunks & -chunks;
+  return (low < 16 ? low : 16) - 1;
+}
+NSTL_DEV int rope_off(int t, int chunk, int row_bytes, int swz) { return t * row_bytes + ((chunk ^ (t & swz)) << 4); }
 
 // An accumulator tile read out of the AGPRs at the point of use ...  Left to the
 // compiler, the epilogue's VALU uses split the accumulators' live range at the
@@ -557,6 +566,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
 #pragma unroll
       for (int e = 0; e < 4; ++e) csum[b][e] = 0.f;
     const int rope_rb = p.rope_dim * 4;  // bytes per table row in LDS
+    const int rswz = rope_swz(p.rope_dim);
     // RoPE: the lane's table chunk per column block (col % rope_dim) / 4, once
     // per tile (a power-of-two rope_dim, the production case: a mask)
     int rchunk[8];
@@ -580,7 +590,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       f32x4 rcs[8];
       if constexpr (EM == EM_ROPE) {
 #pragma unroll
-        for (int b = 0; b < 8; ++b) rcs[b] = *(const f32x4*)(rope_lds + rope_off(t, rchunk[b], rope_rb));
+        for (int b = 0; b < 8; ++b) rcs[b] = *(const f32x4*)(rope_lds + rope_off(t, rchunk[b], rope_rb, rswz));
       }
 #pragma unroll
       for (int bp = 0; bp < 8; bp += 2) {
@@ -717,12 +727,12 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   if constexpr (EM == EM_ROPE) {
     // the whole cos/sin table, once per workgroup (one problem per launch)
     const Params& p0 = gp.g[0];
-    const int half = p0.rope_dim >> 1, chunks = p0.rope_dim >> 2;
+    const int half = p0.rope_dim >> 1, chunks = p0.rope_dim >> 2, swz = rope_swz(p0.rope_dim);
     for (int i = tid; i < p0.rope_T * chunks; i += NT) {
       const int tt = i / chunks, k = i - tt * chunks;
       const float2 cs = *(const float2*)(p0.rope_cos + tt * half + 2 * k);
       const float2 sn = *(const float2*)(p0.rope_sin + tt * half + 2 * k);
-      *(f32x4*)(smem + SMEM + rope_off(tt, k, p0.rope_dim * 4)) = (f32x4){cs.x, sn.x, cs.y, sn.y};
+      *(f32x4*)(smem + SMEM + rope_off(tt, k, p0.rope_dim * 4, swz)) = (f32x4){cs.x, sn.x, cs.y, sn.y};
     }
     __syncthreads();
   }

@@ -40,11 +40,24 @@ struct SkSpace {
   unsigned* cnt = nullptr;
   int G = 0;
 };
+// At most SK_SPACES of them (2 G x 256 KB each, 128 MB at G = 256): a new
+// stream past that synchronizes the devices and frees the others (stream-K is
+// opt-in; streams that launch it are few and long-lived).
+constexpr size_t SK_SPACES = 4;
 bool sk_space(hipStream_t st, int G, g4::StreamK& sk) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, SkSpace> spaces;
   const int dev = nstl::stream_device(st);  // the stream's device, not the current one
   std::lock_guard<std::mutex> lk(mu);
+  if (spaces.find({dev, st}) == spaces.end() && spaces.size() >= SK_SPACES) {
+    for (auto& kv : spaces) {
+      nstl::DeviceGuard on(kv.first.first);
+      if (hipDeviceSynchronize() != hipSuccess) return false;
+      if (kv.second.slab) (void)hipFree(kv.second.slab);
+      if (kv.second.cnt) (void)hipFree(kv.second.cnt);
+    }
+    spaces.clear();
+  }
   SkSpace& s = spaces[{dev, st}];
   if (s.G < G) {
     nstl::DeviceGuard on(dev);

@@ -5,6 +5,8 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <mutex>
+#include <map>
 
 #include "../../include/nstl.h"
 
@@ -51,7 +53,7 @@ int stream_device(hipStream_t st) {
   return dev;
 }
 
-int stream_cus(hipStream_t st) {
+static int stream_cus_query(hipStream_t st) {
   static int cus[64] = {0};
   const int dev = stream_device(st);
   if (dev < 0 || dev >= 64) return 0;
@@ -70,8 +72,39 @@ int stream_cus(hipStream_t st) {
   } else {
     (void)hipGetLastError();  // no mask (or not queryable): every CU
   }
-  const char* e = getenv("NSTL_PERSIST_CUS");
-  if (e && atoi(e) > 0 && atoi(e) < g) g = atoi(e);
+  static const int cap = [] {
+    const char* e = getenv("NSTL_PERSIST_CUS");
+    return e ? atoi(e) : 0;
+  }();
+  if (cap > 0 && cap < g) g = cap;
+  return g;
+}
+
+// A stream's CU mask is fixed when it is created, so the grid is cached per
+// stream handle (the query is a runtime call per GEMM launch otherwise).  A
+// handle reused by a new stream with another mask would keep the old grid: a
+// speed matter only, every persistent kernel runs any grid size correctly.
+// (The null stream is per device: keyed by the current device.)
+int stream_cus(hipStream_t st) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, int> cache;
+  int dev = -1;
+  if (st == nullptr && hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return stream_cus_query(st);
+  }
+  const std::pair<int, hipStream_t> key(dev, st);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  const int g = stream_cus_query(st);
+  if (g > 0) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache.size() >= 1024) cache.clear();
+    cache[key] = g;
+  }
   return g;
 }
 }  // namespace nstl

@@ -939,10 +939,8 @@ class Seq2SeqEngine:
             K.reduce_rows3(part, bb.n_part, self.D, outs, bf, stream=self.st)
 
     def _attn(self, q, k, v, o, lse, seed, T, B, mask=None):
-        a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
-                        v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed,
-                        dh=self.dh)
-        a.mask_bits = K.ptr(mask)
+        a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, 0, 0, 0, 0, 0, 0, 0, 0, 0, self.p, seed, dh=self.dh)
+        K.attn_set(a, q=q, k=k, v=v, o=o, lse=lse, mask_bits=mask)
         K.attn_fwd(a, stream=self.st)
 
     def _attn_bwd(self, q, k, v, o, lse, do, dq, dk, dv, seed, T, B, mask=None, bias=(), bf=0.0):
@@ -950,16 +948,11 @@ class Seq2SeqEngine:
         view) -- the projection bias gradients, reduced from the kernel's fused
         column sums.  Returns False when the call took the generic kernels (no
         sums: the caller's colsum provides them)."""
-        a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0),
-                        v.data_ptr(), v.stride(0), o.data_ptr(), o.stride(0), lse.data_ptr(), self.p, seed,
-                        dh=self.dh)
-        a.dout, a.dout_ld = do.data_ptr(), do.stride(0)
-        a.dq, a.dq_ld, a.dk, a.dk_ld, a.dv, a.dv_ld = (dq.data_ptr(), dq.stride(0), dk.data_ptr(), dk.stride(0),
-                                                        dv.data_ptr(), dv.stride(0))
+        a = K.attn_args(K.dtype_code(self.dt), B, T, self.H, 0, 0, 0, 0, 0, 0, 0, 0, 0, self.p, seed, dh=self.dh)
         cs, sn = self.rope(T, self.dh)
-        a.rope_cos, a.rope_sin, a.rope_q, a.rope_k = cs.data_ptr(), sn.data_ptr(), 1, 1
-        a.dsum = self.cur.dsum.data_ptr()
-        a.mask_bits = K.ptr(mask)
+        a.rope_q, a.rope_k = 1, 1
+        K.attn_set(a, q=q, k=k, v=v, o=o, lse=lse, dout=do, dq=dq, dk=dk, dv=dv, rope_cos=cs, rope_sin=sn,
+                   dsum=self.cur.dsum, mask_bits=mask)
         part = self.cur.abias
         if self._red is not None:
             part = self.cur.abias_slots[self._ab_slot]
@@ -967,7 +960,7 @@ class Seq2SeqEngine:
         rows = K.attn_bias_rows(a) if bias and self.fused_bias_on else 0
         fused = 0 < rows <= part.shape[0]
         if fused:
-            a.dbias_part = part.data_ptr()
+            K.attn_set(a, dbias_part=part)
         self._guard(dq, dk, dv)
         K.attn_bwd(a, stream=self.st)
         for off, n, out in (bias if fused else ()):
@@ -1160,6 +1153,8 @@ class Seq2SeqEngine:
         g = grad_pred.reshape(M, self.out_dim)
         K.copy2d(g, g.stride(0), bb.dpred, 64, M, self.out_dim, 64, scale=self.grad_scale_t, stream=self.st)
         red = self.grad_reducer
+        if red is not None:
+            red.begin(self.grads_fresh)
         ready = (lambda name: self._ready(red, self.end_of[name])) if red is not None else (lambda name: None)
         dpred = bb.dpred[:, :self.out_dim]
         self._dw(dpred, bb.xf, "decoder.fc_output.weight", 1, bf, ws)

@@ -122,11 +122,38 @@ class GradAllReducer:
         self.bucket = max(1, bucket_bytes // grads.element_size())
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.active = dist.is_initialized() and self.world >= min_world
+        # a finish() completed and no optimizer step has consumed it yet: the arena
+        # holds reduced gradients (the step must not reduce them again)
+        self.completed = False
         self.reset()
 
     def reset(self):
         self.sent = 0
         self.works = []
+
+    def begin(self, fresh):
+        """Start of a backward.  Drops what an aborted backward left (its buckets
+        are waited for, its progress reset).  ``fresh`` False (the backward adds to
+        the arena: gradient accumulation) after a completed in-backward reduction
+        would count the other ranks' earlier micro-batches twice, so it raises."""
+        if not self.active:
+            return
+        for w in self.works:
+            w.wait()
+        self.reset()
+        if not fresh and self.completed:
+            raise RuntimeError("gradient accumulation over several backwards per step is not supported by the "
+                               "in-backward reduction (NSTL_DP=%s): the first backward's gradients are already "
+                               "reduced; use NSTL_DP=zero1" % self.mode)
+        self.completed = False
+
+    def consume(self):
+        """Whether the arena holds this step's reduced gradients (a finish()
+        completed since the last call); resets the flag."""
+        done, self.completed = self.completed, False
+        return done
+
+    mode = "allreduce"
 
     def ready(self, upto):
         """Arena prefix [0, upto) is final: launch buckets of the unsent part."""
@@ -148,6 +175,7 @@ class GradAllReducer:
         for w in self.works:
             w.wait()
         self.reset()
+        self.completed = True
 
 
 class GradShardReducer(GradAllReducer):
@@ -156,6 +184,8 @@ class GradShardReducer(GradAllReducer):
     shard boundaries; [comm.numel, end) -- the replicated tail -- is left to
     zero1_step.  After finish(), rank r's arena [comm.lo, comm.hi) holds the
     summed gradients (what the reduce-scatter would have written)."""
+
+    mode = "zero1_overlap"
 
     def __init__(self, grads, comm, bucket_bytes=DEFAULT_BUCKET_BYTES, min_world=2):
         self.comm = comm
@@ -187,6 +217,7 @@ class GradShardReducer(GradAllReducer):
         for w in self.works:
             w.wait()
         self.reset()
+        self.completed = True
 
 
 class ShardComm:

@@ -161,8 +161,8 @@ class MultiHeadAttention(nn.Module):
             K.rope(t, D, t, D, B * Tq, D, cs, sn, Tq, dh)
         o = torch.empty_like(q)
         lse = torch.empty(B * H * Tq, dtype=torch.float32, device=query.device)
-        K.attn_fwd(K.attn_args(K.F32, B, Tq, H, q.data_ptr(), D, k.data_ptr(), D, v.data_ptr(), D, o.data_ptr(), D,
-                               lse.data_ptr(), 0.0, 0, dh=dh))
+        a = K.attn_args(K.F32, B, Tq, H, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0.0, 0, dh=dh)
+        K.attn_fwd(K.attn_set(a, q=q, k=k, v=v, o=o, lse=lse))
         return _linear_f32(o, self.out_linear).view(B, Tq, D), None
 
 

@@ -177,6 +177,14 @@ class FusedAdam(torch.optim.Optimizer):
             return loss
         if self._comm is None:
             eng.sync_pending()
+            red = eng.grad_reducer
+            if red is not None and red.active and not red.consume():
+                # replicated (NSTL_DP=allreduce) and no in-backward all-reduce
+                # finished for these gradients (written by hand, or a backward that
+                # raised): reduce them here
+                import torch.distributed as dist
+                eng.invalidate_sq()
+                dist.all_reduce(eng.g32, op=dist.ReduceOp.SUM, group=red.group)
             sq = eng.take_sq_partials() if max_norm is not None and self.trust_backward_norm else None
             eng.invalidate_sq()
             if sq is not None:
@@ -199,7 +207,11 @@ class FusedAdam(torch.optim.Optimizer):
         from .. import parallel
         if max_norm is None:
             self.partial.zero_()
-        reduced = isinstance(eng.grad_reducer, parallel.GradShardReducer) and eng.grad_reducer.active
+        # the shard was summed in place during backward only if that backward's
+        # reducer finished (not for gradients written by hand, or a backward that
+        # raised): otherwise the step reduce-scatters as plain zero1 does
+        red = eng.grad_reducer
+        reduced = isinstance(red, parallel.GradShardReducer) and red.active and red.consume()
         parallel.zero1_step(self._comm, eng.g32, self._gs, self.partial, sumsq_fn, adam_fn,
                             [eng.p16] if eng.p16 is not eng.p32 else [eng.p32], tail=(eng.n_shardable, eng.numel),
                             reduced=reduced)

@@ -180,3 +180,48 @@ def test_overlapped_shard_reduce_is_bit_identical_gloo(tmp_path, world):
                 assert torch.equal(a[k], b[k]), (r, k)
             else:
                 torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-7)
+
+
+def _reducer_state_worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from neurosync_trainer_lite_amd import parallel
+    parallel.init_from_env(backend="gloo")
+    ns = 64 * 840
+    comm = parallel.ShardComm(ns)
+    for cls in (parallel.GradAllReducer, parallel.GradShardReducer):
+        g = torch.ones(ns) * (rank + 1)
+        red = cls(g, bucket_bytes=4000) if cls is parallel.GradAllReducer else cls(g, comm, bucket_bytes=4000)
+        # a completed in-backward reduction is consumed once
+        red.begin(True)
+        red.ready(ns)
+        red.finish()
+        assert red.consume() and not red.consume()
+        # a backward that raised half-way: the next backward starts from bucket 0
+        red.begin(True)
+        red.ready(ns // 2)
+        assert red.sent > 0 and red.works
+        red.begin(True)
+        assert red.sent == 0 and not red.works and not red.completed
+        # accumulation onto a reduced arena (a second backward before the step) is refused
+        red.ready(ns)
+        red.finish()
+        with pytest.raises(RuntimeError, match="accumulation"):
+            red.begin(False)
+        # after the step consumed it, accumulation starts a new reduction normally
+        red.begin(True)
+        red.finish()
+        assert red.consume()
+        red.begin(False)
+    dist.destroy_process_group()
+
+
+def test_reducer_consume_and_abort_bookkeeping_gloo(tmp_path):
+    """the in-backward reducers (NSTL_DP=allreduce / zero1_overlap) mark
+    a reduction as done only when finish() completed, the step consumes that
+    once (otherwise it reduces itself), a backward that raised leaves no stale
+    progress behind, and accumulating a second backward onto already reduced
+    gradients raises instead of counting the other ranks' first micro-batch
+    twice."""
+    mp.spawn(_reducer_state_worker, args=(_port(), str(tmp_path)), nprocs=WORLD, join=True)

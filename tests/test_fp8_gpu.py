@@ -95,7 +95,11 @@ def test_fp8_gemm_f32(M, N, K_):
     close(c, fp8_ref.gemm(qa.cpu(), sa.cpu(), qb.cpu(), sb.cpu()), 1e-4, "fp8 gemm %dx%dx%d" % (M, N, K_))
 
 
-def test_fp8_gemm_bias_relu_rope():
+@pytest.mark.parametrize("T", [128, 256])
+def test_fp8_gemm_bias_relu_rope(T):
+    """Bias, ReLU and RoPE epilogues of the fp8 GEMM against float64 of the same
+    quantized operands; T = 256 is C5's long-clip position table (its RoPE GEMMs
+    run on the fp8 kernel with the 256-position tables)."""
     M, N, K_ = 512, 1024, 1024
     qa, sa, qb, sb = fp8_operands(M, N, K_, 7)
     ref = fp8_ref.gemm(qa.cpu(), sa.cpu(), qb.cpu(), sb.cpu())
@@ -108,12 +112,15 @@ def test_fp8_gemm_bias_relu_rope():
     K.gemm(qa, qb, c, M, N, K_, a_scale=sa, b_scale=sb, epilogue=K.EPI_BIAS_RELU_DROP, bias=bias, p_drop=0.0)
     torch.cuda.synchronize()
     close(c, ref_b.clamp_min(0), 1e-2, "bias+relu")
-    # RoPE over the first 512 columns (dh 64), T = 128 positions
-    T, dh = 128, 64
+    # RoPE over the first 512 columns (dh 64), T positions
+    dh = 64
+    K.kernel_counts_reset()
     cos_t, sin_t = rotation_tables(T, dh, DEV)
     K.gemm(qa, qb, c, M, N, K_, a_scale=sa, b_scale=sb, epilogue=K.EPI_BIAS_ROPE, bias=bias,
            rope=(cos_t, sin_t, T, dh), rope_cols=512)
     torch.cuda.synchronize()
+    c_ = K.kernel_counts()
+    assert c_["gemm_fp8"] == 1 and c_["gemm_fp8_rope"] == 1, c_
     r = ref_b.clone()
     t = torch.arange(M) % T
     cs, sn = cos_t.double().cpu()[t], sin_t.double().cpu()[t]          # [M, dh/2]

@@ -129,17 +129,21 @@ def test_gemm4_drelu_mask_colsum_matches_ring(monkeypatch, M, N, Kd):
     assert rel_err(d4, ref) < 1e-2
 
 
-@pytest.mark.parametrize("T,rope_cols", [(128, 2048), (64, 1024)])
-def test_gemm4_rope_matches_ring(monkeypatch, T, rope_cols):
+@pytest.mark.parametrize("T,rope_cols,dim", [(128, 2048, 64), (64, 1024, 64), (256, 1024, 32), (128, 960, 96),
+                                               (128, 1024, 16)])
+def test_gemm4_rope_matches_ring(monkeypatch, T, rope_cols, dim):
     """q|k|v + RoPE (the tables staged in LDS) against the ring kernel (which reads
-    them from global memory) and float64."""
+    them from global memory) and float64.  Head dims below 64 and not a power of
+    two (rows of fewer than 16 or of 24 table chunks) check that the LDS table's
+    swizzle stays inside each row (with chunk ^ (t & 15) a 32-wide row
+    wrote into the next row's slots)."""
     M, N, Kd = 4096, 3072, 256
     X, W, b = rnd(M, Kd, dtype=bf, seed=31), rnd(N, Kd, dtype=bf, scale=0.05, seed=32), rnd(N, seed=33)
-    cs, sn = rotation_tables(T, 64, DEV)
+    cs, sn = rotation_tables(T, dim, DEV)
 
     def run():
         C = torch.empty(M, N, dtype=bf, device=DEV)
-        K.gemm(X, W, C, M, N, Kd, epilogue=K.EPI_BIAS_ROPE, bias=b, rope=(cs, sn, T, 64), rope_cols=rope_cols)
+        K.gemm(X, W, C, M, N, Kd, epilogue=K.EPI_BIAS_ROPE, bias=b, rope=(cs, sn, T, dim), rope_cols=rope_cols)
         return C
 
     c4, cr, cnt = both(monkeypatch, run)
@@ -155,8 +159,8 @@ def test_gemm4_rope_matches_ring(monkeypatch, T, rope_cols):
     c64, s64 = f64(cs), f64(sn)
     t = torch.arange(M) % T
     zr = z.clone()
-    for h0 in range(0, rope_cols, 64):
-        e, o = z[:, h0:h0 + 64:2], z[:, h0 + 1:h0 + 64:2]
+    for h0 in range(0, rope_cols, dim):
+        e, o = z[:, h0:h0 + dim:2], z[:, h0 + 1:h0 + dim:2]
         zr[:, h0:h0 + 64:2] = e * c64[t] - o * s64[t]
         zr[:, h0 + 1:h0 + 64:2] = e * s64[t] + o * c64[t]
     assert rel_err(c4, zr) < 1e-2

@@ -1009,208 +1009,6 @@ def test_reduce_rows_batch():
         K.reduce_rows_batch(jobs * 5)
 
 
-# ---------------------------------------------------------------------------
-# Persistent XCD-phased ring GEMM (multi-round problems: tiles = rounds x CUs).
-# Its tiles run the one-shot kernel's arithmetic; a split tile's two K pieces
-# are added once in f32 (second + first) instead of one accumulation chain, so
-# a problem of two rounds equals its two one-round halves (rows 0..M/2, M/2..M,
-# computed by the one-shot grid) up to the f32 rounding of that add: bf16
-# outputs differ only where it crosses a bf16 rounding boundary (measured: 5e-5
-# of the elements, one or two bf16 steps; NSTL_GEMM_DEBUG=nocut is bit-exact).
-def _same(got, ref, what, f32=False):
-    g, r = got.float(), ref.float()
-    d = (g - r).abs()
-    if f32:
-        assert (d <= 1e-6 * r.abs().max() + 0.0).all(), "%s: max diff %.3e" % (what, d.max().item())
-        return
-    # two bf16 ulps, plus an f32-rounding floor for results that cancel to ~0
-    ulp = torch.maximum(r.abs(), g.abs()) * 2.0 ** -6 + 1e-5 * r.abs().max()
-    assert (d <= ulp).all(), "%s: diff beyond two bf16 ulps (max %.3e)" % (what, d.max().item())
-    frac = (d > 0).double().mean().item()
-    assert frac < 1e-3, "%s: %.2e of the elements differ" % (what, frac)
-
-
-def _cus():
-    return torch.cuda.get_device_properties(0).multi_processor_count
-
-
-# the persistent kernels are opt-in (NSTL_GEMM_PERSIST=1: the 256^2 XCD-phased
-# grid; NSTL_GEMM_H=2: the two-per-CU 128 x 256 grid; read once per process):
-# tools/run_persist.sh and tools/run_gemm_h.sh run these tests with them on
-persistent = pytest.mark.skipif(os.environ.get("NSTL_GEMM_PERSIST") != "1" and os.environ.get("NSTL_GEMM_H") != "2"
-                                and os.environ.get("NSTL_GEMM_PQ") != "1",
-                                reason="persistent GEMM off (NSTL_GEMM_PERSIST=1 / NSTL_GEMM_H=2 / NSTL_GEMM_PQ=1 enable it)")
-
-
-def _halves(run, M):
-    """run(i0, rows) computes output rows [i0, i0+rows) of the same problem."""
-    full = run(0, M)
-    lo = run(0, M // 2)
-    hi = run(M // 2, M // 2)
-    return full, lo, hi
-
-
-def _persist_rows():
-    """M (multiple of 256) such that N=2048 gives two rounds of 256-tiles on this device."""
-    tiles_n = 2048 // 256
-    return 2 * _cus() // tiles_n * 256
-
-
-@persistent
-@pytest.mark.parametrize("epi", ["bias", "rope", "relu0", "relu_mask"])
-def test_gemm256_persistent_forward_matches_one_shot(epi):
-    dt, N, Kd, T = torch.bfloat16, 2048, 1024, 128
-    M = _persist_rows()
-    assert (M // 256) * (N // 256) == 2 * _cus()
-    X, W, b = rnd(M, Kd, dtype=dt, seed=400), rnd(N, Kd, dtype=dt, scale=0.05, seed=401), rnd(N, seed=402)
-    cs, sn = rotation_tables(T, 64, DEV)
-    kw = dict(bias=b)
-    if epi == "bias":
-        kw.update(epilogue=K.EPI_BIAS)
-    elif epi == "rope":
-        kw.update(epilogue=K.EPI_BIAS_ROPE, rope=(cs, sn, T, 64), rope_cols=N // 2)
-    else:
-        kw.update(epilogue=K.EPI_BIAS_RELU_DROP, p_drop=0.0)
-    masks = {}
-
-    def run(i0, rows):
-        C = torch.empty(rows, N, dtype=dt, device=DEV)
-        extra = {}
-        if epi == "relu_mask":
-            words = K.gemm_relu_mask_words(X[i0:], W, C, rows, N, Kd, **kw)
-            assert words > 0
-            masks[(i0, rows)] = torch.zeros(words, dtype=torch.int64, device=DEV)
-            extra["relu_mask"] = masks[(i0, rows)]
-        K.gemm(X[i0:i0 + rows], W, C, rows, N, Kd, **kw, **extra)
-        return C
-
-    full, lo, hi = _halves(run, M)
-    torch.cuda.synchronize()
-    _same(full[:M // 2], lo, "fwd lo")
-    _same(full[M // 2:], hi, "fwd hi")
-    if epi == "relu_mask":
-        mf = masks[(0, M)]
-        half = mf.numel() // 2
-        for got, ref in ((mf[:half], masks[(0, M // 2)]), (mf[half:], masks[(M // 2, M // 2)])):
-            flips = torch.bitwise_xor(got, ref)
-            nbits = sum(bin(int(x) & (2 ** 64 - 1)).count("1") for x in flips[flips != 0].tolist())
-            assert nbits <= 1e-5 * 64 * got.numel(), "relu mask: %d bits differ" % nbits
-    y = f64(X) @ f64(W).T + f64(b)
-    if epi == "bias":
-        check(full, y, 1e-2, "persistent fwd")
-
-
-@persistent
-@pytest.mark.parametrize("layout", ["fwd", "dx"])
-def test_gemm256_persistent_four_rounds(layout):
-    """Four rounds of 256-tiles per workgroup (the FFN shapes' depth): every
-    quarter of the persistent result equals the one-shot kernel's result for
-    those rows (one round each), and the whole matches the f64 product to bf16."""
-    dt, N, Kd = torch.bfloat16, 2048, 1024
-    M = 2 * _persist_rows()
-    b = rnd(N, seed=412)
-    if layout == "fwd":
-        X, W = rnd(M, Kd, dtype=dt, seed=410), rnd(N, Kd, dtype=dt, scale=0.05, seed=411)
-        kw = dict(epilogue=K.EPI_BIAS, bias=b)
-        ref = f64(X) @ f64(W).T + f64(b)
-    else:
-        X, W = rnd(M, Kd, dtype=dt, seed=413), rnd(Kd, N, dtype=dt, scale=0.05, seed=414)
-        kw = dict(a_kmajor=True, b_kmajor=False)
-        ref = f64(X) @ f64(W)
-
-    def run(i0, rows):
-        C = torch.empty(rows, N, dtype=dt, device=DEV)
-        K.gemm(X[i0:i0 + rows], W, C, rows, N, Kd, **kw)
-        return C
-
-    full = run(0, M)
-    q = M // 4
-    parts = [run(i * q, q) for i in range(4)]
-    torch.cuda.synchronize()
-    for i, part in enumerate(parts):
-        _same(full[i * q:(i + 1) * q], part, "quarter %d" % i)
-    err = (f64(full) - ref).abs().max().item()
-    assert err <= 1e-2 * ref.abs().max().item(), err
-
-
-@persistent
-def test_gemm256_persistent_dropout_rows():
-    """With dropout the keep bits depend on the global row: the first half of the
-    persistent result equals the one-shot first half; the kept fraction is 0.7."""
-    dt, N, Kd = torch.bfloat16, 2048, 1024
-    M = _persist_rows()
-    X, W, b = rnd(M, Kd, dtype=dt, seed=403), rnd(N, Kd, dtype=dt, scale=0.05, seed=404), rnd(N, seed=405)
-    kw = dict(epilogue=K.EPI_BIAS_RELU_DROP, bias=b, p_drop=0.3, seed=77)
-    full = torch.empty(M, N, dtype=dt, device=DEV)
-    lo = torch.empty(M // 2, N, dtype=dt, device=DEV)
-    K.gemm(X, W, full, M, N, Kd, **kw)
-    K.gemm(X[:M // 2], W, lo, M // 2, N, Kd, **kw)
-    torch.cuda.synchronize()
-    _same(full[:M // 2], lo, "dropout lo")
-    y = torch.relu(f64(X) @ f64(W).T + f64(b))
-    pos = y > 1e-2
-    kept = (f64(full)[pos] != 0).double().mean().item()
-    assert abs(kept - 0.7) < 0.01
-
-
-@persistent
-@pytest.mark.parametrize("mode", ["bf16", "drelu_colsum", "f32_beta"])
-def test_gemm256_persistent_dx_matches_one_shot(mode):
-    dt, N, Kd = torch.bfloat16, 2048, 1024  # dX [M][N] = dY [M][Kd] W [Kd][N]
-    M = _persist_rows()
-    dY, W = rnd(M, Kd, dtype=dt, seed=406), rnd(Kd, N, dtype=dt, seed=407)
-    h = torch.relu(rnd(M, N, dtype=dt, seed=408))
-    C0 = rnd(M, N, seed=409)
-    parts = {}
-
-    def run(i0, rows):
-        kw = dict(a_kmajor=True, b_kmajor=False)
-        if mode == "f32_beta":
-            C = C0[i0:i0 + rows].clone()
-            kw.update(beta=1.0)
-        else:
-            C = torch.empty(rows, N, dtype=dt, device=DEV)
-        if mode == "drelu_colsum":
-            kw.update(epilogue=K.EPI_DRELU_DROP, aux=h[i0:], ld_aux=N, p_drop=0.3)
-            nr = K.gemm_colsum_rows(dY[i0:], W, C, rows, N, Kd, **kw)
-            assert nr == rows // 128
-            parts[i0, rows] = torch.empty(nr, N, dtype=torch.float32, device=DEV)
-            kw.update(colsum_part=parts[i0, rows])
-        K.gemm(dY[i0:i0 + rows], W, C, rows, N, Kd, **kw)
-        return C
-
-    full, lo, hi = _halves(run, M)
-    torch.cuda.synchronize()
-    _same(full[:M // 2], lo, "dX lo", f32=mode == "f32_beta")
-    _same(full[M // 2:], hi, "dX hi", f32=mode == "f32_beta")
-    if mode == "drelu_colsum":
-        # the partial column sums are sums of what the epilogue stored (128 rows each)
-        ref = full.float().view(M // 128, 128, N).sum(1)
-        torch.testing.assert_close(parts[0, M], ref, rtol=1e-4, atol=1e-2)
-    if mode == "f32_beta":
-        check(full, f64(C0) + f64(dY) @ f64(W), 1e-5, "persistent dX f32")
-
-
-@persistent
-def test_gemm256_persistent_dw_matches_one_shot():
-    """Weight-gradient layout (both operands MN-major, f32 out) over two rounds."""
-    dt, Mt = torch.bfloat16, 2048
-    N = 2048
-    Kd = 2 * _cus() // (N // 256) * 256  # output columns: two rounds of tiles
-    dY, X = rnd(Mt, N, dtype=dt, seed=410), rnd(Mt, Kd, dtype=dt, seed=411)
-
-    def run(i0, rows):  # output rows i0.. = columns i0.. of dY
-        C = torch.empty(rows, Kd, dtype=torch.float32, device=DEV)
-        K.gemm(dY[:, i0:], X, C, rows, Kd, Mt, a_kmajor=False, b_kmajor=False, lda=N)
-        return C
-
-    full, lo, hi = _halves(run, N)
-    torch.cuda.synchronize()
-    _same(full[:N // 2], lo, "dW lo", f32=True)
-    _same(full[N // 2:], hi, "dW hi", f32=True)
-    check(full, f64(dY).T @ f64(X), 1e-5, "persistent dW")
-
-
 def test_transpose_bf16_batched_bit_exact():
     """nstl_transpose_bf16: several jobs of different shapes in one launch, padded
     leading dimensions on both sides, every element moved exactly."""

@@ -209,13 +209,12 @@ def masked_stream(excluded):
     return torch.cuda.ExternalStream(st.value, device=DEV), n
 
 
-def test_masked_stream_grid_and_gemm():
+def test_masked_stream_grid_and_gemm(monkeypatch):
     """Mask bit i is a CU of XCD i % 8, shader engine (i / 8) % 4: a stream ceding
     one CU of every (XCD, SE) pair (bits 0..31) runs 32 fewer persistent
     workgroups, and so does one ceding a single CU (bit 0: that SE's share
     sets the grid); the GEMM on it takes the stream-K tail."""
-    import os
-    os.environ["NSTL_GEMM4_SK"] = "1"
+    monkeypatch.setenv("NSTL_GEMM4_SK", "1")  # read per call; undone even when an assertion fails
     s1, n = masked_stream(set(range(32)))
     s2, _ = masked_stream({0})
     assert K.stream_cus(torch.cuda.current_stream().cuda_stream) == n
@@ -230,6 +229,5 @@ def test_masked_stream_grid_and_gemm():
         K.gemm(X, W, C, M, N, Kd)
     s1.synchronize()
     c = K.kernel_counts()
-    del os.environ["NSTL_GEMM4_SK"]
     assert c["gemm4"] == 1 and c["gemm4_sk"] == 1, c
     assert rel_err(C, f64(X) @ f64(W).T) < 1e-5
