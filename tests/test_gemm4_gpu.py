@@ -161,8 +161,8 @@ def test_gemm4_rope_matches_ring(monkeypatch, T, rope_cols, dim):
     zr = z.clone()
     for h0 in range(0, rope_cols, dim):
         e, o = z[:, h0:h0 + dim:2], z[:, h0 + 1:h0 + dim:2]
-        zr[:, h0:h0 + 64:2] = e * c64[t] - o * s64[t]
-        zr[:, h0 + 1:h0 + 64:2] = e * s64[t] + o * c64[t]
+        zr[:, h0:h0 + dim:2] = e * c64[t] - o * s64[t]
+        zr[:, h0 + 1:h0 + dim:2] = e * s64[t] + o * c64[t]
     assert rel_err(c4, zr) < 1e-2
 
 
