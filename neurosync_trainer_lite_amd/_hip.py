@@ -312,10 +312,10 @@ def _need(t, last, what):
 
 
 def _need_mat(t, rows, cols, ld, what):
-    """A row-major [rows][cols] operand with row stride ld (elements)."""
+    """A row-major [rows][cols] operand with row stride ld (elements): its last
+    addressed element lies inside the storage.  (Stride rules -- ld >= cols, the
+    alignments -- are the library's own argument checks.)"""
     if rows > 0 and cols > 0:
-        if ld < cols:
-            raise ValueError("%s: row stride %d < %d columns" % (what, ld, cols))
         _need(t, (rows - 1) * ld + cols - 1, what)
 
 

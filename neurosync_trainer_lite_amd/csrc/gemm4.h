@@ -196,17 +196,17 @@ NSTL_DEV void rd_one(bf16x8& f, const RdAddr<KMAJ>& r) {
     else f = (bf16x8){f[0], f[1], f[2], f[3], b[0], b[1], b[2], b[3]};
   }
 }
-// read slot R of the half-step
-template <bool AK, bool BKM, int SO, int H, int R>
+// read slot R of the half-step (SOA / SOB: the A / B stage slot's byte offset)
+template <bool AK, bool BKM, int SOA, int SOB, int H, int R>
 NSTL_DEV void rd_slot(bf16x8 (&fa)[8], bf16x8 (&fb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb) {
   constexpr int NA = AK ? 8 : 16;
   if constexpr (R < NA) {
     constexpr int J = AK ? R : R / 2, SUB = AK ? 0 : R % 2;
-    rd_one<SO, AK, H, J, SUB>(fa[J], ra);
+    rd_one<SOA, AK, H, J, SUB>(fa[J], ra);
   } else {
     constexpr int Q = R - NA;
     constexpr int J = BKM ? Q : Q / 2, SUB = BKM ? 0 : Q % 2;
-    rd_one<SO, BKM, H, J, SUB>(fb[J], rb);
+    rd_one<SOB, BKM, H, J, SUB>(fb[J], rb);
   }
 }
 
@@ -242,7 +242,7 @@ NSTL_DEV void dma_tile(Dma& d, const Params& p, int m0, int n0, int ks) {
 template <bool AK, bool BKM, int R>
 NSTL_DEV void rd_all(bf16x8 (&fa)[8], bf16x8 (&fb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb) {
   if constexpr (R < n_reads<AK, BKM>()) {
-    rd_slot<AK, BKM, 0, 0, R>(fa, fb, ra, rb);
+    rd_slot<AK, BKM, 0, 0, 0, R>(fa, fb, ra, rb);
     rd_all<AK, BKM, R + 1>(fa, fb, ra, rb);
   }
 }
@@ -251,25 +251,28 @@ NSTL_DEV void rd_all(bf16x8 (&fa)[8], bf16x8 (&fb)[8], const RdAddr<AK>& ra, con
 // instructions: read slots, rd_slot) into (na, nb) spread over MFMAs 1 .. 46 (read
 // slot r after MFMA 1 + 46 r / R: each transpose read gets a gap of its own as far
 // as the count allows, and the last read has 17 MFMAs to land before the closing
-// lgkmcnt(0)); if DMA, the 16 pieces follow MFMAs 2, 6, ..., 62 (A pieces to adst,
-// B pieces to bdst, stage offsets sa / sb).  RSO: the read slot's byte offset.
+// lgkmcnt(0)).  DMAM: the stage DMA this half-step issues -- 0 none; 1 all 16
+// pieces of the stage after MFMAs 2, 6, ..., 62 (A pieces to adst, B pieces to
+// bdst, stage offsets sa / sb; the two-stage ring); 2 the 8 A pieces, 3 the 8 B
+// pieces, after MFMAs 2, 10, ..., 58 (the A3/B2 ring: one operand per half-step).
+// RSOA / RSOB: the read slots' byte offsets.
 // DBG (timing experiments only, wrong results): 1 no DMA, 2 no reads, 8 no MFMA.
 // (experiments, profiles/r4_gemm4_read_spread.txt: DBG & 256 spreads the reads over
 // MFMAs 1 .. 56, DBG & 512 over 1 .. 32, DBG & 1024 over 1 .. 24)
-template <bool AK, bool BKM, int RSO, int RH, int I, int R, int SPAN = 46>
+template <bool AK, bool BKM, int RSOA, int RSOB, int RH, int I, int R, int SPAN = 46>
 NSTL_DEV void rd_after(bf16x8 (&na)[8], bf16x8 (&nb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb) {
   constexpr int NR = n_reads<AK, BKM>();
   if constexpr (R < NR) {
     if constexpr (1 + (SPAN * R) / NR == I) {
-      rd_slot<AK, BKM, RSO, RH, R>(na, nb, ra, rb);
+      rd_slot<AK, BKM, RSOA, RSOB, RH, R>(na, nb, ra, rb);
       G4_SB();
-      rd_after<AK, BKM, RSO, RH, I, R + 1, SPAN>(na, nb, ra, rb);
+      rd_after<AK, BKM, RSOA, RSOB, RH, I, R + 1, SPAN>(na, nb, ra, rb);
     } else if constexpr (1 + (SPAN * R) / NR < I) {
-      rd_after<AK, BKM, RSO, RH, I, R + 1, SPAN>(na, nb, ra, rb);
+      rd_after<AK, BKM, RSOA, RSOB, RH, I, R + 1, SPAN>(na, nb, ra, rb);
     }
   }
 }
-template <bool AK, bool BKM, bool RD, int RSO, int RH, bool DMA, int DBG, int I = 0>
+template <bool AK, bool BKM, bool RD, int RSOA, int RSOB, int RH, int DMAM, int DBG, int I = 0>
 NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 (&cb)[8], bf16x8 (&na)[8],
                         bf16x8 (&nb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb, const Dma& d, char* adst,
                         char* bdst, uint32_t sa, uint32_t sb) {
@@ -277,7 +280,14 @@ NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 
     if constexpr (!(DBG & 8)) mma16(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
     G4_SB();
     if constexpr (RD && !(DBG & 2))
-      rd_after<AK, BKM, RSO, RH, I, 0, (DBG & 256) ? 56 : (DBG & 512) ? 32 : (DBG & 1024) ? 24 : 46>(na, nb, ra, rb);
+      rd_after<AK, BKM, RSOA, RSOB, RH, I, 0, (DBG & 256) ? 56 : (DBG & 512) ? 32 : (DBG & 1024) ? 24 : 46>(na, nb, ra,
+                                                                                                       rb);
+    if constexpr ((DMAM == 2 || DMAM == 3) && !(DBG & 1) && (I & 7) == ((DBG & 2048) ? 6 : 2)) {
+      constexpr int q = I >> 3;
+      if constexpr (DMAM == 2) dma16(d.ra, adst + q * 1024, d.va[q], d.ta + sa);
+      else dma16(d.rb, bdst + q * 1024, d.vb[q], d.tb + sb);
+      G4_SB();
+    }
     // the 16 DMA pieces: after MFMAs 2, 6, ..., 62, or (experiments) after MFMAs
     // 0 .. 15 (DBG & 16) / 0, 2, ..., 30 (DBG & 32): issued earlier in h = 1; after
     // MFMAs 32, 34, ..., 62 (DBG & 64) / 47 .. 62 (DBG & 128): later
@@ -286,7 +296,7 @@ NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 
                               : (DBG & 64)  ? (I >= 32 && (I & 1) == 0)
                               : (DBG & 128) ? (I >= 47 && I < 63)
                                             : (I & 3) == 2;
-    if constexpr (DMA && !(DBG & 1) && DMA_HERE) {
+    if constexpr (DMAM == 1 && !(DBG & 1) && DMA_HERE) {
       constexpr int q = (DBG & 16)    ? I
                         : (DBG & 32)  ? I >> 1
                         : (DBG & 64)  ? (I - 32) >> 1
@@ -296,7 +306,7 @@ NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 
       else dma16(d.rb, bdst + (q - 8) * 1024, d.vb[q - 8], d.tb + sb);
       G4_SB();
     }
-    half_step<AK, BKM, RD, RSO, RH, DMA, DBG, I + 1>(acc, ca, cb, na, nb, ra, rb, d, adst, bdst, sa, sb);
+    half_step<AK, BKM, RD, RSOA, RSOB, RH, DMAM, DBG, I + 1>(acc, ca, cb, na, nb, ra, rb, d, adst, bdst, sa, sb);
   }
 }
 
@@ -708,9 +718,25 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
 // aligned rows; operand extents < 2^31 bytes; EM_ROPE: T * rope_dim * 4 <=
 // ROPE_LDS and rope_dim % 4 == 0; EM_F32: beta 0.  Tiles of up to 16 problems
 // (gp.tile_end; one problem: n = 1).
-template <bool AK, bool BKM, int EM, bool GROUPED, int DBG = 0, bool SK = false>
+//
+// R3 (round 5): the stage DMA spread over both half-steps.  With two 64 KB
+// stages, stage s + 2 can only go into the slot stage s vacates, i.e. after the
+// mid-step barrier: all 16 pieces of a step sat in h = 1, beside that half's
+// fragment reads, while h = 0 issued none (the pieces' issue slots, not their
+// latency, cost the MFMA pipe: DESIGN.md section 4).  R3 gives A a ring of
+// three 32 KB slots and B a ring of two (160 KB, the whole LDS; not with the RoPE
+// table): in h = 0 of step s the 8 A pieces of stage s + 2 go into the A slot of
+// stage s - 1 (free since step s - 1's barrier), in h = 1 the 8 B pieces into
+// the B slot of stage s (free since this step's barrier).  The counted wait
+// before the barrier then leaves this step's 8 A pieces in flight.  A's slot
+// has period 3, so its read addresses carry the slot (one add per address and
+// step: 2 for a K-major A, 8 for an MN-major one); B's slot stays an immediate.
+template <bool AK, bool BKM, int EM, bool GROUPED, int DBG = 0, bool SK = false, bool R3 = false>
 __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + (EM == EM_ROPE ? ROPE_LDS : 0)];
+  static_assert(!(R3 && EM == EM_ROPE), "the A3/B2 ring fills the LDS: no room for the RoPE table");
+  constexpr int SMEM_ALL = R3 ? 5 * OPS : SMEM + (EM == EM_ROPE ? ROPE_LDS : 0);
+  constexpr int B_BASE = R3 ? 3 * OPS : 2 * OPS;  // B's slot 0
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_ALL];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -722,7 +748,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   if (!wk.next(sg)) return;
   const uint32_t smem_u32 = lds_addr(smem);
   char* const adst0 = smem + wave * 8 * 1024;
-  char* const bdst0 = smem + 2 * OPS + wave * 8 * 1024;
+  char* const bdst0 = smem + B_BASE + wave * 8 * 1024;
   const char* rope_lds = smem + SMEM;
   if constexpr (EM == EM_ROPE) {
     // the whole cos/sin table, once per workgroup (one problem per launch)
@@ -764,7 +790,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   RdAddr<AK> ra;
   RdAddr<BKM> rb;
   rd_addr<AK>(ra, smem_u32, wm * 128, lane);
-  rd_addr<BKM>(rb, smem_u32 + 2 * OPS, wn * 128, lane);
+  rd_addr<BKM>(rb, smem_u32 + B_BASE, wn * 128, lane);
 
   f32x4 acc[8][8];
 #pragma unroll
@@ -774,6 +800,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   bf16x8 f0a[8], f0b[8], f1a[8], f1b[8];
   // prologue of the first tile: stages 0 and 1 landed (both: step 0's counted
   // wait assumes an epilogue's stores behind stage 1), stage 0's k 0..31 read
+  // (R3: A stage s in A slot s % 3, B stage s in B slot s % 2 -- slots 0, 1 here)
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
 #pragma unroll
@@ -787,25 +814,60 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   rd_all<AK, BKM, 0>(f0a, f0b, ra, rb);
   G4_LGKM0();
 
+  // R3: the A slot of the stage this step computes (runtime: period 3); the A
+  // read addresses carry it (ra holds slot 0 + the current slot)
+  int sa_cur = 0;
+  auto move_a = [&](int from, int to) {  // A read addresses: slot `from` -> `to`
+    const uint32_t delta = (uint32_t)((to - from) * OPS);
+    if constexpr (AK) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) ra.k[h] += delta;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ra.t[j] += delta;
+    }
+  };
+
   // step on stage slot S: h = 0 on F0, the counted wait + barrier, h = 1 on F1
   // with the reads of the following stage (slot 1 - S) into F0 and the DMA of
   // stage `dma_stage` of the tile `dd` describes into slot S.  WAITN: how many VMEM
   // operations may stay in flight (issued after this wave's pieces of the stage to
   // retire).  The slot is a template constant: every LDS read takes it as an
   // immediate offset (no address arithmetic in the loop).
+  // R3: S is B's slot (period 2); A's slots come from sa_cur (see move_a), and
+  // h = 0 issues stage dma_stage's A pieces into A slot (sa_cur + 2) % 3.
   auto step = [&](auto slot_c, auto waitn_c, uint32_t dma_stage, const Dma& dd) {
     constexpr int S = decltype(slot_c)::value;
     constexpr int WAITN = decltype(waitn_c)::value;
-    half_step<AK, BKM, true, S * OPS, 1, false, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, dd, adst0, bdst0, 0, 0);
-    G4_LGKM0();
-    if constexpr (WAITN == 0) G4_VMCNT(0);
-    else if constexpr (WAITN == 32) G4_VMCNT(32);
-    else G4_VMCNT(63);
-    __builtin_amdgcn_s_barrier();
-    G4_SB();
-    half_step<AK, BKM, true, (1 - S) * OPS, 0, true, DBG>(acc, f1a, f1b, f0a, f0b, ra, rb, dd, adst0 + S * OPS,
-                                                         bdst0 + S * OPS, dma_stage * dd.a_kb, dma_stage * dd.b_kb);
-    G4_LGKM0();
+    if constexpr (R3) {
+      const int sa_dma = sa_cur == 0 ? 2 : sa_cur - 1;  // (sa_cur + 2) % 3
+      const int sa_next = sa_cur == 2 ? 0 : sa_cur + 1;
+      half_step<AK, BKM, true, 0, S * OPS, 1, 2, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, dd, adst0 + sa_dma * OPS,
+                                                    bdst0, dma_stage * dd.a_kb, 0);
+      G4_LGKM0();
+      if constexpr (WAITN == 0) G4_VMCNT(8);
+      else if constexpr (WAITN == 32) G4_VMCNT(40);
+      else G4_VMCNT(63);
+      __builtin_amdgcn_s_barrier();
+      G4_SB();
+      move_a(sa_cur, sa_next);
+      half_step<AK, BKM, true, 0, (1 - S) * OPS, 0, 3, DBG>(acc, f1a, f1b, f0a, f0b, ra, rb, dd, adst0,
+                                                          bdst0 + S * OPS, 0, dma_stage * dd.b_kb);
+      G4_LGKM0();
+      sa_cur = sa_next;
+    } else {
+      half_step<AK, BKM, true, S * OPS, S * OPS, 1, 0, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, dd, adst0, bdst0, 0, 0);
+      G4_LGKM0();
+      if constexpr (WAITN == 0) G4_VMCNT(0);
+      else if constexpr (WAITN == 32) G4_VMCNT(32);
+      else G4_VMCNT(63);
+      __builtin_amdgcn_s_barrier();
+      G4_SB();
+      half_step<AK, BKM, true, (1 - S) * OPS, (1 - S) * OPS, 0, 1, DBG>(acc, f1a, f1b, f0a, f0b, ra, rb, dd,
+                                                                      adst0 + S * OPS, bdst0 + S * OPS,
+                                                                      dma_stage * dd.a_kb, dma_stage * dd.b_kb);
+      G4_LGKM0();
+    }
   };
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;

@@ -127,6 +127,83 @@ int dma_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
   return 0;
 }
 
+// G4_R3_AB=1: the A3/B2 ring (R3: the stage DMA spread over both half-steps)
+// against the two-stage ring, alternated after a warm-up block; outputs compared
+// bit for bit (same accumulation order)
+template <bool AK, bool BKM, int EM, bool R3>
+void launch_r3(const g4::GroupParams& gp, hipStream_t st) {
+  const int grid = std::min(256, gp.tile_end[0]);
+  hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, EM, false, 0, false, R3>), dim3(grid), dim3(g4::NT), 0, st, gp);
+}
+int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
+  struct Case { const char* name; int M, N, K; int kind; };  // kind 0 TT, 1 TN, 2 NN f32 (dW)
+  const Case cs[] = {{"fwd out  16384x1024x1024", 16384, 1024, 1024, 0},
+                     {"fwd ffn1 16384x4096x1024", 16384, 4096, 1024, 0},
+                     {"fwd ffn2 16384x1024x4096", 16384, 1024, 4096, 0},
+                     {"dX  ffn2 16384x4096x1024", 16384, 4096, 1024, 1},
+                     {"dX  ffn1 16384x1024x4096", 16384, 1024, 4096, 1},
+                     {"dW  4096^2 K=16384     ", 4096, 4096, 16384, 2},
+                     {"dW  1024x4096 K=16384  ", 1024, 4096, 16384, 2}};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  typedef void (*F)(const g4::GroupParams&, hipStream_t);
+  const F fs[3][2] = {{launch_r3<true, true, g4::EM_BF16, false>, launch_r3<true, true, g4::EM_BF16, true>},
+                      {launch_r3<true, false, g4::EM_BF16, false>, launch_r3<true, false, g4::EM_BF16, true>},
+                      {launch_r3<false, false, g4::EM_F32, false>, launch_r3<false, false, g4::EM_F32, true>}};
+  const int64_t cmax = 16384LL * 4096;
+  bf16* C2;
+  float* Cf2;
+  CK(hipMalloc(&C2, cmax * 2));
+  CK(hipMalloc(&Cf2, 4096LL * 4096 * 4));
+  for (int round = 0; round < 4; ++round)
+    for (const Case& c : cs) {
+      g4::GroupParams gp{};
+      g4::Params& p = gp.g[0];
+      p.M = c.M; p.N = c.N; p.K = c.K; p.alpha = 1.f;
+      if (c.kind == 2) {  // dW = A^T B, A [K][M], B [K][N] (MN-major)
+        p.A = (const char*)A; p.lda = c.M; p.B = (const char*)B; p.ldb = c.N; p.C = (char*)Cf; p.ldc = c.N;
+        p.a_bytes = (uint32_t)((int64_t)c.K * c.M * 2); p.b_bytes = (uint32_t)((int64_t)c.K * c.N * 2);
+      } else {
+        p.A = (const char*)A; p.lda = c.K; p.B = (const char*)B; p.ldb = c.kind == 0 ? c.K : c.N; p.C = (char*)C; p.ldc = c.N;
+        p.a_bytes = (uint32_t)((int64_t)c.M * c.K * 2); p.b_bytes = (uint32_t)((int64_t)c.N * c.K * 2);
+      }
+      p.tiles_m = c.M / 256; p.tiles_n = c.N / 256;
+      gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
+      if (round == 0) {  // bitwise check: R3 against the two-stage kernel
+        fs[c.kind][0](gp, st);
+        CK(hipStreamSynchronize(st));
+        g4::GroupParams g2 = gp;
+        g2.g[0].C = c.kind == 2 ? (char*)Cf2 : (char*)C2;
+        fs[c.kind][1](g2, st);
+        CK(hipStreamSynchronize(st));
+        const size_t bytes = (size_t)c.M * c.N * (c.kind == 2 ? 4 : 2);
+        std::vector<unsigned char> h1(bytes), h2(bytes);
+        CK(hipMemcpy(h1.data(), gp.g[0].C, bytes, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h2.data(), g2.g[0].C, bytes, hipMemcpyDeviceToHost));
+        size_t diff = 0;
+        for (size_t i = 0; i < bytes; ++i) diff += h1[i] != h2[i];
+        printf("check %s  R3 vs two-stage: %zu differing bytes of %zu %s\n", c.name, diff, bytes, diff ? "BAD" : "ok");
+        fflush(stdout);
+        continue;
+      }
+      for (int arm = 0; arm < 2; ++arm) {
+        const F f = fs[c.kind][arm];
+        for (int w = 0; w < 3; ++w) f(gp, st);
+        std::vector<float> ts;
+        for (int r = 0; r < 15; ++r) {
+          CK(hipEventRecord(e0, st)); f(gp, st); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+          float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        const double us = ts[7] * 1e3, fl = 2.0 * c.M * c.N * c.K;
+        printf("round %d  %s  %-9s %8.1f us  %7.1f TF/s\n", round, c.name, arm ? "R3" : "two-stage", us, fl / us * 1e-6);
+        fflush(stdout);
+      }
+    }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   struct Shape { const char* name; int M, N, K, bkm; };
   const Shape shapes[] = {
@@ -151,6 +228,11 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&R, maxC * 4));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, st, A, maxA, 1u);
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, st, B, maxA, 2u);
+  if (getenv("G4_R3_AB")) {
+    float* Cf;
+    CK(hipMalloc(&Cf, 4096LL * 4096 * 4));
+    return r3_ab(A, B, C, Cf, st);
+  }
   if (getenv("G4_DMA_AB")) {
     float* Cf;
     CK(hipMalloc(&Cf, 4096LL * 4096 * 4));
