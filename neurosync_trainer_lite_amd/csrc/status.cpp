@@ -72,12 +72,14 @@ static int stream_cus_query(hipStream_t st) {
   } else {
     (void)hipGetLastError();  // no mask (or not queryable): every CU
   }
-  static const int cap = [] {
-    const char* e = getenv("NSTL_PERSIST_CUS");
-    return e ? atoi(e) : 0;
-  }();
-  if (cap > 0 && cap < g) g = cap;
   return g;
+}
+
+// NSTL_PERSIST_CUS caps the grid (tests of the stream-K tail; read per call)
+static int persist_cap(int g) {
+  const char* e = getenv("NSTL_PERSIST_CUS");
+  const int cap = e ? atoi(e) : 0;
+  return cap > 0 && cap < g ? cap : g;
 }
 
 // A stream's CU mask is fixed when it is created, so the grid is cached per
@@ -91,13 +93,13 @@ int stream_cus(hipStream_t st) {
   int dev = -1;
   if (st == nullptr && hipGetDevice(&dev) != hipSuccess) {
     (void)hipGetLastError();
-    return stream_cus_query(st);
+    return persist_cap(stream_cus_query(st));
   }
   const std::pair<int, hipStream_t> key(dev, st);
   {
     std::lock_guard<std::mutex> lk(mu);
     auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
+    if (it != cache.end()) return persist_cap(it->second);
   }
   const int g = stream_cus_query(st);
   if (g > 0) {
@@ -105,7 +107,7 @@ int stream_cus(hipStream_t st) {
     if (cache.size() >= 1024) cache.clear();
     cache[key] = g;
   }
-  return g;
+  return persist_cap(g);
 }
 }  // namespace nstl
 
