@@ -731,11 +731,13 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
 // before the barrier then leaves this step's 8 A pieces in flight.  A's slot
 // has period 3, so its read addresses carry the slot (one add per address and
 // step: 2 for a K-major A, 8 for an MN-major one); B's slot stays an immediate.
-template <bool AK, bool BKM, int EM, bool GROUPED, int DBG = 0, bool SK = false, bool R3 = false>
+template <bool AK, bool BKM, int EM, bool GROUPED, int DBG = 0, bool SK = false, int R3 = 0>
 __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
-  static_assert(!(R3 && EM == EM_ROPE), "the A3/B2 ring fills the LDS: no room for the RoPE table");
+  // R3 1: A has the ring of three (DMA'd in h = 0), B the ring of two; 2: the reverse
+  constexpr bool A3 = R3 == 1, B3 = R3 == 2;
+  static_assert(!(R3 && EM == EM_ROPE), "the 3 + 2 ring fills the LDS: no room for the RoPE table");
   constexpr int SMEM_ALL = R3 ? 5 * OPS : SMEM + (EM == EM_ROPE ? ROPE_LDS : 0);
-  constexpr int B_BASE = R3 ? 3 * OPS : 2 * OPS;  // B's slot 0
+  constexpr int B_BASE = A3 ? 3 * OPS : 2 * OPS;  // B's slot 0
   __shared__ __attribute__((aligned(16))) char smem[SMEM_ALL];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -814,17 +816,27 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   rd_all<AK, BKM, 0>(f0a, f0b, ra, rb);
   G4_LGKM0();
 
-  // R3: the A slot of the stage this step computes (runtime: period 3); the A
-  // read addresses carry it (ra holds slot 0 + the current slot)
-  int sa_cur = 0;
-  auto move_a = [&](int from, int to) {  // A read addresses: slot `from` -> `to`
+  // R3: the three-ring operand's slot of the stage this step computes (runtime:
+  // period 3); that operand's read addresses carry it (slot 0 + the current slot)
+  int s3_cur = 0;
+  auto move3 = [&](int from, int to) {  // read addresses: slot `from` -> `to`
     const uint32_t delta = (uint32_t)((to - from) * OPS);
-    if constexpr (AK) {
+    if constexpr (A3) {
+      if constexpr (AK) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) ra.k[h] += delta;
-    } else {
+        for (int h = 0; h < 2; ++h) ra.k[h] += delta;
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ra.t[j] += delta;
+        for (int j = 0; j < 8; ++j) ra.t[j] += delta;
+      }
+    } else if constexpr (B3) {
+      if constexpr (BKM) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) rb.k[h] += delta;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rb.t[j] += delta;
+      }
     }
   };
 
@@ -840,21 +852,24 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     constexpr int S = decltype(slot_c)::value;
     constexpr int WAITN = decltype(waitn_c)::value;
     if constexpr (R3) {
-      const int sa_dma = sa_cur == 0 ? 2 : sa_cur - 1;  // (sa_cur + 2) % 3
-      const int sa_next = sa_cur == 2 ? 0 : sa_cur + 1;
-      half_step<AK, BKM, true, 0, S * OPS, 1, 2, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, dd, adst0 + sa_dma * OPS,
-                                                    bdst0, dma_stage * dd.a_kb, 0);
+      const int s3_dma = s3_cur == 0 ? 2 : s3_cur - 1;  // (s3_cur + 2) % 3
+      const int s3_next = s3_cur == 2 ? 0 : s3_cur + 1;
+      const uint32_t oa = dma_stage * dd.a_kb, ob = dma_stage * dd.b_kb;
+      // h = 0: the three-ring operand's 8 pieces of stage dma_stage
+      half_step<AK, BKM, true, A3 ? 0 : S * OPS, B3 ? 0 : S * OPS, 1, A3 ? 2 : 3, DBG>(
+          acc, f0a, f0b, f1a, f1b, ra, rb, dd, adst0 + s3_dma * OPS, bdst0 + s3_dma * OPS, oa, ob);
       G4_LGKM0();
       if constexpr (WAITN == 0) G4_VMCNT(8);
       else if constexpr (WAITN == 32) G4_VMCNT(40);
       else G4_VMCNT(63);
       __builtin_amdgcn_s_barrier();
       G4_SB();
-      move_a(sa_cur, sa_next);
-      half_step<AK, BKM, true, 0, (1 - S) * OPS, 0, 3, DBG>(acc, f1a, f1b, f0a, f0b, ra, rb, dd, adst0,
-                                                          bdst0 + S * OPS, 0, dma_stage * dd.b_kb);
+      move3(s3_cur, s3_next);
+      // h = 1: the two-ring operand's 8 pieces into the slot stage s vacated
+      half_step<AK, BKM, true, A3 ? 0 : (1 - S) * OPS, B3 ? 0 : (1 - S) * OPS, 0, A3 ? 3 : 2, DBG>(
+          acc, f1a, f1b, f0a, f0b, ra, rb, dd, adst0 + S * OPS, bdst0 + S * OPS, oa, ob);
       G4_LGKM0();
-      sa_cur = sa_next;
+      s3_cur = s3_next;
     } else {
       half_step<AK, BKM, true, S * OPS, S * OPS, 1, 0, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, dd, adst0, bdst0, 0, 0);
       G4_LGKM0();

@@ -130,7 +130,7 @@ int dma_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
 // G4_R3_AB=1: the A3/B2 ring (R3: the stage DMA spread over both half-steps)
 // against the two-stage ring, alternated after a warm-up block; outputs compared
 // bit for bit (same accumulation order)
-template <bool AK, bool BKM, int EM, bool R3>
+template <bool AK, bool BKM, int EM, int R3>
 void launch_r3(const g4::GroupParams& gp, hipStream_t st) {
   const int grid = std::min(256, gp.tile_end[0]);
   hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, EM, false, 0, false, R3>), dim3(grid), dim3(g4::NT), 0, st, gp);
@@ -148,9 +148,9 @@ int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   typedef void (*F)(const g4::GroupParams&, hipStream_t);
-  const F fs[3][2] = {{launch_r3<true, true, g4::EM_BF16, false>, launch_r3<true, true, g4::EM_BF16, true>},
-                      {launch_r3<true, false, g4::EM_BF16, false>, launch_r3<true, false, g4::EM_BF16, true>},
-                      {launch_r3<false, false, g4::EM_F32, false>, launch_r3<false, false, g4::EM_F32, true>}};
+  const F fs[3][3] = {{launch_r3<true, true, g4::EM_BF16, 0>, launch_r3<true, true, g4::EM_BF16, 1>, launch_r3<true, true, g4::EM_BF16, 2>},
+                      {launch_r3<true, false, g4::EM_BF16, 0>, launch_r3<true, false, g4::EM_BF16, 1>, launch_r3<true, false, g4::EM_BF16, 2>},
+                      {launch_r3<false, false, g4::EM_F32, 0>, launch_r3<false, false, g4::EM_F32, 1>, launch_r3<false, false, g4::EM_F32, 2>}};
   const int64_t cmax = 16384LL * 4096;
   bf16* C2;
   float* Cf2;
@@ -170,24 +170,28 @@ int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
       }
       p.tiles_m = c.M / 256; p.tiles_n = c.N / 256;
       gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
-      if (round == 0) {  // bitwise check: R3 against the two-stage kernel
+      if (round == 0) {  // bitwise check: R3 (both assignments) against the two-stage kernel
         fs[c.kind][0](gp, st);
         CK(hipStreamSynchronize(st));
-        g4::GroupParams g2 = gp;
-        g2.g[0].C = c.kind == 2 ? (char*)Cf2 : (char*)C2;
-        fs[c.kind][1](g2, st);
-        CK(hipStreamSynchronize(st));
-        const size_t bytes = (size_t)c.M * c.N * (c.kind == 2 ? 4 : 2);
-        std::vector<unsigned char> h1(bytes), h2(bytes);
-        CK(hipMemcpy(h1.data(), gp.g[0].C, bytes, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(h2.data(), g2.g[0].C, bytes, hipMemcpyDeviceToHost));
-        size_t diff = 0;
-        for (size_t i = 0; i < bytes; ++i) diff += h1[i] != h2[i];
-        printf("check %s  R3 vs two-stage: %zu differing bytes of %zu %s\n", c.name, diff, bytes, diff ? "BAD" : "ok");
+        for (int v = 1; v <= 2; ++v) {
+          g4::GroupParams g2 = gp;
+          g2.g[0].C = c.kind == 2 ? (char*)Cf2 : (char*)C2;
+          CK(hipMemset(g2.g[0].C, 0xFF, (size_t)c.M * c.N * (c.kind == 2 ? 4 : 2)));
+          fs[c.kind][v](g2, st);
+          CK(hipStreamSynchronize(st));
+          const size_t bytes = (size_t)c.M * c.N * (c.kind == 2 ? 4 : 2);
+          std::vector<unsigned char> h1(bytes), h2(bytes);
+          CK(hipMemcpy(h1.data(), gp.g[0].C, bytes, hipMemcpyDeviceToHost));
+          CK(hipMemcpy(h2.data(), g2.g[0].C, bytes, hipMemcpyDeviceToHost));
+          size_t diff = 0;
+          for (size_t i = 0; i < bytes; ++i) diff += h1[i] != h2[i];
+          printf("check %s  R3=%d vs two-stage: %zu differing bytes of %zu %s\n", c.name, v, diff, bytes,
+                 diff ? "BAD" : "ok");
+        }
         fflush(stdout);
         continue;
       }
-      for (int arm = 0; arm < 2; ++arm) {
+      for (int arm = 0; arm < 3; ++arm) {
         const F f = fs[c.kind][arm];
         for (int w = 0; w < 3; ++w) f(gp, st);
         std::vector<float> ts;
@@ -197,7 +201,8 @@ int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
         }
         std::sort(ts.begin(), ts.end());
         const double us = ts[7] * 1e3, fl = 2.0 * c.M * c.N * c.K;
-        printf("round %d  %s  %-9s %8.1f us  %7.1f TF/s\n", round, c.name, arm ? "R3" : "two-stage", us, fl / us * 1e-6);
+        printf("round %d  %s  %-9s %8.1f us  %7.1f TF/s\n", round, c.name, arm == 0 ? "two-stage" : arm == 1 ? "A3/B2" : "B3/A2",
+               us, fl / us * 1e-6);
         fflush(stdout);
       }
     }
