@@ -851,7 +851,27 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   auto step = [&](auto slot_c, auto waitn_c, uint32_t dma_stage, const Dma& dd) {
     constexpr int S = decltype(slot_c)::value;
     constexpr int WAITN = decltype(waitn_c)::value;
-    if constexpr (R3) {
+    if constexpr (R3 && WAITN != 0 && !(DBG & 4096)) {
+      // a tile's first step: h = 0 issues no DMA (it runs right behind the
+      // epilogue's stores), h = 1 all 16 pieces -- the three-ring operand's into
+      // the slot of stage s - 1, free since the previous step's barrier
+      const int s3_dma = s3_cur == 0 ? 2 : s3_cur - 1;
+      const int s3_next = s3_cur == 2 ? 0 : s3_cur + 1;
+      const uint32_t oa = dma_stage * dd.a_kb, ob = dma_stage * dd.b_kb;
+      half_step<AK, BKM, true, A3 ? 0 : S * OPS, B3 ? 0 : S * OPS, 1, 0, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, dd,
+                                                                           adst0, bdst0, 0, 0);
+      G4_LGKM0();
+      if constexpr (WAITN == 32) G4_VMCNT(32);
+      else G4_VMCNT(63);
+      __builtin_amdgcn_s_barrier();
+      G4_SB();
+      move3(s3_cur, s3_next);
+      half_step<AK, BKM, true, A3 ? 0 : (1 - S) * OPS, B3 ? 0 : (1 - S) * OPS, 0, 1, DBG>(
+          acc, f1a, f1b, f0a, f0b, ra, rb, dd, adst0 + (A3 ? s3_dma : S) * OPS, bdst0 + (B3 ? s3_dma : S) * OPS, oa,
+          ob);
+      G4_LGKM0();
+      s3_cur = s3_next;
+    } else if constexpr (R3) {
       const int s3_dma = s3_cur == 0 ? 2 : s3_cur - 1;  // (s3_cur + 2) % 3
       const int s3_next = s3_cur == 2 ? 0 : s3_cur + 1;
       const uint32_t oa = dma_stage * dd.a_kb, ob = dma_stage * dd.b_kb;

@@ -110,7 +110,7 @@ int dma_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
       }
       p.tiles_m = c.M / 256; p.tiles_n = c.N / 256;
       gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
-      for (int arm = 0; arm < 3; ++arm) {
+      for (int arm = 0; arm < 4; ++arm) {
         const F f = fs[c.kind][arm];
         for (int w = 0; w < 3; ++w) f(gp, st);
         std::vector<float> ts;
@@ -130,10 +130,15 @@ int dma_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
 // G4_R3_AB=1: the A3/B2 ring (R3: the stage DMA spread over both half-steps)
 // against the two-stage ring, alternated after a warm-up block; outputs compared
 // bit for bit (same accumulation order)
+// R3 arms: 0 two-stage, 1 A3/B2, 2 B3/A2 (a tile's first step: all 16 pieces in h = 1),
+// 3 A3/B2 with the first step split like the others (DBG 4096)
 template <bool AK, bool BKM, int EM, int R3>
 void launch_r3(const g4::GroupParams& gp, hipStream_t st) {
   const int grid = std::min(256, gp.tile_end[0]);
-  hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, EM, false, 0, false, R3>), dim3(grid), dim3(g4::NT), 0, st, gp);
+  if constexpr (R3 == 3)
+    hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, EM, false, 4096, false, 1>), dim3(grid), dim3(g4::NT), 0, st, gp);
+  else
+    hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, EM, false, 0, false, R3>), dim3(grid), dim3(g4::NT), 0, st, gp);
 }
 int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
   struct Case { const char* name; int M, N, K; int kind; };  // kind 0 TT, 1 TN, 2 NN f32 (dW)
@@ -148,9 +153,9 @@ int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   typedef void (*F)(const g4::GroupParams&, hipStream_t);
-  const F fs[3][3] = {{launch_r3<true, true, g4::EM_BF16, 0>, launch_r3<true, true, g4::EM_BF16, 1>, launch_r3<true, true, g4::EM_BF16, 2>},
-                      {launch_r3<true, false, g4::EM_BF16, 0>, launch_r3<true, false, g4::EM_BF16, 1>, launch_r3<true, false, g4::EM_BF16, 2>},
-                      {launch_r3<false, false, g4::EM_F32, 0>, launch_r3<false, false, g4::EM_F32, 1>, launch_r3<false, false, g4::EM_F32, 2>}};
+  const F fs[3][4] = {{launch_r3<true, true, g4::EM_BF16, 0>, launch_r3<true, true, g4::EM_BF16, 1>, launch_r3<true, true, g4::EM_BF16, 2>, launch_r3<true, true, g4::EM_BF16, 3>},
+                      {launch_r3<true, false, g4::EM_BF16, 0>, launch_r3<true, false, g4::EM_BF16, 1>, launch_r3<true, false, g4::EM_BF16, 2>, launch_r3<true, false, g4::EM_BF16, 3>},
+                      {launch_r3<false, false, g4::EM_F32, 0>, launch_r3<false, false, g4::EM_F32, 1>, launch_r3<false, false, g4::EM_F32, 2>, launch_r3<false, false, g4::EM_F32, 3>}};
   const int64_t cmax = 16384LL * 4096;
   bf16* C2;
   float* Cf2;
@@ -173,7 +178,7 @@ int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
       if (round == 0) {  // bitwise check: R3 (both assignments) against the two-stage kernel
         fs[c.kind][0](gp, st);
         CK(hipStreamSynchronize(st));
-        for (int v = 1; v <= 2; ++v) {
+        for (int v = 1; v <= 3; ++v) {
           g4::GroupParams g2 = gp;
           g2.g[0].C = c.kind == 2 ? (char*)Cf2 : (char*)C2;
           CK(hipMemset(g2.g[0].C, 0xFF, (size_t)c.M * c.N * (c.kind == 2 ? 4 : 2)));
@@ -191,7 +196,7 @@ int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
         fflush(stdout);
         continue;
       }
-      for (int arm = 0; arm < 3; ++arm) {
+      for (int arm = 0; arm < 4; ++arm) {
         const F f = fs[c.kind][arm];
         for (int w = 0; w < 3; ++w) f(gp, st);
         std::vector<float> ts;
@@ -201,7 +206,7 @@ int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
         }
         std::sort(ts.begin(), ts.end());
         const double us = ts[7] * 1e3, fl = 2.0 * c.M * c.N * c.K;
-        printf("round %d  %s  %-9s %8.1f us  %7.1f TF/s\n", round, c.name, arm == 0 ? "two-stage" : arm == 1 ? "A3/B2" : "B3/A2",
+        printf("round %d  %s  %-9s %8.1f us  %7.1f TF/s\n", round, c.name, arm == 0 ? "two-stage" : arm == 1 ? "A3/B2" : arm == 2 ? "B3/A2" : "A3 split1",
                us, fl / us * 1e-6);
         fflush(stdout);
       }
