@@ -165,37 +165,47 @@ void fill(g4::Params& q, const nstl_gemm_args* a) {
   q.tiles_n = a->N / g4::TILE;
 }
 
-template <bool AK, bool BKM, bool GROUPED, bool SK>
+// R3 (gemm4.h): the stage DMA spread over both half-steps with a 3 + 2 slot
+// ring.  Measured on isolated shapes (profiles/r5_r3_ab.txt, outputs bit-
+// identical): the weight gradients (K = 16,384) 3-6 % faster, K = 4096 shapes
+// ~1 %, the K = 1024 multi-round forward (FFN1) 4-9 % slower, the rest neutral:
+// taken for K >= 2048 (every weight gradient).  NSTL_GEMM4_R3=0: never (A/B).
+int r3_env() {
+  const char* e = getenv("NSTL_GEMM4_R3");
+  return e ? atoi(e) : 1;
+}
+
+template <bool AK, bool BKM, bool GROUPED, bool SK, int R3>
 void launch_em(int em, dim3 grid, hipStream_t st, const g4::GroupParams& gp) {
   const dim3 block(g4::NT);
   switch (em) {
-    case g4::EM_BF16: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_BF16, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
+    case g4::EM_BF16: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_BF16, GROUPED, 0, SK, R3>), grid, block, 0, st, gp); break;
     case g4::EM_RELU_DROP:
-      hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_RELU_DROP, GROUPED, 0, SK>), grid, block, 0, st, gp);
+      hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_RELU_DROP, GROUPED, 0, SK, R3>), grid, block, 0, st, gp);
       break;
-    case g4::EM_ROPE:  // the q|k|v forward (TT) only: g4_mode takes RoPE with a K-major B
-      if constexpr (BKM) hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_ROPE, GROUPED, 0, SK>), grid, block, 0, st, gp);
+    case g4::EM_ROPE:  // the q|k|v forward (TT) only: g4_mode takes RoPE with a K-major B; never R3
+      if constexpr (BKM && !R3) hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_ROPE, GROUPED, 0, SK>), grid, block, 0, st, gp);
       break;
-    case g4::EM_DRELU: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_DRELU, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
-    default: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_F32, GROUPED, 0, SK>), grid, block, 0, st, gp); break;
+    case g4::EM_DRELU: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_DRELU, GROUPED, 0, SK, R3>), grid, block, 0, st, gp); break;
+    default: hipLaunchKernelGGL((g4::gemm4_kernel<AK, BKM, g4::EM_F32, GROUPED, 0, SK, R3>), grid, block, 0, st, gp); break;
   }
 }
 
 // the instantiations the step uses: forward and dX (A K-major) with every
 // epilogue; the weight gradients (NN) with f32 output, grouped or not; each
-// with and without the stream-K tail
-template <bool SK>
+// with and without the stream-K tail (R3 only without it)
+template <bool SK, int R3>
 int launch_sk(int em, bool ak, bool bk, bool grouped, dim3 grid, hipStream_t st, const g4::GroupParams& gp) {
   if (ak && bk) {
     if (grouped) return 0;
-    launch_em<true, true, false, SK>(em, grid, st, gp);
+    launch_em<true, true, false, SK, R3>(em, grid, st, gp);
   } else if (ak && !bk) {
     if (grouped) return 0;
-    launch_em<true, false, false, SK>(em, grid, st, gp);
+    launch_em<true, false, false, SK, R3>(em, grid, st, gp);
   } else {
     if (em != g4::EM_F32) return 0;
-    if (grouped) hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, true, 0, SK>), grid, dim3(g4::NT), 0, st, gp);
-    else hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 0, SK>), grid, dim3(g4::NT), 0, st, gp);
+    if (grouped) hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, true, 0, SK, R3>), grid, dim3(g4::NT), 0, st, gp);
+    else hipLaunchKernelGGL((g4::gemm4_kernel<false, false, g4::EM_F32, false, 0, SK, R3>), grid, dim3(g4::NT), 0, st, gp);
   }
   return 1;
 }
@@ -204,8 +214,13 @@ int launch(int em, bool ak, bool bk, bool grouped, int G, hipStream_t st, g4::Gr
   const int tiles = gp.tile_end[gp.n - 1];
   const dim3 grid(tiles < G ? tiles : G);
   plan_sk(gp, G, st);
-  if (!gp.sk.slab) return launch_sk<false>(em, ak, bk, grouped, grid, st, gp);
-  if (!launch_sk<true>(em, ak, bk, grouped, grid, st, gp)) return 0;
+  if (!gp.sk.slab) {
+    int kmin = gp.g[0].K;
+    for (int i = 1; i < gp.n; ++i) kmin = gp.g[i].K < kmin ? gp.g[i].K : kmin;
+    if (em != g4::EM_ROPE && kmin >= 2048 && r3_env()) return launch_sk<false, 1>(em, ak, bk, grouped, grid, st, gp);
+    return launch_sk<false, 0>(em, ak, bk, grouped, grid, st, gp);
+  }
+  if (!launch_sk<true, 0>(em, ak, bk, grouped, grid, st, gp)) return 0;
   nstl::count(NSTL_K_GEMM4_SK);
   return 1;
 }

@@ -257,3 +257,60 @@ def test_gemm4_stress_many_rounds():
     ref = (X.double() @ W.double().T)
     err = (C.double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("layout,M,N,Kd", [("tt", 4096, 2048, 2048), ("tn", 8192, 1024, 4096), ("nn", 1024, 2048, 8192),
+                                           ("tt_drelu", 2048, 4096, 2048), ("tt_relu", 2048, 4096, 2048)])
+def test_gemm4_r3_ring_bit_identical(monkeypatch, layout, M, N, Kd):
+    """The 3 + 2 slot ring (R3, taken for K >= 2048: the stage DMA spread over both
+    half-steps) accumulates in the same order as the two-stage ring: outputs,
+    keep bits and column sums bit for bit (NSTL_GEMM4_R3=0 selects the two-stage
+    ring, read per call)."""
+    ak, bk = layout != "nn", layout in ("tt", "tt_relu")
+    if layout == "nn":
+        X, W = rnd(Kd, M, dtype=bf, seed=61), rnd(Kd, N, dtype=bf, scale=0.05, seed=62)
+    else:
+        X = rnd(M, Kd, dtype=bf, seed=61)
+        W = rnd(N, Kd, dtype=bf, scale=0.05, seed=62) if bk else rnd(Kd, N, dtype=bf, scale=0.05, seed=62)
+    b = rnd(N, seed=63)
+    kw = dict(a_kmajor=ak, b_kmajor=bk)
+    f32 = layout == "nn"
+    if layout == "tt":
+        kw.update(epilogue=K.EPI_BIAS, bias=b)
+    if layout == "tt_relu":
+        kw.update(epilogue=K.EPI_BIAS_RELU_DROP, bias=b, p_drop=0.3, seed=9)
+    mask = None
+    if layout == "tt_drelu":
+        # keep bits from a forward of the same output shape
+        X1, W1 = rnd(M, 256, dtype=bf, seed=64), rnd(N, 256, dtype=bf, seed=65)
+        fw = dict(epilogue=K.EPI_BIAS_RELU_DROP, bias=b, p_drop=0.3, seed=5)
+        h = torch.empty(M, N, dtype=bf, device=DEV)
+        mask = torch.zeros(K.gemm_relu_mask_words(X1, W1, h, M, N, 256, **fw), dtype=torch.int64, device=DEV)
+        K.gemm(X1, W1, h, M, N, 256, relu_mask=mask, **fw)
+        kw.update(a_kmajor=True, b_kmajor=False, epilogue=K.EPI_DRELU_DROP, aux=h, ld_aux=N, p_drop=0.3,
+                  relu_mask=mask)
+
+    def run(r3):
+        monkeypatch.setenv("NSTL_GEMM4_R3", r3)
+        C = torch.full((M, N), float("nan"), dtype=torch.float32 if f32 else bf, device=DEV)
+        extra = {}
+        if layout == "tt_relu":
+            extra["relu_mask"] = torch.full((K.gemm_relu_mask_words(X, W, C, M, N, Kd, **kw),), -1, dtype=torch.int64,
+                                            device=DEV)
+        if layout == "tt_drelu":
+            extra["colsum_part"] = torch.full((K.gemm_colsum_rows(X, W, C, M, N, Kd, **kw), N), float("nan"),
+                                              device=DEV)
+        K.kernel_counts_reset()
+        K.gemm(X, W, C, M, N, Kd, **kw, **extra)
+        torch.cuda.synchronize()
+        assert K.kernel_counts()["gemm4"] == 1
+        return C, extra
+
+    (c1, e1), (c0, e0) = run("1"), run("0")
+    monkeypatch.delenv("NSTL_GEMM4_R3")
+    assert torch.equal(c1, c0)
+    for k in e1:
+        assert torch.equal(e1[k], e0[k]), k
+    ref = (f64(X).T if layout == "nn" else f64(X)) @ (f64(W).T if bk else f64(W))
+    if layout == "nn":
+        assert rel_err(c1, ref) < 1e-5
