@@ -354,6 +354,31 @@ enum {
   NSTL_K_GEMM_FP8_ROPE,      /* fp8 GEMM launches with the RoPE epilogue (C5 q|k|v, cross q, cross k|v) */
   NSTL_K_COUNT
 };
+/* Copy-engine ZeRO-1 (parallel.ShardPusher; replaces the reference's gather of
+ * every gradient to cuda:0 and broadcast back, utils/training_utils.py:228-257).
+ * Each rank exports its receive buffer with nstl_ipc_handle; every other rank
+ * maps it with nstl_ipc_open and, during backward, pushes the slices of its
+ * gradient arena that the owner's shard holds with nstl_copy_engine: a device-
+ * to-device copy on the copy engines (no kernel, no CU taken from the step).
+ * After a collective orders every push before it, the owner forms its shard's
+ * gradient with nstl_shard_sum. */
+#define NSTL_IPC_HANDLE_BYTES 64
+/* handle_out: NSTL_IPC_HANDLE_BYTES naming the allocation that holds ptr;
+   offset_out: ptr's byte offset in it.  nstl_ipc_open returns that allocation's
+   base in the calling process (add the offset). */
+int nstl_ipc_handle(const void* ptr, void* handle_out, int64_t* offset_out);
+int nstl_ipc_open(const void* handle, void** ptr_out);
+int nstl_ipc_close(void* ptr);
+int nstl_copy_engine(void* dst, const void* src, int64_t bytes, void* stream);
+/* out[i] = own[i] + slots[0][i] + ... + slots[n_slots-1][i] (f32, slot order;
+ * slot k at slots + k * ld), and partial[b] = the sum of squares of block b of
+ * out exactly as nstl_sumsq(out, n, partial, n_partial) computes it -- the
+ * reduce-scatter and the clip norm's first stage (utils/training_utils.py:73)
+ * in one pass over the shard.  Starts with a system-scope acquire: the slots
+ * are written by other devices' copy engines. */
+int nstl_shard_sum(const float* own, const float* slots, int64_t ld, int n_slots, int64_t n, float* out,
+                   float* partial, int n_partial, void* stream);
+
 /* Workgroups a persistent one-per-CU grid launches on `stream` (the GEMM and
  * attention-forward grids): 32 x the fewest CUs the stream's CU mask leaves on
  * one (XCD, shader engine) pair (mask bit i = a CU of XCD i % 8, SE (i / 8) % 4).

@@ -119,7 +119,9 @@ EXPORTS = [
     "nstl_features", "nstl_stft_mel", "nstl_features_workspace_bytes", "nstl_features_frames", "nstl_last_error_string",
     "nstl_version", "nstl_fp8_quant_rows", "nstl_fp8_quant_cols", "nstl_kernel_counts", "nstl_kernel_counts_reset",
     "nstl_cmvn_delta_reduce", "nstl_reduce_frame_pairs", "nstl_transpose_bf16", "nstl_stream_cus", "nstl_mask_grid",
+    "nstl_ipc_handle", "nstl_ipc_open", "nstl_ipc_close", "nstl_copy_engine", "nstl_shard_sum",
 ]
+IPC_HANDLE_BYTES = 64
 
 # nstl_kernel_counts order (NSTL_K_* in include/nstl.h)
 KERNEL_COUNT_NAMES = ["gemm128", "gemm_ring", "gemm_ring_tiles", "gemm_group", "gemm_group_tiles",
@@ -186,6 +188,11 @@ def lib():
         L.nstl_stream_cus.restype = _i32
         L.nstl_mask_grid.argtypes = [_vp, _i32]
         L.nstl_mask_grid.restype = _i32
+        L.nstl_ipc_handle.argtypes = [_vp, _vp, ctypes.POINTER(_i64)]
+        L.nstl_ipc_open.argtypes = [_vp, ctypes.POINTER(_vp)]
+        L.nstl_ipc_close.argtypes = [_vp]
+        L.nstl_copy_engine.argtypes = [_vp, _vp, _i64, _vp]
+        L.nstl_shard_sum.argtypes = [_vp, _vp, _i64, _i32, _i64, _vp, _vp, _i32, _vp]
         _lib = L
     return _lib
 
@@ -551,6 +558,48 @@ def clip_coef(partial, n_partial, max_norm, coef, norm_out=None, stream=None):
     check(lib().nstl_clip_coef(partial.data_ptr(), n_partial, float(max_norm), coef.data_ptr(),
                                norm_out.data_ptr() if norm_out is not None else None,
                                stream if stream is not None else stream_of()), "nstl_clip_coef")
+
+
+def ipc_handle(t):
+    """The 64-byte IPC handle of the allocation holding device tensor t
+    (nstl_ipc_handle) and t's byte offset in it."""
+    h = ctypes.create_string_buffer(IPC_HANDLE_BYTES)
+    off = _i64()
+    check(lib().nstl_ipc_handle(t.data_ptr(), h, ctypes.byref(off)), "nstl_ipc_handle")
+    return h.raw, off.value
+
+
+def ipc_open(handle):
+    """Map another process's allocation (nstl_ipc_open); returns its base pointer."""
+    p = _vp()
+    check(lib().nstl_ipc_open(ctypes.create_string_buffer(handle, IPC_HANDLE_BYTES), ctypes.byref(p)), "nstl_ipc_open")
+    return p.value
+
+
+def ipc_close(ptr):
+    check(lib().nstl_ipc_close(ptr), "nstl_ipc_close")
+
+
+def copy_engine(dst_ptr, src, nbytes, stream=None):
+    """nbytes from device tensor src to the device address dst_ptr on the copy
+    engines (nstl_copy_engine: no kernel)."""
+    if not src.is_contiguous() or nbytes > src.numel() * src.element_size():
+        raise ValueError("copy_engine: %d bytes past the (contiguous) source tensor" % nbytes)
+    check(lib().nstl_copy_engine(dst_ptr, src.data_ptr(), nbytes, stream if stream is not None else stream_of()),
+          "nstl_copy_engine")
+
+
+def shard_sum(own, slots, n_slots, out, partial, n_partial, stream=None):
+    """out = own + slots[0] + ... (slot order) and the sum-of-squares partials of
+    out (nstl_shard_sum).  own / out f32 [n]; slots f32 [n_slots][ld >= n]."""
+    n = own.numel()
+    ld = slots.stride(0) if n_slots else n
+    if out.numel() < n or (n_slots and (slots.shape[0] < n_slots or slots.shape[1] < n)):
+        raise ValueError("shard_sum: operand sizes")
+    _check_side(partial, n_partial, "nstl_shard_sum partial")
+    check(lib().nstl_shard_sum(own.data_ptr(), slots.data_ptr() if n_slots else None, ld, n_slots, n, out.data_ptr(),
+                               partial.data_ptr(), n_partial, stream if stream is not None else stream_of()),
+          "nstl_shard_sum")
 
 
 def stft_mel(y, n_samples, sr, mel, n_frames, stream=None):

@@ -14,7 +14,51 @@
 namespace {
 constexpr int NT = 256;
 
-__global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, float* partial) {
+// Sum of squares of one slice per block (grid = the partial count).  SUM: the
+// slice is first formed as own + slots[0] + slots[1] + ... (in slot order, f32)
+// and written to `out` (nstl_shard_sum: the copy-engine ZeRO-1 reduction);
+// the squares are then accumulated exactly as for a plain read of `out`, so the
+// partials are bit-identical to nstl_sumsq of the summed shard.
+struct SumSrc {
+  const float* own;
+  const float* slots;  // [n_slots][ld]
+  int64_t ld;
+  int n_slots;
+  float* out;
+};
+
+template <bool SUM>
+NSTL_DEV float sum_one(const float* g, const SumSrc& s, int64_t i) {
+  if constexpr (!SUM) {
+    return g[i];
+  } else {
+    float x = s.own[i];
+    for (int k = 0; k < s.n_slots; ++k) x += s.slots[k * s.ld + i];
+    s.out[i] = x;
+    return x;
+  }
+}
+template <bool SUM>
+NSTL_DEV f32x4 sum_four(const float* g, const SumSrc& s, int64_t i4) {
+  if constexpr (!SUM) {
+    return ((const f32x4*)g)[i4];
+  } else {
+    f32x4 x = ((const f32x4*)s.own)[i4];
+    for (int k = 0; k < s.n_slots; ++k) x += ((const f32x4*)(s.slots + k * s.ld))[i4];
+    ((f32x4*)s.out)[i4] = x;
+    return x;
+  }
+}
+
+template <bool SUM>
+__global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, float* partial, SumSrc src) {
+  if constexpr (SUM) {
+    // the slots were written by other GPUs' copy engines (peer writes into this
+    // device's memory, ordered before this launch by a collective): a
+    // system-scope acquire drops any line of them this device's caches kept
+    // from an earlier step
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
   const int64_t per = (n + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * per, hi = min(n, lo + per);
   double acc = 0.0;
@@ -22,22 +66,28 @@ __global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, fl
   int64_t v0 = (lo + 3) & ~(int64_t)3, v1 = hi & ~(int64_t)3;
   if (v0 > hi) v0 = hi;
   if (v1 < v0) v1 = v0;
-  for (int64_t i = lo + threadIdx.x; i < v0; i += NT) acc += (double)g[i] * g[i];
+  for (int64_t i = lo + threadIdx.x; i < v0; i += NT) {
+    const float x = sum_one<SUM>(g, src, i);
+    acc += (double)x * x;
+  }
   // four 16-byte loads in flight per thread before their squares are summed
   int64_t i = v0 / 4 + threadIdx.x;
   for (; i + 3 * NT < v1 / 4; i += 4 * NT) {
     f32x4 x[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = ((const f32x4*)g)[i + u * NT];
+    for (int u = 0; u < 4; ++u) x[u] = sum_four<SUM>(g, src, i + u * NT);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       acc += (double)(x[u][0] * x[u][0] + x[u][1] * x[u][1]) + (double)(x[u][2] * x[u][2] + x[u][3] * x[u][3]);
   }
   for (; i < v1 / 4; i += NT) {
-    const f32x4 x = ((const f32x4*)g)[i];
+    const f32x4 x = sum_four<SUM>(g, src, i);
     acc += (double)(x[0] * x[0] + x[1] * x[1]) + (double)(x[2] * x[2] + x[3] * x[3]);
   }
-  for (int64_t i = v1 + threadIdx.x; i < hi; i += NT) acc += (double)g[i] * g[i];
+  for (int64_t i = v1 + threadIdx.x; i < hi; i += NT) {
+    const float x = sum_one<SUM>(g, src, i);
+    acc += (double)x * x;
+  }
   __shared__ double red[NT / 64];
   acc = wave_sum_d(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -389,8 +439,21 @@ int grid_for(int64_t n, int per_thread = 1) {
 extern "C" int nstl_sumsq(const float* g, int64_t n, float* partial, int n_partial, void* stream) {
   NSTL_CHECK_ARG(g && partial && n > 0 && n_partial > 0 && n_partial <= 1024, "nstl_sumsq: bad args");
   NSTL_CHECK_ARG(((uintptr_t)g % 16) == 0, "nstl_sumsq: g must be 16-byte aligned");
-  hipLaunchKernelGGL(sumsq_kernel, dim3(n_partial), dim3(NT), 0, (hipStream_t)stream, g, n, partial);
+  hipLaunchKernelGGL(sumsq_kernel<false>, dim3(n_partial), dim3(NT), 0, (hipStream_t)stream, g, n, partial, SumSrc{});
   NSTL_LAUNCH_CHECK("nstl_sumsq");
+  return 0;
+}
+
+extern "C" int nstl_shard_sum(const float* own, const float* slots, int64_t ld, int n_slots, int64_t n, float* out,
+                              float* partial, int n_partial, void* stream) {
+  NSTL_CHECK_ARG(own && out && partial && n > 0 && n_partial > 0 && n_partial <= 1024 && n_slots >= 0 &&
+                     (n_slots == 0 || (slots && ld >= n)),
+                 "nstl_shard_sum: bad args");
+  NSTL_CHECK_ARG((((uintptr_t)own | (uintptr_t)out | (uintptr_t)slots) % 16) == 0 && ld % 4 == 0,
+                 "nstl_shard_sum: 16-byte aligned arrays and slot stride");
+  hipLaunchKernelGGL(sumsq_kernel<true>, dim3(n_partial), dim3(NT), 0, (hipStream_t)stream, out, n, partial,
+                     SumSrc{own, slots, ld, n_slots, out});
+  NSTL_LAUNCH_CHECK("nstl_shard_sum");
   return 0;
 }
 

@@ -220,6 +220,173 @@ class GradShardReducer(GradAllReducer):
         self.completed = True
 
 
+class _DeviceTransport:
+    """The receive buffers of a ShardPusher in device memory, shared between the
+    ranks' processes through HIP IPC handles (nstl_ipc_*); pushes are copy-engine
+    copies (nstl_copy_engine: hipMemcpyDeviceToDeviceNoCU, no kernel) on a side
+    stream."""
+
+    def __init__(self, grads, comm, n_slots):
+        from . import _hip as K
+        self.K = K
+        self.shard = comm.shard
+        self.recv = torch.empty(max(1, n_slots) * comm.shard, dtype=torch.float32, device=grads.device)
+        self.side = torch.cuda.Stream(grads.device)
+        mine = K.ipc_handle(self.recv)
+        allh = [None] * comm.world
+        dist.all_gather_object(allh, mine, group=comm.group)
+        self.peer = {}
+        self._opened = []
+        for r, (h, off) in enumerate(allh):
+            if r != comm.rank:
+                base = K.ipc_open(h)
+                self._opened.append(base)
+                self.peer[r] = base + off
+
+    def push(self, owner, slot, off, src):
+        """src (a contiguous f32 slice of the arena) -> owner's receive slot `slot`
+        at element offset `off`; ordered after the work queued on the current
+        stream so far."""
+        self.side.wait_stream(torch.cuda.current_stream(src.device))
+        dst = self.peer[owner] + (slot * self.shard + off) * 4
+        self.K.copy_engine(dst, src, src.numel() * 4, stream=self.side.cuda_stream)
+
+    def flush(self):
+        torch.cuda.current_stream(self.recv.device).wait_stream(self.side)
+
+    def sync(self, group):
+        """Every rank's pushes into every receive buffer have landed."""
+        if dist.get_backend(group) == "nccl":
+            # stream-ordered: each rank's all-reduce starts after its own pushes
+            # (flush) and ends after every rank's has started
+            dist.all_reduce(torch.zeros(1, device=self.recv.device), group=group)
+        else:
+            torch.cuda.current_stream(self.recv.device).synchronize()
+            dist.barrier(group=group)
+
+    def slots(self, n_slots):
+        return self.recv[:n_slots * self.shard].view(n_slots, self.shard) if n_slots else self.recv[:0].view(0, 0)
+
+    def close(self):
+        for base in self._opened:
+            self.K.ipc_close(base)
+        self._opened = []
+
+
+class _HostTransport:
+    """The same over host memory (CPU tests with gloo): each rank's receive
+    buffer is a shared file under /dev/shm that every rank maps."""
+
+    def __init__(self, grads, comm, n_slots):
+        import uuid
+        tag = [uuid.uuid4().hex if comm.rank == 0 else None]
+        dist.broadcast_object_list(tag, src=dist.get_global_rank(comm.group, 0) if comm.group is not None else 0,
+                                   group=comm.group)
+        self.shard = comm.shard
+        n = max(1, n_slots) * comm.shard
+        self.paths = {r: "/dev/shm/nstl_push_%s_%d" % (tag[0], r) for r in range(comm.world)}
+        self.recv = torch.from_file(self.paths[comm.rank], shared=True, size=n, dtype=torch.float32)
+        dist.barrier(group=comm.group)
+        self.peer = {r: torch.from_file(p, shared=True, size=n, dtype=torch.float32)
+                     for r, p in self.paths.items() if r != comm.rank}
+        dist.barrier(group=comm.group)
+        import os as _os
+        _os.unlink(self.paths[comm.rank])  # mapped by every rank: the memory stays until they exit
+
+    def push(self, owner, slot, off, src):
+        o = slot * self.shard + off
+        self.peer[owner][o:o + src.numel()].copy_(src)
+
+    def flush(self):
+        pass
+
+    def sync(self, group):
+        dist.barrier(group=group)
+
+    def slots(self, n_slots):
+        return self.recv[:n_slots * self.shard].view(n_slots, self.shard) if n_slots else self.recv[:0].view(0, 0)
+
+    def close(self):
+        pass
+
+
+class ShardPusher(GradAllReducer):
+    """ZeRO-1 with the reduction moved onto the copy engines (NSTL_DP=zero1_push).
+
+    As soon as a bucket of the gradient arena is final (backward's reverse-order
+    prefix, engine.py), each slice of it that another rank's shard holds is
+    pushed into that owner's receive buffer -- a slot per sending rank, mapped
+    from the owner's memory through an IPC handle -- by a device-to-device copy
+    on the copy engines.  No collective kernel runs during backward, so the
+    step's one-tile-per-CU persistent grids keep every CU (the CU-mask route,
+    zero1_overlap, cost +33 %: DESIGN.md section 5).  After backward one tiny
+    collective orders every push before the optimizer, and the owner forms its
+    shard's gradient as own + the slots in rank order in the pass that already
+    computes the clip norm's sums of squares (nstl_shard_sum), then runs the
+    sharded Adam and the bf16 all-gather as zero1 does.
+
+    Pushes overwrite the slots, so a second backward before the step (gradient
+    accumulation) simply pushes the accumulated slices again; a step after a
+    backward that did not finish falls back to the reduce-scatter (consume())."""
+
+    mode = "zero1_push"
+
+    def __init__(self, grads, comm, bucket_bytes=DEFAULT_BUCKET_BYTES, min_world=2):
+        self.comm = comm
+        super().__init__(grads, comm.group, bucket_bytes, min_world)
+        self.n_slots = comm.world - 1
+        self.transport = None
+        if self.active:
+            self.transport = (_DeviceTransport if grads.is_cuda else _HostTransport)(grads, comm, self.n_slots)
+
+    def slot(self, src_rank, owner):
+        """Slot of rank src_rank's contribution in owner's receive buffer."""
+        return src_rank if src_rank < owner else src_rank - 1
+
+    def begin(self, fresh):
+        # no accumulation check: pushes overwrite the slots (see the class doc)
+        if not self.active:
+            return
+        self.reset()
+        self.completed = False
+
+    def ready(self, upto):
+        if not self.active:
+            return
+        upto = min(upto, self.comm.numel)
+        while self.sent < upto:
+            owner = self.sent // self.comm.shard
+            end = min((owner + 1) * self.comm.shard, self.sent + self.bucket)
+            if end > upto:
+                return
+            self._push(self.sent, end, owner)
+
+    def _push(self, lo, hi, owner):
+        if owner != self.comm.rank:
+            self.transport.push(owner, self.slot(self.comm.rank, owner), lo - owner * self.comm.shard, self.g[lo:hi])
+        self.sent = hi
+
+    def finish(self):
+        if not self.active:
+            return
+        while self.sent < self.comm.numel:
+            owner = self.sent // self.comm.shard
+            self._push(self.sent, min((owner + 1) * self.comm.shard, self.sent + self.bucket), owner)
+        self.transport.flush()
+        self.transport.sync(self.group)
+        self.reset()
+        self.completed = True
+
+    def slots(self):
+        """This rank's receive slots [world - 1][shard]: slot k = rank k (k < rank)
+        or k + 1."""
+        return self.transport.slots(self.n_slots)
+
+    def close(self):
+        if self.transport is not None:
+            self.transport.close()
+
+
 class ShardComm:
     """Equal contiguous shards of a flat arena over the ranks of `group`:
     reduce-scatter / all-gather of the arena (torch's tensor collectives, the
@@ -245,20 +412,25 @@ class ShardComm:
         dist.all_gather_into_tensor(full, full[self.lo:self.hi].clone(), group=self.group)
 
 
-def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=None, reduced=False):
+def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=None, reduced=False, sum_fn=None):
     """One sharded clip + Adam step (the FusedAdam kernels passed in as callables,
     so the orchestration is testable on CPU): reduce-scatter the gradients of
     the shardable region [0, comm.numel) (``reduced``: GradShardReducer already
-    summed this rank's shard in place during backward), sum of squares of this
-    shard, all-reduce of the partial sums; `tail` = (lo, hi), a small replicated
-    region (the f32 vectors), is all-reduced whole, its squares added once and
-    updated on every rank; Adam on this shard (+ tail), then all-gather each
-    tensor of `gather` over the shardable region."""
-    if reduced:
-        g_shard.copy_(g_full[comm.lo:comm.hi])
+    summed this rank's shard in place during backward; ``sum_fn``: ShardPusher's
+    slots hold the other ranks' slices, and sum_fn(g_shard, partial) forms the
+    shard and its sums of squares in one pass), sum of squares of this shard,
+    all-reduce of the partial sums; `tail` = (lo, hi), a small replicated region
+    (the f32 vectors), is all-reduced whole, its squares added once and updated
+    on every rank; Adam on this shard (+ tail), then all-gather each tensor of
+    `gather` over the shardable region."""
+    if sum_fn is not None:
+        sum_fn(g_shard, partial)
     else:
-        comm.reduce_scatter(g_full[:comm.numel], g_shard)
-    sumsq_fn(g_shard, partial)
+        if reduced:
+            g_shard.copy_(g_full[comm.lo:comm.hi])
+        else:
+            comm.reduce_scatter(g_full[:comm.numel], g_shard)
+        sumsq_fn(g_shard, partial)
     dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=comm.group)
     if tail is not None and tail[1] > tail[0]:
         lo, hi = tail

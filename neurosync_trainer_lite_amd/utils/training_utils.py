@@ -186,10 +186,12 @@ def attach_data_parallel(model, optimizer, world):
     """Wire one rank's engine/optimizer for data parallelism (parallel.py): the
     loss gradient pre-scaled by 1/world, per-rank dropout streams, and one of
     NSTL_DP=zero1 (default: the sharded optimizer, no collective during
-    backward), zero1_overlap (the same with each shard reduced onto its owner
-    bucket by bucket during backward, the compute stream ceding NSTL_CEDE_CUS
-    CUs, 32 by default (one per XCD shader engine), to the collectives) or allreduce (bucketed all-reduce
-    during backward, replicated optimizer)."""
+    backward), zero1_push (the same with each shard's slices pushed to their
+    owner by the copy engines during backward: parallel.ShardPusher),
+    zero1_overlap (each shard reduced onto its owner bucket by bucket during
+    backward, the compute stream ceding NSTL_CEDE_CUS CUs, 32 by default (one
+    per XCD shader engine), to the collectives) or allreduce (bucketed
+    all-reduce during backward, replicated optimizer)."""
     eng = _engine_of(model)
     if eng is None or world == 1 or eng.grad_scale_t is not None:
         return
@@ -201,7 +203,10 @@ def attach_data_parallel(model, optimizer, world):
         eng.grad_reducer = GradAllReducer(eng.g32)
     else:
         optimizer.shard()
-        if mode == "zero1_overlap":
+        if mode == "zero1_push":
+            from ..parallel import ShardPusher
+            eng.grad_reducer = ShardPusher(eng.g32, optimizer._comm)
+        elif mode == "zero1_overlap":
             from ..parallel import GradShardReducer, cede_cus
             cede_cus(int(os.environ.get("NSTL_CEDE_CUS", "32")), eng.device)
             eng.grad_reducer = GradShardReducer(eng.g32, optimizer._comm)

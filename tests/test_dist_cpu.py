@@ -93,7 +93,7 @@ def test_data_parallel_gloo(tmp_path, monkeypatch):
         torch.testing.assert_close(a[k], v, rtol=1e-5, atol=1e-6)
 
 
-def _shard_worker(rank, port, out_dir, world=WORLD, overlap=False):
+def _shard_worker(rank, port, out_dir, world=WORLD, overlap=False, push=False, accumulate=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -121,14 +121,43 @@ def _shard_worker(rank, port, out_dir, world=WORLD, overlap=False):
         v[lo:lo + k] = 0.999 * v[lo:lo + k] + 0.001 * gg * gg
         p[lo:lo + k] -= 1e-3 / 0.1 * m[lo:lo + k] / ((v[lo:lo + k] / 0.001).sqrt() + 1e-8)
 
-    if overlap:
+    sum_fn = None
+    red = None
+    if push:
+        red = parallel.ShardPusher(grads, comm, bucket_bytes=4000)
+    if accumulate:
+        # two backwards before the step: the arena holds g1, then g1 + g2
+        g1 = torch.randn(n, generator=torch.Generator().manual_seed(30 + rank))
+        g2 = grads.clone()
+        grads.copy_(g1)
+        if push:  # the first backward pushes g1's slices
+            red.begin(True)
+            for upto in (9000, ns - 5, n):
+                red.ready(upto)
+            red.finish()
+        grads += g2
+    if overlap or push:
         # backward's arena prefixes become final in uneven steps; buckets of 1000
-        # elements (cut at the shard boundaries) are reduced as they complete
-        red = parallel.GradShardReducer(grads, comm, bucket_bytes=4000)
+        # elements (cut at the shard boundaries) are reduced / pushed as they complete
+        if push:
+            red.begin(not accumulate)
+        else:
+            red = parallel.GradShardReducer(grads, comm, bucket_bytes=4000)
         for upto in (700, 2500, 2600, 9000, 30001, ns // 2 + 7, ns - 5, n):
             red.ready(upto)
         red.finish()
-    parallel.zero1_step(comm, grads, gs, partial, sumsq_fn, adam_fn, [p], tail=(ns, n), reduced=overlap)
+        if push:
+            assert red.consume()
+            own, slots = grads[comm.lo:comm.hi], red.slots()
+
+            def sum_fn(out, part):
+                x = own.clone()
+                for k in range(red.n_slots):  # slot order: the ranks in order, this one left out
+                    x += slots[k]
+                out.copy_(x)
+                sumsq_fn(out, part)
+    parallel.zero1_step(comm, grads, gs, partial, sumsq_fn, adam_fn, [p], tail=(ns, n), reduced=overlap,
+                        sum_fn=sum_fn)
     for t in (m, v):
         comm.all_gather(t[:ns])  # consolidate
     torch.save({"p": p, "m": m, "v": v}, os.path.join(out_dir, "s%d.pt" % rank))
@@ -158,6 +187,30 @@ def test_sharded_optimizer_step_gloo(tmp_path, world):
     torch.testing.assert_close(r0["p"], p, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(r0["m"], m, rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(r0["v"], v, rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("world,accumulate", [(2, False), (4, False), (2, True)])
+def test_pushed_shard_reduce_is_bit_identical_gloo(tmp_path, world, accumulate):
+    """NSTL_DP=zero1_push (parallel.ShardPusher, host transport: each rank's
+    receive slots a shared /dev/shm mapping, the stand-in for the IPC-mapped
+    device buffers the copy engines write): the slices pushed bucket by bucket
+    during backward and summed by their owner (own + slots in rank order) give
+    the same parameters and moments as the post-backward reduce-scatter -- bit
+    for bit at two ranks (one addition either way), to f32 rounding at four.
+    With two backwards before the step (gradient accumulation), the second
+    push overwrites the first: nothing is counted twice."""
+    for push, sub in ((False, "rs"), (True, "push")):
+        d = tmp_path / sub
+        d.mkdir()
+        mp.spawn(_shard_worker, args=(_port(), str(d), world, False, push, accumulate), nprocs=world, join=True)
+    for r in range(world):
+        a = torch.load(tmp_path / "rs" / ("s%d.pt" % r), weights_only=True)
+        b = torch.load(tmp_path / "push" / ("s%d.pt" % r), weights_only=True)
+        for k in a:
+            if world == 2:
+                assert torch.equal(a[k], b[k]), (r, k)
+            else:
+                torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-7)
 
 
 @pytest.mark.parametrize("world", [2, 4])

@@ -38,9 +38,9 @@ def _batch(i):
     return (torch.randn(2, 64, 256, generator=g).cuda(), (torch.randn(2, 64, 61, generator=g) * 20).cuda())
 
 
-def _worker(rank, port, out_dir):
+def _worker(rank, port, out_dir, mode="zero1"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
-                      LOCAL_RANK="0", NSTL_DP="zero1")
+                      LOCAL_RANK="0", NSTL_DP=mode)
     from neurosync_trainer_lite_amd import parallel
     from neurosync_trainer_lite_amd.utils.training_utils import attach_data_parallel
     parallel.init_from_env(backend="gloo")
@@ -49,6 +49,8 @@ def _worker(rank, port, out_dir):
     model(_batch(0)[0])  # build the engine
     attach_data_parallel(model, opt, WORLD)
     assert opt._comm is not None
+    if mode == "zero1_push":
+        assert isinstance(model.engine().grad_reducer, parallel.ShardPusher)
     for s in range(STEPS):
         src, trg = _batch(2 * s + rank)
         opt.zero_grad()
@@ -61,7 +63,10 @@ def _worker(rank, port, out_dir):
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     osd = opt.state_dict()
     torch.save({"params": sd, "m": osd["state"][3]["exp_avg"].cpu(), "norm": float(opt.last_norm.item())},
-               os.path.join(out_dir, "z%d.pt" % rank))
+               os.path.join(out_dir, "%s%d.pt" % ("z" if mode == "zero1" else mode, rank)))
+    red = model.engine().grad_reducer
+    if hasattr(red, "close"):
+        red.close()
     dist.destroy_process_group()
 
 
@@ -89,3 +94,23 @@ def test_sharded_optimizer_matches_single_process(tmp_path):
         torch.testing.assert_close(z0["params"][k], v, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(z0["m"], opt.state_dict()["state"][3]["exp_avg"].cpu(), rtol=1e-5, atol=1e-8)
     assert abs(z0["norm"] - float(opt.last_norm.item())) < 1e-4 * float(opt.last_norm.item())
+
+
+def test_pushed_shards_bit_identical_to_zero1(tmp_path):
+    """NSTL_DP=zero1_push through the real kernels and copy engines: two ranks on
+    cuda:0 map each other's receive buffers by IPC handle, push their gradient
+    slices with device-to-device copies on the copy engines
+    (hipMemcpyDeviceToDeviceNoCU) during backward, and each owner sums its shard
+    with nstl_shard_sum (own + the other rank's slot, and the clip norm's
+    partials in the same pass).  At two ranks that is the reduce-scatter's one
+    addition, so parameters, moments and the clip norm equal zero1's bit for
+    bit."""
+    for mode in ("zero1", "zero1_push"):
+        mp.spawn(_worker, args=(_port(), str(tmp_path), mode), nprocs=WORLD, join=True)
+    for r in range(WORLD):
+        a = torch.load(tmp_path / ("z%d.pt" % r), weights_only=True)
+        b = torch.load(tmp_path / ("zero1_push%d.pt" % r), weights_only=True)
+        for k in a["params"]:
+            assert torch.equal(a["params"][k], b["params"][k]), (r, k)
+        assert torch.equal(a["m"], b["m"]), r
+        assert a["norm"] == b["norm"], (a["norm"], b["norm"])
