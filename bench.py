@@ -707,7 +707,10 @@ def main():
             "data": "synthetic (seeded features [B,T,256] + targets [B,T,61], resident in HBM)",
             "config": {"workload": "228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam)",
                        "model": "NeuroSync Seq2Seq 228M", "global_batch": B * world, "seq_len": T,
-                       "frames_per_step": B * T * world, "parallelism": "dp%d" % world},
+                       "frames_per_step": B * T * world, "parallelism": "dp%d" % world,
+                       "gradient_exchange": (None if world == 1 else
+                                             type(eng.grad_reducer).__name__ if eng.grad_reducer is not None
+                                             else "zero1 (reduce-scatter after backward)")},
             "roofline": {"bound": "mfma", "kernel": "nstl GEMM family, all hand-written: gemm4_kernel (4-wave persistent "
                                                     "256^2: every full-tile forward / dX / grouped dW), gemm256r_kernel "
                                                     "(8-wave ring: f32 beta-1 dX, the memory gradient), gemm_kernel "

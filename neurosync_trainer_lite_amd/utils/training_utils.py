@@ -185,9 +185,10 @@ def rank_batches(dataloader, rank, world):
 def attach_data_parallel(model, optimizer, world):
     """Wire one rank's engine/optimizer for data parallelism (parallel.py): the
     loss gradient pre-scaled by 1/world, per-rank dropout streams, and one of
-    NSTL_DP=zero1 (default: the sharded optimizer, no collective during
-    backward), zero1_push (the same with each shard's slices pushed to their
-    owner by the copy engines during backward: parallel.ShardPusher),
+    NSTL_DP=zero1_push (default: the sharded optimizer, each shard's slices
+    pushed to their owner by the copy engines during backward, no collective
+    kernel in it: parallel.ShardPusher), zero1 (the same with a reduce-scatter
+    after backward),
     zero1_overlap (each shard reduced onto its owner bucket by bucket during
     backward, the compute stream ceding NSTL_CEDE_CUS CUs, 32 by default (one
     per XCD shader engine), to the collectives) or allreduce (bucketed
@@ -197,7 +198,7 @@ def attach_data_parallel(model, optimizer, world):
         return
     eng.grad_scale_t = torch.full((1,), 1.0 / world, device=eng.device)
     eng.seed_salt = dist.get_rank()
-    mode = os.environ.get("NSTL_DP", "zero1")
+    mode = os.environ.get("NSTL_DP", "zero1_push")
     if mode == "allreduce" or not hasattr(optimizer, "shard"):
         from ..parallel import GradAllReducer
         eng.grad_reducer = GradAllReducer(eng.g32)
@@ -205,7 +206,7 @@ def attach_data_parallel(model, optimizer, world):
         optimizer.shard()
         if mode == "zero1_push":
             from ..parallel import ShardPusher
-            eng.grad_reducer = ShardPusher(eng.g32, optimizer._comm)
+            eng.grad_reducer = ShardPusher.create(eng.g32, optimizer._comm)  # None: zero1 (every rank agrees)
         elif mode == "zero1_overlap":
             from ..parallel import GradShardReducer, cede_cus
             cede_cus(int(os.environ.get("NSTL_CEDE_CUS", "32")), eng.device)
