@@ -342,7 +342,7 @@ enum {
   NSTL_K_GEMM_GROUP,         /* grouped ring GEMM launches (weight gradients) */
   NSTL_K_GEMM_GROUP_TILES,   /*   ... their tiles */
   NSTL_K_GEMM_SPLITK_REDUCE, /* split-K combine launches */
-  NSTL_K_GEMM_FP8,           /* fp8 ring GEMM launches */
+  NSTL_K_GEMM_FP8,           /* fp8 GEMM launches (either kernel) */
   NSTL_K_ATTN_FWD,           /* MFMA attention forward */
   NSTL_K_ATTN_FWD_GENERIC,
   NSTL_K_ATTN_BWD_FUSED,     /* one-kernel attention backward */
@@ -352,6 +352,7 @@ enum {
   NSTL_K_GEMM4_TILES,        /*   ... their 256x256 output tiles */
   NSTL_K_GEMM4_SK,           /*   ... launches with a stream-K tail (grid not dividing the tiles) */
   NSTL_K_GEMM_FP8_ROPE,      /* fp8 GEMM launches with the RoPE epilogue (C5 q|k|v, cross q, cross k|v) */
+  NSTL_K_GEMM4F8,            /* fp8 GEMM launches on the 4-wave persistent kernel (the rest: NSTL_K_GEMM_FP8) */
   NSTL_K_COUNT
 };
 /* Copy-engine ZeRO-1 (parallel.ShardPusher; replaces the reference's gather of

@@ -126,7 +126,7 @@ IPC_HANDLE_BYTES = 64
 # nstl_kernel_counts order (NSTL_K_* in include/nstl.h)
 KERNEL_COUNT_NAMES = ["gemm128", "gemm_ring", "gemm_ring_tiles", "gemm_group", "gemm_group_tiles",
                       "gemm_splitk_reduce", "gemm_fp8", "attn_fwd", "attn_fwd_generic", "attn_bwd_fused",
-                      "attn_bwd_split", "attn_bwd_generic", "gemm4", "gemm4_tiles", "gemm4_sk", "gemm_fp8_rope"]
+                      "attn_bwd_split", "attn_bwd_generic", "gemm4", "gemm4_tiles", "gemm4_sk", "gemm_fp8_rope", "gemm4_fp8"]
 
 _lib = None
 

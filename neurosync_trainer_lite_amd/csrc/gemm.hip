@@ -1328,12 +1328,24 @@ int make_params(const nstl_gemm_args* a, GemmParams& p) {
   return 0;
 }
 
-// FP8 operands: the fp8 ring kernel (K-major A and B, K % 64 == 0, no split-K)
+}  // namespace
+namespace nstl {
+int gemm4_f8(const nstl_gemm_args* a, hipStream_t st, int* handled);  // gemm4.hip
+}
+namespace {
+
+// FP8 operands: the 4-wave kernel for full tiles (gemm4f8_kernel), the fp8 ring
+// kernel otherwise (K-major A and B, K % 64 == 0, no split-K)
 int gemm_f8(const nstl_gemm_args* a, GemmParams& p, hipStream_t st) {
   NSTL_CHECK_ARG(a->a_kmajor && a->b_kmajor, "nstl_gemm: FP8 needs K-major A and B (Y = X W^T)");
   NSTL_CHECK_ARG(a->K % 64 == 0, "nstl_gemm: FP8 needs K %% 64 == 0 (got %d)", a->K);
   NSTL_CHECK_ARG(a->a_scale && a->b_scale, "nstl_gemm: FP8 needs the row scales a_scale [M] and b_scale [N]");
   NSTL_CHECK_ARG(a->split_k <= 1, "nstl_gemm: FP8: no split-K");
+  {
+    int handled = 0;
+    if (int rc = nstl::gemm4_f8(a, st, &handled)) return rc;
+    if (handled) return 0;
+  }
   const int em = ring_epi_mode(a, p);
   NSTL_CHECK_ARG(em == EM_BF16 || em == EM_RELU_DROP || em == EM_ROPE || em == EM_DRELU || em == EM_F32,
                  "nstl_gemm: FP8 supports the NONE / BIAS / BIAS_RELU_DROP / BIAS_ROPE / DRELU_DROP epilogues "

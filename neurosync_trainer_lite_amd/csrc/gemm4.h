@@ -66,6 +66,9 @@ struct Params {
   float* colsum_part;              // [M / 128][N] (DRELU)
   uint64_t* relu_mask;             // keep & positive bits, the ring layout (RELU_DROP writes, DRELU reads)
   float* sq_part;                  // [tiles][8] sums of squares of C (F32)
+  const float* a_scale;            // fp8 (gemm4f8_kernel): f32 row scales of A [M] and of B [N]
+  const float* b_scale;
+  int rope_bf16;                   // EM_ROPE: the LDS table holds bf16 (cos, sin) (fp8 at T = 256)
   uint32_t a_bytes, b_bytes;       // extents of A and B (buffer range checks)
   int tiles_m, tiles_n;
 };
@@ -348,6 +351,8 @@ NSTL_DEV int rope_swz(int rope_dim) {
   return (low < 16 ? low : 16) - 1;
 }
 NSTL_DEV int rope_off(int t, int chunk, int row_bytes, int swz) { return t * row_bytes + ((chunk ^ (t & swz)) << 4); }
+// the bf16 table: 8-byte chunks
+NSTL_DEV int rope_off8(int t, int chunk, int row_bytes, int swz) { return t * row_bytes + ((chunk ^ (t & swz)) << 3); }
 
 // An accumulator tile read out of the AGPRs at the point of use ...  Left to the
 // compiler, the epilogue's VALU uses split the accumulators' live range at the
@@ -510,11 +515,22 @@ NSTL_DEV bool sk_handoff(const StreamK& sk, f32x4 (&acc)[8][8], const Seg& s, in
 // No epilogue loads from memory after its first store (vmcnt retires in issue
 // order, so such a load would wait for the stores before it): the inputs are
 // loaded first (bias, dReLU mask words) or read from LDS (RoPE tables).
-template <int EM>
+// SC (the fp8 kernel): C = a_scale[row] b_scale[col] acc, applied as (acc (a_scale
+// alpha)) b_scale -- the fp8 ring kernel's order -- before the bias.
+template <int EM, bool SC = false>
 NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, int lane, int wave, int tile_id,
                        const char* rope_lds, bool fin = true) {
   const int g = lane >> 4, c = lane & 15, odd = g & 1;
   const float alpha = p.alpha;
+  float rsc[8], csc[8][4];  // SC: the lane's row scales (times alpha) and column scales
+  if constexpr (SC) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a) rsc[a] = p.a_scale[row0 + 16 * a + c] * alpha;
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csc[b][e] = p.b_scale[col0 + 16 * b + 4 * g + e];
+  }
   if constexpr (EM == EM_F32) {
     // f32 out: lane stores its 4 columns (16 B); sum of squares of the stored
     // values -> sq_part (the clip norm's partial, training_utils.py:73)
@@ -528,7 +544,14 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       const uint32_t crow = ((uint32_t)(row0 + 16 * a + c) * (uint32_t)p.ldc + col0 + 4 * g) * 4u;
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
-        const f32x4 v = rd_acc(acc[a][b]) * alpha;
+        f32x4 v;
+        if constexpr (SC) {
+          v = rd_acc(acc[a][b]) * rsc[a];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= csc[b][e];
+        } else {
+          v = rd_acc(acc[a][b]) * alpha;
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) ssq += v[e] * v[e];
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, v), rc, crow + 64 * b, 0, 0);
@@ -600,7 +623,15 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       f32x4 rcs[8];
       if constexpr (EM == EM_ROPE) {
 #pragma unroll
-        for (int b = 0; b < 8; ++b) rcs[b] = *(const f32x4*)(rope_lds + rope_off(t, rchunk[b], rope_rb, rswz));
+        for (int b = 0; b < 8; ++b) {
+          if (p.rope_bf16) {  // (cos, sin) pairs as bf16 (8-byte chunks): the fp8 kernel at T = 256
+            const uint2 w = *(const uint2*)(rope_lds + rope_off8(t, rchunk[b], p.rope_dim * 2, rswz));
+            rcs[b] = (f32x4){__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xFFFF0000u),
+                             __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xFFFF0000u)};
+          } else {
+            rcs[b] = *(const f32x4*)(rope_lds + rope_off(t, rchunk[b], rope_rb, rswz));
+          }
+        }
       }
 #pragma unroll
       for (int bp = 0; bp < 8; bp += 2) {
@@ -613,7 +644,14 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
         for (int s = 0; s < 2; ++s) {
           const int b = bp + s;
           const int col = col0 + 16 * b + 4 * g;
-          f32x4 v = uv[s] * alpha;
+          f32x4 v;
+          if constexpr (SC) {
+            v = uv[s] * rsc[a];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] *= csc[b][e];
+          } else {
+            v = uv[s] * alpha;
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += bias[b][e];
           if constexpr (EM == EM_RELU_DROP) {
@@ -948,6 +986,251 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     lt = nlt;
   }
   G4_VMCNT(0);  // the refill must land before the workgroup's LDS is released
+}
+
+// ---------------------------------------------------------------------------
+// fp8 (e4m3) on the same structure (BASELINE config C5: the q|k|v / cross q,
+// k|v / encoder FFN linear1 forward and FFN linear2 input-gradient GEMMs):
+//   C[i, j] = a_scale[i] b_scale[j] sum_r A[i][r] B[j][r]   (+ epilogue)
+// A [M][K], B [N][K] OCP e4m3 bytes, K-major (nstl_fp8_quant_rows / _cols), on
+// v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0 block scales: 128 K-bytes
+// per instruction at twice the bf16 rate per clock, and the 16 x 16
+// accumulator layout of the bf16 kernel, so its epilogues (bias, ReLU-dropout +
+// keep bits, RoPE, dReLU + column sums, f32) are reused as they are, with the
+// row and column scales applied first (SC).
+// A stage is 128 K-bytes: 256 rows x 128 B per operand, the bf16 K-major image
+// byte for byte (chunk c of row r at c ^ ((r >> 1) & 7)), filled by the same
+// LDS-DMA pieces.  A lane's fragment of a 16-row block is 32 K-bytes (chunks
+// 2g, 2g + 1 of its row, g = lane >> 4): 8 VGPRs, two ds_read_b128.  A stage's
+// 64 MFMAs per wave need all 8 B fragments (64 VGPRs) and 8 A fragments (64),
+// so the half-steps split the output rows instead of K: h = 0 computes A row
+// blocks 0..3 against all of B while reading blocks 4..7; h = 1 computes 4..7
+// while reading the next stage's blocks 0..3 and all of its B into the second
+// B set, and issues the stage after next by DMA.  Fragment registers: 2 x 32
+// (A) + 2 x 64 (B) = 192.
+constexpr int F8_BK = 128;  // K-bytes per stage
+
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+
+NSTL_DEV void mma_f8(f32x4& acc, const i32x8_t& w, const i32x8_t& x) {
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w, x, acc, 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+}
+
+// per-lane DMA sources of one operand's stage (K-major, 128-byte rows of bytes)
+NSTL_DEV void dma_lane_offsets_f8(uint32_t (&vo)[8], int64_t ld, int wave, int lane) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int q = wave * 8 + s;
+    const int row = 8 * q + (lane >> 3), pc = lane & 7;
+    const int lc = pc ^ ((row >> 1) & 7);
+    vo[s] = (uint32_t)((int64_t)row * ld + lc * 16);
+  }
+}
+NSTL_DEV void dma_tile_f8(Dma& d, const Params& p, int m0, int n0) {
+  d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)p.a_bytes, 0x00020000);
+  d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, (int)p.b_bytes, 0x00020000);
+  d.a_kb = F8_BK;
+  d.b_kb = F8_BK;
+  d.ta = __builtin_amdgcn_readfirstlane((uint32_t)(m0 * p.lda));
+  d.tb = __builtin_amdgcn_readfirstlane((uint32_t)(n0 * p.ldb));
+}
+
+// the two read addresses of a lane's fragment (chunks 2g, 2g + 1 of its row of
+// row block 0; block j at + 2048 j)
+struct RdAddrF8 {
+  uint32_t k[2];
+};
+NSTL_DEV void rd_addr_f8(RdAddrF8& r, uint32_t img, int blk0, int lane) {
+  const int row = blk0 + (lane & 15), sw = (row >> 1) & 7, g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) r.k[j] = img + row * 128 + (((2 * g + j) ^ sw) << 4);
+}
+template <int OFF>
+NSTL_DEV void rd_f8(i32x8_t& f, const RdAddrF8& r) {
+  i32x4_t v0, v1;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v0) : "v"(r.k[0]), "i"(OFF));
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v1) : "v"(r.k[1]), "i"(OFF));
+  f = (i32x8_t){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+}
+
+// One fp8 half-step: 32 MFMAs, column-major -- for B block b = 0..7, A blocks
+// 4H .. 4H + 3 (ca) -- so that in h = 1 B fragment b dies after MFMA 4b + 3 and
+// the next stage's B block b is read into its registers right there (one B
+// register set, not two).  Reads: h = 0 A blocks 4..7 of the current stage (slot
+// offset SO) into na after MFMAs 1, 6, 11, 16; h = 1 the next stage's (SO) A
+// blocks 0..3 into na after MFMAs 0, 8, 16, 24 and B block b after MFMA 4b + 3
+// (the last, block 7, after the final MFMA: the next h = 0 uses it first at
+// MFMA 28 and waits for it there).  DMA (h = 1): the 16 pieces after MFMAs 1, 3,
+// ..., 31.  H = 2: h = 1 without any read.
+template <int H, int SO, int DBG, int I = 0>
+NSTL_DEV void half_step_f8(f32x4 (&acc)[8][8], const i32x8_t (&ca)[4], i32x8_t (&cb)[8], i32x8_t (&na)[4],
+                           const RdAddrF8& ra, const RdAddrF8& rb, const Dma& d, char* adst, char* bdst, uint32_t sa,
+                           uint32_t sb) {
+  if constexpr (I < 32) {
+    constexpr int b = I >> 2, a = I & 3;
+    if constexpr (H == 0 && I == 28) {
+      // B block 7's read (the previous h = 1's last) is older than the 8 A reads
+      // issued since: retire it
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      G4_SB();
+    }
+    if constexpr (!(DBG & 8)) mma_f8(acc[4 * (H ? 1 : 0) + a][b], cb[b], ca[a]);
+    G4_SB();
+    if constexpr (!(DBG & 2)) {
+      if constexpr (H == 0 && (I == 1 || I == 6 || I == 11 || I == 16)) {
+        constexpr int r = I == 1 ? 0 : I == 6 ? 1 : I == 11 ? 2 : 3;
+        rd_f8<SO + (4 + r) * 2048>(na[r], ra);
+        G4_SB();
+      }
+      if constexpr (H == 1 && (I & 7) == 0) {
+        rd_f8<SO + (I >> 3) * 2048>(na[I >> 3], ra);
+        G4_SB();
+      }
+      if constexpr (H == 1 && a == 3) {
+        rd_f8<SO + b * 2048>(cb[b], rb);
+        G4_SB();
+      }
+    }
+    if constexpr (H >= 1 && !(DBG & 1) && (I & 1) == 1) {
+      constexpr int q = I >> 1;
+      if constexpr (q < 8) dma16(d.ra, adst + q * 1024, d.va[q], d.ta + sa);
+      else dma16(d.rb, bdst + (q - 8) * 1024, d.vb[q - 8], d.tb + sb);
+      G4_SB();
+    }
+    half_step_f8<H, SO, DBG, I + 1>(acc, ca, cb, na, ra, rb, d, adst, bdst, sa, sb);
+  }
+}
+
+// Preconditions (host-checked): e4m3 A [M][K] and B [N][K], M and N multiples of
+// 256, K a multiple of 256 with K >= 512 (whole pairs of 128-byte stages, at
+// least two pairs), 16-byte aligned rows, operand extents < 2^31 bytes; EM_ROPE:
+// the table fits ROPE_LDS as f32 or (rope_bf16) as bf16.
+template <int EM, int DBG = 0>
+__global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + (EM == EM_ROPE ? ROPE_LDS : 0)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int T = gp.tile_end[0];
+  const int G = gridDim.x;
+  const Params& p = gp.g[0];
+  Walker wk;
+  wk.init(gp, T, blockIdx.x, G, false);
+  Seg sg;
+  if (!wk.next(sg)) return;
+  const uint32_t smem_u32 = lds_addr(smem);
+  char* const adst0 = smem + wave * 8 * 1024;
+  char* const bdst0 = smem + 2 * OPS + wave * 8 * 1024;
+  const char* rope_lds = smem + SMEM;
+  if constexpr (EM == EM_ROPE) {
+    const int half = p.rope_dim >> 1, chunks = p.rope_dim >> 2, swz = rope_swz(p.rope_dim);
+    for (int i = tid; i < p.rope_T * chunks; i += NT) {
+      const int tt = i / chunks, k = i - tt * chunks;
+      const float2 cs = *(const float2*)(p.rope_cos + tt * half + 2 * k);
+      const float2 sn = *(const float2*)(p.rope_sin + tt * half + 2 * k);
+      if (p.rope_bf16) {
+        *(uint2*)(smem + SMEM + rope_off8(tt, k, p.rope_dim * 2, swz)) =
+            make_uint2(pack_bf16x2(cs.x, sn.x), pack_bf16x2(cs.y, sn.y));
+      } else {
+        *(f32x4*)(smem + SMEM + rope_off(tt, k, p.rope_dim * 4, swz)) = (f32x4){cs.x, sn.x, cs.y, sn.y};
+      }
+    }
+    __syncthreads();
+  }
+  int m0, n0;
+  tile_coords(xcd_remap(sg.t, T), p.tiles_m, p.tiles_n, m0, n0);
+  int lt = 0;
+  Dma d;
+  dma_lane_offsets_f8(d.va, p.lda, wave, lane);
+  dma_lane_offsets_f8(d.vb, p.ldb, wave, lane);
+  dma_tile_f8(d, p, m0, n0);
+  RdAddrF8 ra, rb;
+  rd_addr_f8(ra, smem_u32, wm * 128, lane);
+  rd_addr_f8(rb, smem_u32 + 2 * OPS, wn * 128, lane);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  i32x8_t fa0[4], fa1[4], fb[8];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma16(d.ra, adst0 + s * OPS + q * 1024, d.va[q], d.ta + (uint32_t)s * d.a_kb);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma16(d.rb, bdst0 + s * OPS + q * 1024, d.vb[q], d.tb + (uint32_t)s * d.b_kb);
+  }
+  G4_VMCNT(0);
+  __builtin_amdgcn_s_barrier();
+  G4_SB();
+  // stage 0 (slot 0): A blocks 0..3 and all of B
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rd_f8<0>(fa0[j], (RdAddrF8){{ra.k[0] + j * 2048, ra.k[1] + j * 2048}});
+#pragma unroll
+  for (int j = 0; j < 8; ++j) rd_f8<0>(fb[j], (RdAddrF8){{rb.k[0] + j * 2048, rb.k[1] + j * 2048}});
+  G4_LGKM0();
+
+  // step on stage slot S: h = 0 on A blocks 0..3 (reading blocks 4..7), the
+  // counted wait + barrier, h = 1 on blocks 4..7 with the next stage's reads
+  // (slot 1 - S) and the DMA of stage `dma_stage` into slot S.  After h = 1 every
+  // read but the last B block's has retired (lgkmcnt(2): its two instructions).
+  auto step = [&](auto slot_c, auto waitn_c, uint32_t dma_stage) {
+    constexpr int S = decltype(slot_c)::value;
+    constexpr int WAITN = decltype(waitn_c)::value;
+    half_step_f8<0, S * OPS, DBG>(acc, fa0, fb, fa1, ra, rb, d, adst0, bdst0, 0, 0);
+    G4_LGKM0();
+    if constexpr (WAITN == 0) G4_VMCNT(0);
+    else if constexpr (WAITN == 32) G4_VMCNT(32);
+    else G4_VMCNT(63);
+    __builtin_amdgcn_s_barrier();
+    G4_SB();
+    half_step_f8<1, (1 - S) * OPS, DBG>(acc, fa1, fb, fa0, ra, rb, d, adst0 + S * OPS, bdst0 + S * OPS,
+                                        dma_stage * d.a_kb, dma_stage * d.b_kb);
+    asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+    G4_SB();
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using W0 = std::integral_constant<int, 0>;
+  using WE = std::integral_constant<int, EM == EM_F32 ? 63 : 32>;
+
+  const int nk = p.K / F8_BK;
+  for (;;) {
+    Seg ns;
+    const bool has_next = wk.next(ns);
+    if (!has_next) ns = sg;
+    int nm0 = m0, nn0 = n0;
+    if (has_next) tile_coords(xcd_remap(ns.t, T), p.tiles_m, p.tiles_n, nm0, nn0);
+    step(S0{}, WE{}, 2u);
+    for (int kt = 1; kt < nk; kt += 2) {
+      step(S1{}, W0{}, (uint32_t)(kt + 2 < nk ? kt + 2 : kt + 2 - nk));
+      if (kt + 1 < nk) {
+        if (kt + 1 == nk - 2) dma_tile_f8(d, p, nm0, nn0);
+        step(S0{}, W0{}, (uint32_t)(kt + 3 < nk ? kt + 3 : kt + 3 - nk));
+      }
+    }
+    G4_LGKM0();  // the next tile's last B fragment: before the epilogue's own LDS reads
+    lt = sg.t < T ? xcd_remap(sg.t, T) : sg.t;
+    epilogue<EM, true>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, true);
+    if (!has_next) break;
+    if constexpr (EM != EM_BF16) {
+      // the per-lane DMA offsets and read addresses, recomputed after every
+      // epilogue from a lane index the compiler cannot see through: kept live
+      // across it (20 VGPRs) they made the scaled RoPE / dReLU epilogues spill
+      // (the plain one is spill-free without, and spills with it)
+      int lane_o = lane;
+      asm volatile("" : "+v"(lane_o));
+      dma_lane_offsets_f8(d.va, p.lda, wave, lane_o);
+      dma_lane_offsets_f8(d.vb, p.ldb, wave, lane_o);
+      rd_addr_f8(ra, smem_u32, wm * 128, lane_o);
+      rd_addr_f8(rb, smem_u32 + 2 * OPS, wn * 128, lane_o);
+    }
+    sg = ns;
+    m0 = nm0;
+    n0 = nn0;
+  }
+  G4_VMCNT(0);
 }
 
 }  // namespace g4

@@ -225,9 +225,79 @@ int launch(int em, bool ak, bool bk, bool grouped, int G, hipStream_t st, g4::Gr
   return 1;
 }
 
+// ---------------------------------------------------------------------------
+// fp8 (gemm4f8_kernel): e4m3 A [M][K] and B [N][K] with row scales (C5)
+int g4f8_mode(const nstl_gemm_args* a) {
+  if (a->dtype != NSTL_FP8 || a->split_k > 1 || a->beta != 0.f || !a->a_kmajor || !a->b_kmajor) return 0;
+  if (!a->a_scale || !a->b_scale || a->sq_part) return 0;
+  const bool bf_out = a->c_dtype == NSTL_BF16;
+  if (a->colsum_part != nullptr && a->epilogue != NSTL_EPI_DRELU_DROP) return 0;
+  if (a->relu_mask != nullptr && a->epilogue != NSTL_EPI_BIAS_RELU_DROP && a->epilogue != NSTL_EPI_DRELU_DROP)
+    return 0;
+  switch (a->epilogue) {
+    case NSTL_EPI_NONE: return bf_out ? g4::EM_BF16 : 0;  // f32 out: the ring kernel (tests only)
+    case NSTL_EPI_BIAS: return bf_out ? g4::EM_BF16 : 0;
+    case NSTL_EPI_BIAS_RELU_DROP: return bf_out && (a->N & 1) == 0 ? g4::EM_RELU_DROP : 0;
+    case NSTL_EPI_BIAS_ROPE:
+      // the table in LDS: f32, or bf16 when only that fits (T = 256 with head dim 64)
+      return bf_out && a->rope_dim % 4 == 0 && a->rope_cols % 16 == 0 &&
+                     (int64_t)a->rope_T * a->rope_dim * 2 <= g4::ROPE_LDS
+                 ? g4::EM_ROPE
+                 : 0;
+    case NSTL_EPI_DRELU_DROP: return bf_out && a->relu_mask != nullptr ? g4::EM_DRELU : 0;
+    default: return 0;
+  }
+}
+
+bool g4f8_shape_ok(const nstl_gemm_args* a) {
+  if (a->M % g4::TILE || a->N % g4::TILE || a->K % (2 * g4::F8_BK) || a->K < 4 * g4::F8_BK) return false;
+  if (((uintptr_t)a->A | (uintptr_t)a->B | (uintptr_t)a->C) % 16) return false;
+  if (a->lda % 16 || a->ldb % 16) return false;
+  if (a->ldc % (a->c_dtype == NSTL_F32 ? 4 : 8)) return false;
+  const int64_t ae = (int64_t)(a->M - 1) * a->lda + a->K, be = (int64_t)(a->N - 1) * a->ldb + a->K;
+  const int64_t ce = a->c_dtype == NSTL_F32 ? (int64_t)a->M * a->ldc * 4 : 0;
+  return ae < (1ll << 31) && be < (1ll << 31) && ce < (1ll << 31);
+}
+
 }  // namespace
 
 namespace nstl {
+
+// NSTL_GEMM4_F8=0 keeps every fp8 GEMM on the 8-wave ring kernel (A/B runs; read per call)
+int gemm4_f8(const nstl_gemm_args* a, hipStream_t st, int* handled) {
+  *handled = 0;
+  const char* e = getenv("NSTL_GEMM4_F8");
+  if ((e && atoi(e) == 0) || !gemm4_env() || !g4f8_shape_ok(a)) return 0;
+  const int em = g4f8_mode(a);
+  if (!em) return 0;
+  const int G = nstl::stream_cus(st);
+  if (G <= 0) return 0;
+  g4::GroupParams gp;
+  memset(&gp, 0, sizeof(gp));
+  g4::Params& q = gp.g[0];
+  fill(q, a);
+  q.a_bytes = (uint32_t)((int64_t)(a->M - 1) * a->lda + a->K);
+  q.b_bytes = (uint32_t)((int64_t)(a->N - 1) * a->ldb + a->K);
+  q.a_scale = a->a_scale;
+  q.b_scale = a->b_scale;
+  q.rope_bf16 = em == g4::EM_ROPE && (int64_t)a->rope_T * a->rope_dim * 4 > g4::ROPE_LDS;
+  gp.n = 1;
+  gp.tile_end[0] = q.tiles_m * q.tiles_n;
+  const dim3 grid(gp.tile_end[0] < G ? gp.tile_end[0] : G), block(g4::NT);
+  switch (em) {
+    case g4::EM_BF16: hipLaunchKernelGGL((g4::gemm4f8_kernel<g4::EM_BF16>), grid, block, 0, st, gp); break;
+    case g4::EM_RELU_DROP: hipLaunchKernelGGL((g4::gemm4f8_kernel<g4::EM_RELU_DROP>), grid, block, 0, st, gp); break;
+    case g4::EM_ROPE: hipLaunchKernelGGL((g4::gemm4f8_kernel<g4::EM_ROPE>), grid, block, 0, st, gp); break;
+    default: hipLaunchKernelGGL((g4::gemm4f8_kernel<g4::EM_DRELU>), grid, block, 0, st, gp); break;
+  }
+  NSTL_LAUNCH_CHECK("nstl_gemm (fp8, 4-wave persistent)");
+  nstl::count(NSTL_K_GEMM_FP8);  // every fp8 launch, either kernel
+  nstl::count(NSTL_K_GEMM4F8);
+  if (em == g4::EM_ROPE) nstl::count(NSTL_K_GEMM_FP8_ROPE);
+  nstl::count(NSTL_K_GEMM4_TILES, gp.tile_end[0]);
+  *handled = 1;
+  return 0;
+}
 
 // One problem: *handled = 1 when the 4-wave kernel took it.
 int gemm4(const nstl_gemm_args* a, hipStream_t st, int* handled) {

@@ -436,3 +436,90 @@ def test_fp8_backward_gradients_near_bf16_step():
     n8 = torch.sqrt(sum((v ** 2).sum() for v in g8.values())).item()
     n16 = torch.sqrt(sum((v ** 2).sum() for v in g16.values())).item()
     assert abs(n8 - n16) < 0.02 * n16, (n8, n16)
+
+
+# ---------------------------------------------------------------------------
+# the 4-wave persistent fp8 kernel (csrc/gemm4.h gemm4f8_kernel:
+# v_mfma_scale_f32_16x16x128_f8f6f4, the bf16 kernel's 16 x 16 accumulator
+# layout and epilogues with the row / column scales applied first) on full
+# 256^2 tiles, K a multiple of 256 (>= 512); NSTL_GEMM4_F8=0 (read per call)
+# selects the 8-wave fp8 ring kernel for comparison.
+def _rope_ref(z, M, T, dh, cols, cs, sn):
+    t = torch.arange(M) % T
+    c64, s64 = cs.double().cpu()[t], sn.double().cpu()[t]
+    r = z.clone()
+    x = r[:, :cols].view(M, cols // dh, dh // 2, 2)
+    x0, x1 = x[..., 0].clone(), x[..., 1].clone()
+    x[..., 0] = x0 * c64[:, None, :] - x1 * s64[:, None, :]
+    x[..., 1] = x0 * s64[:, None, :] + x1 * c64[:, None, :]
+    return r
+
+
+@pytest.mark.parametrize("epi,M,N,K_", [("bias", 2048, 1024, 1024), ("bias", 4096, 3072, 512),
+                                         ("relu", 2048, 4096, 1024), ("rope128", 4096, 3072, 1024),
+                                         ("rope256", 4096, 2048, 1024), ("drelu", 2048, 4096, 1024)])
+def test_fp8_gemm4_epilogues_vs_f64_and_ring(monkeypatch, epi, M, N, K_):
+    """Each epilogue of the fp8 4-wave kernel against float64 of the same e4m3
+    operands and scales (bf16 output: 1e-2 of max|C|), and against the fp8 ring
+    kernel (outputs within a bf16 step in rare elements: the two accumulate the
+    128-byte blocks in different MFMA shapes).  rope256 is C5's T = 256 table,
+    held in LDS as bf16 (f32 does not fit): rotation within 1e-2.  The keep bits
+    of the ReLU-dropout epilogue and the dReLU column sums are compared with the
+    ring kernel's."""
+    qa, sa, qb, sb = fp8_operands(M, N, K_, M + N + K_)
+    ref = fp8_ref.gemm(qa.cpu(), sa.cpu(), qb.cpu(), sb.cpu())
+    bias = rnd(N, seed=3, scale=0.1).to(DEV)
+    kw = dict(a_scale=sa, b_scale=sb)
+    extra_ref = None
+    if epi == "bias":
+        kw.update(epilogue=K.EPI_BIAS, bias=bias)
+        want = ref + bias.double().cpu()
+    elif epi == "relu":
+        kw.update(epilogue=K.EPI_BIAS_RELU_DROP, bias=bias, p_drop=0.0)
+        want = (ref + bias.double().cpu()).clamp_min(0)
+    elif epi.startswith("rope"):
+        T = int(epi[4:])
+        cs, sn = rotation_tables(T, 64, DEV)
+        kw.update(epilogue=K.EPI_BIAS_ROPE, bias=bias, rope=(cs, sn, T, 64), rope_cols=N // 2)
+        want = _rope_ref(ref + bias.double().cpu(), M, T, 64, N // 2, cs, sn)
+    else:  # drelu: keep bits from an fp8 forward of the same output shape
+        X1, W1 = rnd(M, 512, dtype=torch.bfloat16, seed=5).to(DEV), rnd(N, 512, dtype=torch.bfloat16, seed=6).to(DEV)
+        qx, sx = quant_gpu(X1)
+        qw, sw = quant_gpu(W1)
+        h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        fw = dict(a_scale=sx, b_scale=sw, epilogue=K.EPI_BIAS_RELU_DROP, bias=bias, p_drop=0.3, seed=11)
+        mask = torch.zeros(K.gemm_relu_mask_words(qx, qw, h, M, N, 512, **fw), dtype=torch.int64, device=DEV)
+        K.gemm(qx, qw, h, M, N, 512, relu_mask=mask, **fw)
+        kw.update(epilogue=K.EPI_DRELU_DROP, aux=h, ld_aux=N, p_drop=0.3, relu_mask=mask)
+        want = ref * (h.double().cpu() > 0) / 0.7
+        extra_ref = h
+
+    def run(arm):
+        monkeypatch.setenv("NSTL_GEMM4_F8", arm)
+        c = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        extra = {}
+        if epi == "relu":
+            extra["relu_mask"] = torch.full((K.gemm_relu_mask_words(qa, qb, c, M, N, K_, **kw),), -1,
+                                            dtype=torch.int64, device=DEV)
+        if epi == "drelu":
+            extra["colsum_part"] = torch.full((K.gemm_colsum_rows(qa, qb, c, M, N, K_, **kw), N), float("nan"),
+                                              device=DEV)
+        K.kernel_counts_reset()
+        K.gemm(qa, qb, c, M, N, K_, **kw, **extra)
+        torch.cuda.synchronize()
+        return c, extra, K.kernel_counts()
+
+    (c4, e4, n4), (cr, er, nr) = run("1"), run("0")
+    monkeypatch.delenv("NSTL_GEMM4_F8")
+    assert n4["gemm4_fp8"] == 1 and n4["gemm_fp8"] == 1, n4
+    assert nr["gemm4_fp8"] == 0 and nr["gemm_fp8"] == 1, nr
+    close(c4, want, 1e-2, "fp8 gemm4 " + epi)
+    d = (c4.float() - cr.float()).abs()
+    assert d.max().item() <= 2 ** -6 * cr.float().abs().max().item(), epi
+    if epi == "relu":
+        flips = torch.bitwise_xor(e4["relu_mask"], er["relu_mask"])
+        nbits = sum(bin(int(x) & (2 ** 64 - 1)).count("1") for x in flips[flips != 0].tolist())
+        assert nbits <= 1e-4 * 64 * flips.numel(), nbits
+    if epi == "drelu":
+        close(e4["colsum_part"].sum(0), c4.double().sum(0), 1e-4, "fp8 gemm4 dReLU column sums")
+        assert extra_ref is not None
