@@ -964,9 +964,16 @@ __global__ __launch_bounds__(BWD_NT) void attn_bwd_dkv_kernel(AttnParams p) {
 //   phase 2 : barrier; dS^T -> image; barrier; dQ = dS K
 //   stores  : barrier; dQ, dK, dV rows (+ bias column sums, last wave out)
 constexpr int FUSED_MAX_T = 128;
-// LDS map after phase 2: staging [0, 16 KB), bias partials [16 KB, 22 KB), RoPE
-// tables [22 KB, 58 KB) over the dead K image / lse / D, then the counter
-constexpr int FUSED_ROPE_OFF = 8 * 16 * DH * 2 + 3 * 8 * 64 * 4;
+// Output staging of one wave (store_tile16x64_buf): its 16 rows in four groups of
+// 4 rows (lane group g's rows 4g + r), each group padded by 32 bytes.  With
+// 128-byte rows and no padding the four lane groups' 2-byte writes land on the
+// same 8 banks (4-way conflicts on every element write: the fused backward's
+// largest remaining conflict term); the 32-byte pad puts group g on banks
+// 8g .. 8g + 7, and the address stays one per-lane base + immediate offsets.
+constexpr int FUSED_SCR_G = 4 * DH * 2 + 32, FUSED_SCR = 4 * FUSED_SCR_G;
+// LDS map after phase 2: staging [0, 17 KB), bias partials [17 KB, 23 KB), RoPE
+// tables [23 KB, 59 KB) over the dead K image / lse / D, then the counter
+constexpr int FUSED_ROPE_OFF = 8 * FUSED_SCR + 3 * 8 * 64 * 4;
 constexpr int FUSED_RS = DH / 2 + 4;  // padded table row (floats): 144 B, 16-byte aligned
 constexpr int FUSED_ARRIVED_OFF = FUSED_ROPE_OFF + 2 * FUSED_MAX_T * FUSED_RS * 4;
 constexpr int FUSED_DS_RB = FUSED_MAX_T * 2;  // dS^T image row: 128 queries (bf16)
@@ -1003,7 +1010,8 @@ NSTL_DEV void dma_rows_buf(char* img, __amdgpu_buffer_rsrc_t r, uint32_t ld_byte
 }
 typedef int i32x4b __attribute__((ext_vector_type(4)));
 // store_tile16x64<bf16> into a head buffer (head_rsrc of the output), the tile's
-// first row at byte offset off0: 32-bit offsets instead of 64-bit addresses
+// first row at byte offset off0: 32-bit offsets instead of 64-bit addresses.  The
+// wave's staging image is FUSED_SCR bytes, rows grouped by 4 with a 32-byte pad.
 NSTL_DEV void store_tile16x64_buf(const float (&v)[4][4], char* scr, __amdgpu_buffer_rsrc_t r, uint32_t off0,
                                   uint32_t ld_bytes, int lane) {
   constexpr int RB = DH * 2, CPR = RB / 16;
@@ -1011,12 +1019,13 @@ NSTL_DEV void store_tile16x64_buf(const float (&v)[4][4], char* scr, __amdgpu_bu
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) *(bf16*)(scr + (4 * g + rr) * RB + (dt * 16 + (lane & 15)) * 2) = (bf16)v[dt][rr];
+    for (int dt = 0; dt < 4; ++dt)
+      *(bf16*)(scr + g * FUSED_SCR_G + rr * RB + (dt * 16 + (lane & 15)) * 2) = (bf16)v[dt][rr];
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int c = lane; c < 16 * CPR; c += 64) {
     const int row = c / CPR, ch = c % CPR;
-    __builtin_amdgcn_raw_buffer_store_b128(*(const i32x4b*)(scr + row * RB + ch * 16), r,
+    __builtin_amdgcn_raw_buffer_store_b128(*(const i32x4b*)(scr + (row >> 2) * FUSED_SCR_G + (row & 3) * RB + ch * 16), r,
                                            off0 + (uint32_t)row * ld_bytes + ch * 16, 0, 0);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1055,8 +1064,8 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
   char* Kimg = smem + 2 * FUSED_MAX_T * RBK;                   // [128][128 B]
   float* lse_s = (float*)(Kimg + FUSED_MAX_T * RBK);
   float* d_s = lse_s + FUSED_MAX_T;
-  char* scratch = smem;                                        // after phase 2: [NW][16][RBK]
-  float* red = (float*)(smem + NW * 16 * RBK);                 // after phase 2: [3][NW][64]
+  char* scratch = smem;                                        // after phase 2: [NW][FUSED_SCR]
+  float* red = (float*)(smem + NW * FUSED_SCR);                // after phase 2: [3][NW][64]
   float* cos_s = (float*)(smem + FUSED_ROPE_OFF);              // after phase 2: RoPE tables [T][DH/2] x 2
   float* sin_s = cos_s + T_ * FUSED_RS;
   unsigned* arrived = (unsigned*)(smem + FUSED_ARRIVED_OFF);
@@ -1242,7 +1251,7 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
       if (p.rope_q) rope_apply(vq, tc, ts);
       if (p.rope_k) rope_apply(vk, tc, ts);
     }
-    char* scr = scratch + w * 16 * RBK;
+    char* scr = scratch + w * FUSED_SCR;
     store_tile16x64_buf(vq, scr, head_rsrc(p.dq, p.dq_ld, tok0, h, T_), (uint32_t)k0 * p.dq_ld * 2, p.dq_ld * 2, lane);
     store_tile16x64_buf(vk, scr, head_rsrc(p.dk, p.dk_ld, tok0, h, T_), (uint32_t)k0 * p.dk_ld * 2, p.dk_ld * 2, lane);
     store_tile16x64_buf(vv, scr, head_rsrc(p.dv, p.dv_ld, tok0, h, T_), (uint32_t)k0 * p.dv_ld * 2, p.dv_ld * 2, lane);
@@ -1266,7 +1275,8 @@ __global__ __launch_bounds__(BWD_NT, 4) void attn_bwd_fused_kernel(AttnParams p)
 constexpr size_t FUSED_LDS = FUSED_ARRIVED_OFF + 16;  // 58 KB: two workgroups per CU
 static_assert(FUSED_ARRIVED_OFF >= 3 * FUSED_MAX_T * DH * 2 + 2 * FUSED_MAX_T * 4, "counter past the images");
 static_assert(FUSED_ROPE_OFF % 16 == 0, "16-byte table chunks");
-static_assert(8 * 16 * DH * 2 + 3 * 8 * 64 * 4 <= 3 * FUSED_MAX_T * DH * 2, "staging must fit in the images");
+static_assert(8 * FUSED_SCR + 3 * 8 * 64 * 4 <= 3 * FUSED_MAX_T * DH * 2, "staging must fit in the images");
+static_assert(BWD_NT / 64 == 8, "the staging map assumes 8 waves");
 
 
 size_t fwd_lds_bytes(int T, int esz) {  // K, V images (the output leaves from registers)

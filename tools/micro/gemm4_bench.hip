@@ -214,6 +214,48 @@ int r3_ab(const bf16* A, const bf16* B, bf16* C, float* Cf, hipStream_t st) {
   return 0;
 }
 
+// G4_STORE_AB=1: the bf16 epilogue with and without its global stores (DBG 8192,
+// timing only): how much of a multi-tile K = 1024 launch the output drain costs
+int store_ab(const bf16* A, const bf16* B, bf16* C, hipStream_t st) {
+  struct Case { const char* name; int M, N, K; int kind; };  // kind 0 TT, 1 TN
+  const Case cs[] = {{"fwd out  16384x1024x1024", 16384, 1024, 1024, 0},
+                     {"fwd qkv  16384x3072x1024", 16384, 3072, 1024, 0},
+                     {"fwd ffn1 16384x4096x1024", 16384, 4096, 1024, 0},
+                     {"dX  ffn2 16384x4096x1024", 16384, 4096, 1024, 1},
+                     {"fwd ffn2 16384x1024x4096", 16384, 1024, 4096, 0}};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  typedef void (*F)(const g4::GroupParams&, hipStream_t);
+  const F fs[2][2] = {{launch_any<true, true, g4::EM_BF16, 0>, launch_any<true, true, g4::EM_BF16, 8192>},
+                      {launch_any<true, false, g4::EM_BF16, 0>, launch_any<true, false, g4::EM_BF16, 8192>}};
+  for (int round = 0; round < 4; ++round)
+    for (const Case& c : cs) {
+      g4::GroupParams gp{};
+      g4::Params& p = gp.g[0];
+      p.M = c.M; p.N = c.N; p.K = c.K; p.alpha = 1.f;
+      p.A = (const char*)A; p.lda = c.K; p.B = (const char*)B; p.ldb = c.kind == 0 ? c.K : c.N; p.C = (char*)C; p.ldc = c.N;
+      p.a_bytes = (uint32_t)((int64_t)c.M * c.K * 2); p.b_bytes = (uint32_t)((int64_t)c.N * c.K * 2);
+      p.tiles_m = c.M / 256; p.tiles_n = c.N / 256;
+      gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
+      for (int arm = 0; arm < 2; ++arm) {
+        const F f = fs[c.kind][arm];
+        for (int w = 0; w < 3; ++w) f(gp, st);
+        std::vector<float> ts;
+        for (int r = 0; r < 15; ++r) {
+          CK(hipEventRecord(e0, st)); f(gp, st); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+          float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        const double us = ts[7] * 1e3, fl = 2.0 * c.M * c.N * c.K;
+        if (round > 0)
+          printf("round %d  %s  %-9s %8.1f us  %7.1f TF/s\n", round, c.name, arm == 0 ? "stores" : "no stores", us, fl / us * 1e-6);
+        fflush(stdout);
+      }
+    }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   struct Shape { const char* name; int M, N, K, bkm; };
   const Shape shapes[] = {
@@ -243,6 +285,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&Cf, 4096LL * 4096 * 4));
     return r3_ab(A, B, C, Cf, st);
   }
+  if (getenv("G4_STORE_AB")) return store_ab(A, B, C, st);
   if (getenv("G4_DMA_AB")) {
     float* Cf;
     CK(hipMalloc(&Cf, 4096LL * 4096 * 4));
