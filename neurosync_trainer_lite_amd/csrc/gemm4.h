@@ -1213,7 +1213,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
     }
     G4_LGKM0();  // the next tile's last B fragment: before the epilogue's own LDS reads
     lt = sg.t < T ? xcd_remap(sg.t, T) : sg.t;
-    epilogue<EM, true>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, true);
+    epilogue<EM, true, (DBG & 8192) ? 1 : 0>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, true);
     if (!has_next) break;
     if constexpr (EM != EM_BF16) {
       // the per-lane DMA offsets and read addresses, recomputed after every

@@ -256,6 +256,80 @@ int store_ab(const bf16* A, const bf16* B, bf16* C, hipStream_t st) {
   return 0;
 }
 
+// G4_F8_ABL=1: the fp8 4-wave kernel (gemm4f8_kernel, bf16 out, unit scales) on the
+// step's K-major shapes, with ablations (timing only: results are wrong), beside the
+// bf16 kernel on the same shape; arms alternated after a warm-up round
+__global__ void fill_f8(uint8_t* x, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    const float v = ((float)(h & 0xFFFF) / 65536.f - 0.5f) * 200.f;  // |v| < 100: inside e4m3's range
+    x[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, v, 0, false) & 0xFF);
+  }
+}
+__global__ void fill_one(float* x, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[i] = 1.f;
+}
+template <int DBG>
+void launch_f8(const g4::GroupParams& gp, hipStream_t st) {
+  hipLaunchKernelGGL((g4::gemm4f8_kernel<g4::EM_BF16, DBG>), dim3(std::min(256, gp.tile_end[0])), dim3(g4::NT), 0, st, gp);
+}
+int f8_abl(const bf16* A, const bf16* B, bf16* C, hipStream_t st) {
+  struct Case { const char* name; int M, N, K; };
+  const Case cs[] = {{"fwd out  16384x1024x1024", 16384, 1024, 1024},
+                     {"fwd qkv  16384x3072x1024", 16384, 3072, 1024},
+                     {"fwd ffn1 16384x4096x1024", 16384, 4096, 1024},
+                     {"fwd ffn2 16384x1024x4096", 16384, 1024, 4096},
+                     {"sq 4096x4096 K=8192     ", 4096, 4096, 8192}};
+  uint8_t *A8, *B8;
+  float* ones;
+  CK(hipMalloc(&A8, 16384LL * 8192));
+  CK(hipMalloc(&B8, 16384LL * 8192));
+  CK(hipMalloc(&ones, 16384 * 4));
+  hipLaunchKernelGGL(fill_f8, dim3(4096), dim3(256), 0, st, A8, 16384LL * 8192, 3u);
+  hipLaunchKernelGGL(fill_f8, dim3(4096), dim3(256), 0, st, B8, 16384LL * 8192, 4u);
+  hipLaunchKernelGGL(fill_one, dim3(64), dim3(256), 0, st, ones, 16384);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  typedef void (*F)(const g4::GroupParams&, hipStream_t);
+  const int dbgs[7] = {-1, 0, 8192, 1, 2, 3, 8};
+  const char* names[7] = {"bf16 gemm4", "fp8", "fp8 no stores", "fp8 no DMA", "fp8 no reads", "fp8 MFMA only", "fp8 no MFMA"};
+  const F fs[7] = {launch_any<true, true, g4::EM_BF16, 0>, launch_f8<0>, launch_f8<8192>, launch_f8<1>, launch_f8<2>,
+                   launch_f8<3>, launch_f8<8>};
+  for (int round = 0; round < 3; ++round)
+    for (const Case& c : cs) {
+      for (int arm = 0; arm < 7; ++arm) {
+        g4::GroupParams gp{};
+        g4::Params& p = gp.g[0];
+        p.M = c.M; p.N = c.N; p.K = c.K; p.alpha = 1.f; p.C = (char*)C; p.ldc = c.N;
+        if (dbgs[arm] < 0) {
+          p.A = (const char*)A; p.lda = c.K; p.B = (const char*)B; p.ldb = c.K;
+          p.a_bytes = (uint32_t)((int64_t)c.M * c.K * 2); p.b_bytes = (uint32_t)((int64_t)c.N * c.K * 2);
+        } else {
+          p.A = (const char*)A8; p.lda = c.K; p.B = (const char*)B8; p.ldb = c.K;
+          p.a_bytes = (uint32_t)((int64_t)c.M * c.K); p.b_bytes = (uint32_t)((int64_t)c.N * c.K);
+          p.a_scale = ones; p.b_scale = ones;
+        }
+        p.tiles_m = c.M / 256; p.tiles_n = c.N / 256;
+        gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
+        const F f = fs[arm];
+        for (int w = 0; w < 3; ++w) f(gp, st);
+        std::vector<float> ts;
+        for (int r = 0; r < 15; ++r) {
+          CK(hipEventRecord(e0, st)); f(gp, st); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+          float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        const double us = ts[7] * 1e3, fl = 2.0 * c.M * c.N * c.K;
+        if (round > 0)
+          printf("round %d  %s  %-14s %8.1f us  %7.1f TF/s\n", round, c.name, names[arm], us, fl / us * 1e-6);
+        fflush(stdout);
+      }
+    }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   struct Shape { const char* name; int M, N, K, bkm; };
   const Shape shapes[] = {
@@ -286,6 +360,7 @@ int main(int argc, char** argv) {
     return r3_ab(A, B, C, Cf, st);
   }
   if (getenv("G4_STORE_AB")) return store_ab(A, B, C, st);
+  if (getenv("G4_F8_ABL")) return f8_abl(A, B, C, st);
   if (getenv("G4_DMA_AB")) {
     float* Cf;
     CK(hipMalloc(&Cf, 4096LL * 4096 * 4));
