@@ -324,9 +324,42 @@ NSTL_DEV void tile_coords(int id, int nt_m, int nt_n, int& m0, int& n0) {
   n0 = (in_g / gm) * TILE;
 }
 
+// (lo, hi) -> two bf16 (round to nearest even) in one word: ONE v_cvt_pk_bf16_f32
+// (two scalar casts cost two conversions, a shift and an SDWA or per pair: a
+// third of the plain epilogue's vector instructions)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 NSTL_DEV uint32_t pack_bf16x2(float lo, float hi) {
-  const bf16 a = (bf16)lo, b = (bf16)hi;
-  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+}
+// the two bf16 of a packed word back to f32 (exact)
+NSTL_DEV float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+NSTL_DEV float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+// dropout keep masks of an element pair from its hash: all ones where the 16-bit
+// uniform is >= thresh (thresh in 1 .. 65536), else 0 -- the compare of
+// nstl_keep2_32 as integer arithmetic, so the select is an AND (a compare writes
+// VCC, and every VCC-reading select behind it costs a hazard s_nop)
+// (the shift and the min below are asm: written in C the compiler turns them back
+// into a compare and a select)
+NSTL_DEV uint32_t asr31(uint32_t x) {
+  uint32_t r;
+  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+NSTL_DEV uint32_t min1(uint32_t x) {
+  uint32_t r;
+  asm("v_min_u32 %0, 1, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+NSTL_DEV uint32_t keep_lo_mask(uint32_t h, uint32_t thresh) { return asr31(thresh - 1u - (h & 0xFFFFu)); }
+NSTL_DEV uint32_t keep_hi_mask(uint32_t h, uint32_t thresh) { return asr31(thresh - 1u - (h >> 16)); }
+NSTL_DEV float and_mask(float x, uint32_t m) { return __uint_as_float(__float_as_uint(x) & m); }
+// ReLU-mask bits of a packed pair of non-negative bf16 (after max(., 0)): bit 0
+// for the low element, bit 1 for the high one, set where the stored value is
+// not zero (+0 or -0) -- "(bf16)v > 0" for v >= 0
+NSTL_DEV uint32_t pos_bits2(uint32_t w) {
+  const uint32_t t = w & 0x7FFF7FFFu;
+  return min1(t & 0xFFFFu) | (min1(t >> 16) << 1);
 }
 
 // ReLU keep&positive bits in the ring kernel's word layout (gemm.hip
@@ -566,7 +599,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       p.sq_part[tile_id * 8 + 2 * wave + 1] = 0.f;
     }
   } else {
-    float bias[8][4];
+    f32x4 bias[8];
 #pragma unroll
     for (int b = 0; b < 8; ++b)
 #pragma unroll
@@ -652,8 +685,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
           } else {
             v = uv[s] * alpha;
           }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += bias[b][e];
+          v += bias[b];  // two v_pk_add_f32
           if constexpr (EM == EM_RELU_DROP) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -661,17 +693,10 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
               const uint32_t pair = (uint32_t)row * (uint32_t)(p.N >> 1) + (uint32_t)(col >> 1);
 #pragma unroll
               for (int e = 0; e < 4; e += 2) {
-                bool k0, k1;
-                nstl_keep2_32(seed_term, pair + (e >> 1), p.thresh, k0, k1);
-                v[e] = k0 ? v[e] * p.inv_keep : 0.f;
-                v[e + 1] = k1 ? v[e + 1] * p.inv_keep : 0.f;
+                const uint32_t h = nstl_pair_hash32(seed_term, pair + (e >> 1));
+                v[e] = and_mask(v[e] * p.inv_keep, keep_lo_mask(h, p.thresh));
+                v[e + 1] = and_mask(v[e + 1] * p.inv_keep, keep_hi_mask(h, p.thresh));
               }
-            }
-            if (rmask) {
-              uint32_t nib = 0;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) nib |= ((bf16)v[e] > (bf16)0.f ? 1u : 0u) << e;  // as stored
-              mbits[a >> 2][b] |= nib << (4 * (a & 3));
             }
           } else if constexpr (EM == EM_ROPE) {
             // products rounded before the add, as the reference's f32 elementwise
@@ -689,16 +714,26 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
           } else if constexpr (EM == EM_DRELU) {
             const uint32_t nib = mbits[a >> 2][b] >> (4 * (a & 3));
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = ((nib >> e) & 1) ? v[e] * p.inv_keep : 0.f;
-            if (p.colsum_part != nullptr) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) csum[b][e] += (float)(bf16)v[e];  // sum what is stored
-            }
+            for (int e = 0; e < 4; ++e) v[e] = and_mask(v[e] * p.inv_keep, asr31(nib << (31 - e)));
           }
           uv[s] = v;
         }
         const uint32_t x0 = pack_bf16x2(uv[0][0], uv[0][1]), x1 = pack_bf16x2(uv[0][2], uv[0][3]);
         const uint32_t y0 = pack_bf16x2(uv[1][0], uv[1][1]), y1 = pack_bf16x2(uv[1][2], uv[1][3]);
+        if constexpr (EM == EM_RELU_DROP) {
+          if (rmask) {  // keep&positive bits of what is stored
+            mbits[a >> 2][bp] |= (pos_bits2(x0) | (pos_bits2(x1) << 2)) << (4 * (a & 3));
+            mbits[a >> 2][bp + 1] |= (pos_bits2(y0) | (pos_bits2(y1) << 2)) << (4 * (a & 3));
+          }
+        }
+        if constexpr (EM == EM_DRELU) {
+          if (p.colsum_part != nullptr) {  // sum what is stored (the bf16 values, exactly)
+            csum[bp][0] += bf16_lo(x0); csum[bp][1] += bf16_hi(x0);
+            csum[bp][2] += bf16_lo(x1); csum[bp][3] += bf16_hi(x1);
+            csum[bp + 1][0] += bf16_lo(y0); csum[bp + 1][1] += bf16_hi(y0);
+            csum[bp + 1][2] += bf16_lo(y1); csum[bp + 1][3] += bf16_hi(y1);
+          }
+        }
         const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
         // EDBG & 1 (experiment: timing only): the stores skipped, the math kept
