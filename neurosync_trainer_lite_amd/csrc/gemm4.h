@@ -241,6 +241,12 @@ NSTL_DEV void dma_tile(Dma& d, const Params& p, int m0, int n0, int ks) {
   d.tb = __builtin_amdgcn_readfirstlane((BKM ? (uint32_t)(n0 * p.ldb * 2) : (uint32_t)(n0 * 2)) + k0 * d.b_kb);
 }
 
+// a tile's first MFMA on each block: C = 0 (an inline constant), so the epilogue
+// need not zero the accumulators it reads (256 v_accvgpr_write per tile and wave)
+NSTL_DEV void mma16z(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+}
+
 // every read slot of a half-step (slot 0, h = 0): the first tile's prologue
 template <bool AK, bool BKM, int R>
 NSTL_DEV void rd_all(bf16x8 (&fa)[8], bf16x8 (&fb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb) {
@@ -275,12 +281,15 @@ NSTL_DEV void rd_after(bf16x8 (&na)[8], bf16x8 (&nb)[8], const RdAddr<AK>& ra, c
     }
   }
 }
-template <bool AK, bool BKM, bool RD, int RSOA, int RSOB, int RH, int DMAM, int DBG, int I = 0>
+template <bool AK, bool BKM, bool RD, int RSOA, int RSOB, int RH, int DMAM, int DBG, bool Z = false, int I = 0>
 NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 (&cb)[8], bf16x8 (&na)[8],
                         bf16x8 (&nb)[8], const RdAddr<AK>& ra, const RdAddr<BKM>& rb, const Dma& d, char* adst,
                         char* bdst, uint32_t sa, uint32_t sb) {
   if constexpr (I < 64) {
-    if constexpr (!(DBG & 8)) mma16(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
+    if constexpr (!(DBG & 8)) {
+      if constexpr (Z) mma16z(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
+      else mma16(acc[I >> 3][I & 7], cb[I & 7], ca[I >> 3]);
+    }
     G4_SB();
     if constexpr (RD && !(DBG & 2))
       rd_after<AK, BKM, RSOA, RSOB, RH, I, 0, (DBG & 256) ? 56 : (DBG & 512) ? 32 : (DBG & 1024) ? 24 : 46>(na, nb, ra,
@@ -309,7 +318,7 @@ NSTL_DEV void half_step(f32x4 (&acc)[8][8], const bf16x8 (&ca)[8], const bf16x8 
       else dma16(d.rb, bdst + (q - 8) * 1024, d.vb[q - 8], d.tb + sb);
       G4_SB();
     }
-    half_step<AK, BKM, RD, RSOA, RSOB, RH, DMAM, DBG, I + 1>(acc, ca, cb, na, nb, ra, rb, d, adst, bdst, sa, sb);
+    half_step<AK, BKM, RD, RSOA, RSOB, RH, DMAM, DBG, Z, I + 1>(acc, ca, cb, na, nb, ra, rb, d, adst, bdst, sa, sb);
   }
 }
 
@@ -391,20 +400,33 @@ NSTL_DEV int rope_off8(int t, int chunk, int row_bytes, int swz) { return t * ro
 // compiler, the epilogue's VALU uses split the accumulators' live range at the
 // epilogue entry: all 256 are copied to VGPRs at once and the DMA offsets and
 // next fragments spill around them.
+// ZW: ... and zeroed in place for the next tile.  Kernels whose tiles start with
+// C = 0 MFMAs (mma16z: the dX / dW layouts and fp8) read without zeroing (256
+// fewer v_accvgpr_write per tile and wave); the K-major-B (forward) and stream-K
+// instantiations keep the zeroing: with C = 0 their register allocation spilled.
+template <bool ZW = true>
 NSTL_DEV f32x4 rd_acc(f32x4& x) {
-  // ... and zeroed in place for the next tile (an MFMA with C = 0 instead would
-  // give the first step's results new registers: copies and spills)
   float r0, r1, r2, r3;
-  asm volatile(
-      "v_accvgpr_read_b32 %0, %4\n\t"
-      "v_accvgpr_read_b32 %1, %5\n\t"
-      "v_accvgpr_read_b32 %2, %6\n\t"
-      "v_accvgpr_read_b32 %3, %7\n\t"
-      "v_accvgpr_write_b32 %4, 0\n\t"
-      "v_accvgpr_write_b32 %5, 0\n\t"
-      "v_accvgpr_write_b32 %6, 0\n\t"
-      "v_accvgpr_write_b32 %7, 0"
-      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "+a"(x[0]), "+a"(x[1]), "+a"(x[2]), "+a"(x[3]));
+  if constexpr (ZW) {
+    asm volatile(
+        "v_accvgpr_read_b32 %0, %4\n\t"
+        "v_accvgpr_read_b32 %1, %5\n\t"
+        "v_accvgpr_read_b32 %2, %6\n\t"
+        "v_accvgpr_read_b32 %3, %7\n\t"
+        "v_accvgpr_write_b32 %4, 0\n\t"
+        "v_accvgpr_write_b32 %5, 0\n\t"
+        "v_accvgpr_write_b32 %6, 0\n\t"
+        "v_accvgpr_write_b32 %7, 0"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "+a"(x[0]), "+a"(x[1]), "+a"(x[2]), "+a"(x[3]));
+  } else {
+    asm volatile(
+        "v_accvgpr_read_b32 %0, %4\n\t"
+        "v_accvgpr_read_b32 %1, %5\n\t"
+        "v_accvgpr_read_b32 %2, %6\n\t"
+        "v_accvgpr_read_b32 %3, %7"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+        : "a"(x[0]), "a"(x[1]), "a"(x[2]), "a"(x[3]));
+  }
   return (f32x4){r0, r1, r2, r3};
 }
 
@@ -550,7 +572,7 @@ NSTL_DEV bool sk_handoff(const StreamK& sk, f32x4 (&acc)[8][8], const Seg& s, in
 // loaded first (bias, dReLU mask words) or read from LDS (RoPE tables).
 // SC (the fp8 kernel): C = a_scale[row] b_scale[col] acc, applied as (acc (a_scale
 // alpha)) b_scale -- the fp8 ring kernel's order -- before the bias.
-template <int EM, bool SC = false, int EDBG = 0>
+template <int EM, bool SC = false, int EDBG = 0, bool ZW = true>
 NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, int lane, int wave, int tile_id,
                        const char* rope_lds, bool fin = true) {
   const int g = lane >> 4, c = lane & 15, odd = g & 1;
@@ -579,11 +601,11 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       for (int b = 0; b < 8; ++b) {
         f32x4 v;
         if constexpr (SC) {
-          v = rd_acc(acc[a][b]) * rsc[a];
+          v = rd_acc<ZW>(acc[a][b]) * rsc[a];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] *= csc[b][e];
         } else {
-          v = rd_acc(acc[a][b]) * alpha;
+          v = rd_acc<ZW>(acc[a][b]) * alpha;
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) ssq += v[e] * v[e];
@@ -668,7 +690,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       }
 #pragma unroll
       for (int bp = 0; bp < 8; bp += 2) {
-        f32x4 uv[2] = {rd_acc(acc[a][bp]), rd_acc(acc[a][bp + 1])};
+        f32x4 uv[2] = {rd_acc<ZW>(acc[a][bp]), rd_acc<ZW>(acc[a][bp + 1])};
         if (!fin) {  // a stream-K first contributor: only the zeroing reads above
           G4_SB();
           continue;
@@ -812,6 +834,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   static_assert(!(R3 && EM == EM_ROPE), "the 3 + 2 ring fills the LDS: no room for the RoPE table");
   constexpr int SMEM_ALL = R3 ? 5 * OPS : SMEM + (EM == EM_ROPE ? ROPE_LDS : 0);
   constexpr int B_BASE = A3 ? 3 * OPS : 2 * OPS;  // B's slot 0
+  constexpr bool ZC = !BKM && !SK;                 // tiles start with C = 0 MFMAs (rd_acc)
   __shared__ __attribute__((aligned(16))) char smem[SMEM_ALL];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -932,8 +955,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
       const int s3_dma = s3_cur == 0 ? 2 : s3_cur - 1;
       const int s3_next = s3_cur == 2 ? 0 : s3_cur + 1;
       const uint32_t oa = dma_stage * dd.a_kb, ob = dma_stage * dd.b_kb;
-      half_step<AK, BKM, true, A3 ? 0 : S * OPS, B3 ? 0 : S * OPS, 1, 0, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, dd,
-                                                                           adst0, bdst0, 0, 0);
+      half_step<AK, BKM, true, A3 ? 0 : S * OPS, B3 ? 0 : S * OPS, 1, 0, DBG, ZC>(acc, f0a, f0b, f1a, f1b, ra, rb,
+                                                                               dd, adst0, bdst0, 0, 0);
       G4_LGKM0();
       if constexpr (WAITN == 32) G4_VMCNT(32);
       else G4_VMCNT(63);
@@ -950,7 +973,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
       const int s3_next = s3_cur == 2 ? 0 : s3_cur + 1;
       const uint32_t oa = dma_stage * dd.a_kb, ob = dma_stage * dd.b_kb;
       // h = 0: the three-ring operand's 8 pieces of stage dma_stage
-      half_step<AK, BKM, true, A3 ? 0 : S * OPS, B3 ? 0 : S * OPS, 1, A3 ? 2 : 3, DBG>(
+      half_step<AK, BKM, true, A3 ? 0 : S * OPS, B3 ? 0 : S * OPS, 1, A3 ? 2 : 3, DBG, ZC && WAITN != 0>(
           acc, f0a, f0b, f1a, f1b, ra, rb, dd, adst0 + s3_dma * OPS, bdst0 + s3_dma * OPS, oa, ob);
       G4_LGKM0();
       if constexpr (WAITN == 0) G4_VMCNT(8);
@@ -965,7 +988,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
       G4_LGKM0();
       s3_cur = s3_next;
     } else {
-      half_step<AK, BKM, true, S * OPS, S * OPS, 1, 0, DBG>(acc, f0a, f0b, f1a, f1b, ra, rb, dd, adst0, bdst0, 0, 0);
+      half_step<AK, BKM, true, S * OPS, S * OPS, 1, 0, DBG, ZC && WAITN != 0>(acc, f0a, f0b, f1a, f1b, ra, rb, dd,
+                                                                              adst0, bdst0, 0, 0);
       G4_LGKM0();
       if constexpr (WAITN == 0) G4_VMCNT(0);
       else if constexpr (WAITN == 32) G4_VMCNT(32);
@@ -1013,7 +1037,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     }
     bool fin = true;
     if constexpr (SK) fin = sk_handoff(gp.sk, acc, sg, wk.rank, wave, lane);
-    epilogue<EM, false, (DBG & 8192) ? 1 : 0>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, fin);
+    epilogue<EM, false, (DBG & 8192) ? 1 : 0, !ZC>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, fin);
     if (!has_next) break;
     sg = ns;
     prob = nprob;
@@ -1050,6 +1074,10 @@ typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
 NSTL_DEV void mma_f8(f32x4& acc, const i32x8_t& w, const i32x8_t& x) {
   acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w, x, acc, 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+}
+NSTL_DEV void mma_f8z(f32x4& acc, const i32x8_t& w, const i32x8_t& x) {  // a tile's first step: C = 0
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w, x, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0, 0x7f7f7f7f, 0,
+                                                          0x7f7f7f7f);
 }
 
 // per-lane DMA sources of one operand's stage (K-major, 128-byte rows of bytes)
@@ -1098,7 +1126,7 @@ NSTL_DEV void rd_f8(i32x8_t& f, const RdAddrF8& r) {
 // (the last, block 7, after the final MFMA: the next h = 0 uses it first at
 // MFMA 28 and waits for it there).  DMA (h = 1): the 16 pieces after MFMAs 1, 3,
 // ..., 31.  H = 2: h = 1 without any read.
-template <int H, int SO, int DBG, int I = 0>
+template <int H, int SO, int DBG, bool Z = false, int I = 0>
 NSTL_DEV void half_step_f8(f32x4 (&acc)[8][8], const i32x8_t (&ca)[4], i32x8_t (&cb)[8], i32x8_t (&na)[4],
                            const RdAddrF8& ra, const RdAddrF8& rb, const Dma& d, char* adst, char* bdst, uint32_t sa,
                            uint32_t sb) {
@@ -1110,7 +1138,10 @@ NSTL_DEV void half_step_f8(f32x4 (&acc)[8][8], const i32x8_t (&ca)[4], i32x8_t (
       asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
       G4_SB();
     }
-    if constexpr (!(DBG & 8)) mma_f8(acc[4 * (H ? 1 : 0) + a][b], cb[b], ca[a]);
+    if constexpr (!(DBG & 8)) {
+      if constexpr (Z) mma_f8z(acc[4 * (H ? 1 : 0) + a][b], cb[b], ca[a]);
+      else mma_f8(acc[4 * (H ? 1 : 0) + a][b], cb[b], ca[a]);
+    }
     G4_SB();
     if constexpr (!(DBG & 2)) {
       if constexpr (H == 0 && (I == 1 || I == 6 || I == 11 || I == 16)) {
@@ -1133,7 +1164,7 @@ NSTL_DEV void half_step_f8(f32x4 (&acc)[8][8], const i32x8_t (&ca)[4], i32x8_t (
       else dma16(d.rb, bdst + (q - 8) * 1024, d.vb[q - 8], d.tb + sb);
       G4_SB();
     }
-    half_step_f8<H, SO, DBG, I + 1>(acc, ca, cb, na, ra, rb, d, adst, bdst, sa, sb);
+    half_step_f8<H, SO, DBG, Z, I + 1>(acc, ca, cb, na, ra, rb, d, adst, bdst, sa, sb);
   }
 }
 
@@ -1214,15 +1245,15 @@ __global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
   auto step = [&](auto slot_c, auto waitn_c, uint32_t dma_stage) {
     constexpr int S = decltype(slot_c)::value;
     constexpr int WAITN = decltype(waitn_c)::value;
-    half_step_f8<0, S * OPS, DBG>(acc, fa0, fb, fa1, ra, rb, d, adst0, bdst0, 0, 0);
+    half_step_f8<0, S * OPS, DBG, WAITN != 0>(acc, fa0, fb, fa1, ra, rb, d, adst0, bdst0, 0, 0);
     G4_LGKM0();
     if constexpr (WAITN == 0) G4_VMCNT(0);
     else if constexpr (WAITN == 32) G4_VMCNT(32);
     else G4_VMCNT(63);
     __builtin_amdgcn_s_barrier();
     G4_SB();
-    half_step_f8<1, (1 - S) * OPS, DBG>(acc, fa1, fb, fa0, ra, rb, d, adst0 + S * OPS, bdst0 + S * OPS,
-                                        dma_stage * d.a_kb, dma_stage * d.b_kb);
+    half_step_f8<1, (1 - S) * OPS, DBG, WAITN != 0>(acc, fa1, fb, fa0, ra, rb, d, adst0 + S * OPS, bdst0 + S * OPS,
+                                                    dma_stage * d.a_kb, dma_stage * d.b_kb);
     asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
     G4_SB();
   };
@@ -1248,7 +1279,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
     }
     G4_LGKM0();  // the next tile's last B fragment: before the epilogue's own LDS reads
     lt = sg.t < T ? xcd_remap(sg.t, T) : sg.t;
-    epilogue<EM, true, (DBG & 8192) ? 1 : 0>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, true);
+    epilogue<EM, true, (DBG & 8192) ? 1 : 0, false>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds,
+                                                   true);
     if (!has_next) break;
     if constexpr (EM != EM_BF16) {
       // the per-lane DMA offsets and read addresses, recomputed after every
