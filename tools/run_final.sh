@@ -3,7 +3,7 @@
 #   tools/run_final.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-TAG=${1:-r4_final}
+TAG=${1:-r5_final}
 if [ "${2:-all}" != "prof" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.txt 2>&1 || { tail -30 gpurun_out/${TAG}_gpu_tests.txt; exit 1; }
 tail -2 gpurun_out/${TAG}_gpu_tests.txt
@@ -15,11 +15,5 @@ fi
 [ "${2:-all}" = "tests" ] && exit 0
 bash tools/run_prof_step.sh ${TAG}_prof > /dev/null 2>&1 || { echo "profile failed"; exit 1; }
 python tools/prof_summary.py gpurun_out/${TAG}_prof_kernel_stats.csv 23 16 2>/dev/null | head -30
-echo "--- C5 (T=256, B=64): bf16 / fp8 forward / fp8 forward + backward, alternating"
-C5="--seq 256 --batch 64 --steps 15 --warmup 3 --no-traffic --no-cpu-baseline --no-parity --feature-steps 0 --feed-steps 0"
-for rep in 1 2; do
-  for arm in "" "--fp8" "--fp8 --fp8-bwd"; do
-    timeout -k 10 300 python bench.py $C5 $arm > gpurun_out/${TAG}_c5.json 2>/dev/null || { echo "c5 $arm failed"; exit 1; }
-    python -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_c5.json')); print('c5 %-16s %.1f frames/s %.2f ms' % (sys.argv[1], d['value'], d['ms_per_step']))" "$arm" | tee -a gpurun_out/${TAG}_c5_ab.txt
-  done
-done
+echo "--- C5 (T=256, B=64): bf16 / fp8 forward + FFN2 dX (4-wave fp8 kernel) / the same on the fp8 ring kernel, alternating"
+bash tools/run_c5_ab.sh ${TAG} 2 || { echo "c5 failed"; exit 1; }
