@@ -1132,7 +1132,8 @@ class Seq2SeqEngine:
         self._main = torch.cuda.current_stream(self.device)
         self.st = self._main.cuda_stream
         if self.dw_stream_on and self._side is None:
-            self._side = torch.cuda.Stream(self.device)
+            from .parallel import side_stream
+            self._side = side_stream(self.device)
         self._side_reads = []
         self.p, self.base_seed = sv["p"], sv["seed"]
         self._dadd_pending = False

@@ -80,6 +80,37 @@ def init_from_env(backend=None):
 _CEDED = {}
 
 
+_ACTIVE_CEDE = {}  # device index -> k of the ceded compute stream (cede_cus)
+
+
+def _masked_stream(k, device):
+    """A new stream of `device` whose CU mask leaves out mask bits 0 .. k-1."""
+    import ctypes
+    from . import _hip
+    fn = ctypes.CDLL(_hip.LIB_PATH).hipExtStreamCreateWithCUMask
+    fn.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    n = torch.cuda.get_device_properties(device).multi_processor_count
+    words = (n + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in range(k, n):
+        mask[c // 32] |= 1 << (c % 32)
+    with torch.cuda.device(device):
+        st = ctypes.c_void_p()
+        if fn(ctypes.byref(st), words, mask) != 0:
+            raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+    return torch.cuda.ExternalStream(st.value, device=device)
+
+
+def side_stream(device):
+    """A second compute stream for `device` (the engine's weight-gradient stream,
+    the optimizer's update stream): with the CU mask of the ceded compute stream
+    when cede_cus is active there, so persistent grids launched on it size
+    themselves to the same CUs (nstl_stream_cus) and leave the ceded ones to the
+    collectives; otherwise a plain stream."""
+    k = _ACTIVE_CEDE.get(torch.device(device).index, 0)
+    return _masked_stream(k, device) if k > 0 else torch.cuda.Stream(device)
+
+
 def cede_cus(k, device):
     """Make the current stream of `device` a stream whose CU mask leaves out mask
     bits 0 .. k-1 -- bit i is a CU of XCD i % 8, shader engine (i / 8) % 4
@@ -89,24 +120,12 @@ def cede_cus(k, device):
     here); k <= 0 leaves the current stream."""
     if k <= 0:
         return torch.cuda.current_stream(device)
-    import ctypes
-    from . import _hip
     key = (torch.device(device).index, k)
     if key not in _CEDED:
-        fn = ctypes.CDLL(_hip.LIB_PATH).hipExtStreamCreateWithCUMask
-        fn.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
-        n = torch.cuda.get_device_properties(device).multi_processor_count
-        words = (n + 31) // 32
-        mask = (ctypes.c_uint32 * words)()
-        for c in range(k, n):
-            mask[c // 32] |= 1 << (c % 32)
-        with torch.cuda.device(device):
-            st = ctypes.c_void_p()
-            if fn(ctypes.byref(st), words, mask) != 0:
-                raise RuntimeError("hipExtStreamCreateWithCUMask failed")
-        _CEDED[key] = torch.cuda.ExternalStream(st.value, device=device)
+        _CEDED[key] = _masked_stream(k, device)
     s = _CEDED[key]
     torch.cuda.set_stream(s)
+    _ACTIVE_CEDE[key[0]] = k
     return s
 
 

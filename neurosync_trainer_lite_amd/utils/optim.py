@@ -160,7 +160,8 @@ class FusedAdam(torch.optim.Optimizer):
             else:
                 self.coef.fill_(1.0)
             if self._upd_stream is None:
-                self._upd_stream = torch.cuda.Stream(eng.device)
+                from ..parallel import side_stream
+                self._upd_stream = side_stream(eng.device)
             side = self._upd_stream
             side.wait_stream(main)
             a.sumsq_partial, a.n_partial, a.norm_out, a.coef = None, 0, None, self.coef.data_ptr()
