@@ -251,15 +251,18 @@ class GradShardReducer(GradAllReducer):
 class _DeviceTransport:
     """The receive buffers of a ShardPusher in device memory, shared between the
     ranks' processes through HIP IPC handles (nstl_ipc_*); pushes are copy-engine
-    copies (nstl_copy_engine: hipMemcpyDeviceToDeviceNoCU, no kernel) on a side
-    stream."""
+    copies (nstl_copy_engine: hipMemcpyDeviceToDeviceNoCU, no kernel), one side
+    stream per owner: xGMI is point to point, so the copies to different peers
+    travel different links and, on their own streams, different copy engines
+    (one stream would run a rank's 7/8 of the arena through one engine and one
+    link at a time)."""
 
     def __init__(self, grads, comm, n_slots):
         from . import _hip as K
         self.K = K
         self.shard = comm.shard
         self.recv = torch.empty(max(1, n_slots) * comm.shard, dtype=torch.float32, device=grads.device)
-        self.side = torch.cuda.Stream(grads.device)
+        self.sides = {r: torch.cuda.Stream(grads.device) for r in range(comm.world) if r != comm.rank}
         mine = K.ipc_handle(self.recv)
         allh = [None] * comm.world
         dist.all_gather_object(allh, mine, group=comm.group)
@@ -275,12 +278,15 @@ class _DeviceTransport:
         """src (a contiguous f32 slice of the arena) -> owner's receive slot `slot`
         at element offset `off`; ordered after the work queued on the current
         stream so far."""
-        self.side.wait_stream(torch.cuda.current_stream(src.device))
+        side = self.sides[owner]
+        side.wait_stream(torch.cuda.current_stream(src.device))
         dst = self.peer[owner] + (slot * self.shard + off) * 4
-        self.K.copy_engine(dst, src, src.numel() * 4, stream=self.side.cuda_stream)
+        self.K.copy_engine(dst, src, src.numel() * 4, stream=side.cuda_stream)
 
     def flush(self):
-        torch.cuda.current_stream(self.recv.device).wait_stream(self.side)
+        cur = torch.cuda.current_stream(self.recv.device)
+        for side in self.sides.values():
+            cur.wait_stream(side)
 
     def sync(self, group):
         """Every rank's pushes into every receive buffer have landed."""

@@ -8,7 +8,8 @@ as much; on its own HBM that is the same bytes read (its pushes) and written
 the real mechanism: a stand-in reducer on the engine (the ShardPusher
 interface: begin / ready / finish) copies (n-1)/n of every final arena bucket
 into a device buffer with nstl_copy_engine (hipMemcpyDeviceToDeviceNoCU: copy
-engines, no kernel) on a side stream, at the points of backward where
+engines, no kernel) -- one stream per destination owner, n - 1 of them, as
+_DeviceTransport does (--streams 1: one stream) -- at the points of backward where
 ShardPusher would push, and the step waits for the copies before its optimizer
 (as ShardPusher.finish does).  The step time is compared with the same step
 without the copies, in alternating blocks.  A kernel trace of the run
@@ -34,12 +35,12 @@ class CopyProbe:
 
     active = False  # FusedAdam: no reduction to consume
 
-    def __init__(self, K, g, ranks, bucket_bytes=64 << 20):
+    def __init__(self, K, g, ranks, bucket_bytes=64 << 20, streams=None):
         self.K, self.g = K, g
         self.frac = (ranks - 1) / ranks
         self.bucket = bucket_bytes // 4
         self.dst = torch.empty(int(g.numel() * self.frac) + self.bucket, dtype=torch.float32, device=g.device)
-        self.side = torch.cuda.Stream(g.device)
+        self.sides = [torch.cuda.Stream(g.device) for _ in range(streams or max(1, ranks - 1))]
         self.sent = 0
         self.out = 0
         self.bytes = 0
@@ -51,8 +52,16 @@ class CopyProbe:
         n = int((hi - lo) * self.frac)
         if n <= 0:
             return
-        self.side.wait_stream(torch.cuda.current_stream())
-        self.K.copy_engine(self.dst[self.out:].data_ptr(), self.g[lo:lo + n], n * 4, stream=self.side.cuda_stream)
+        # the bucket's pushed part as one slice per owner, each on that owner's stream
+        ns = len(self.sides)
+        cut = [lo + (n * i) // ns for i in range(ns + 1)]
+        for i, side in enumerate(self.sides):
+            a, b = cut[i], cut[i + 1]
+            if b <= a:
+                continue
+            side.wait_stream(torch.cuda.current_stream())
+            self.K.copy_engine(self.dst[self.out + a - lo:].data_ptr(), self.g[a:b], (b - a) * 4,
+                               stream=side.cuda_stream)
         self.out += n
         self.bytes += n * 4
 
@@ -65,7 +74,8 @@ class CopyProbe:
         if self.sent < self.g.numel():
             self._push(self.sent, self.g.numel())
             self.sent = self.g.numel()
-        torch.cuda.current_stream().wait_stream(self.side)
+        for side in self.sides:
+            torch.cuda.current_stream().wait_stream(side)
 
     def consume(self):
         return False
@@ -76,6 +86,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=0, help="copy streams (default ranks - 1, as the product)")
     ap.add_argument("--trace-only", action="store_true", help="a few steps with the copies (for a kernel trace)")
     args = ap.parse_args()
     from neurosync_trainer_lite_amd import _hip as K
@@ -102,7 +113,7 @@ def main():
     for _ in range(3):
         step()
     torch.cuda.synchronize()
-    probe = CopyProbe(K, eng.g32, args.ranks)
+    probe = CopyProbe(K, eng.g32, args.ranks, streams=args.streams or None)
 
     def block(with_copies, steps):
         eng.grad_reducer = probe if with_copies else None
@@ -129,7 +140,7 @@ def main():
     cop = [r["ms_per_step"] for r in rows if r["copies"]]
     mb = sum(base) / len(base)
     mc = sum(cop) / len(cop)
-    print(json.dumps({"ranks": args.ranks, "ms_without": round(mb, 3), "ms_with_copies": round(mc, 3),
+    print(json.dumps({"ranks": args.ranks, "streams": len(probe.sides), "ms_without": round(mb, 3), "ms_with_copies": round(mc, 3),
                       "cost_pct": round((mc / mb - 1) * 100, 2), "copied_MB_per_step": rows[-1]["copied_MB_per_step"]}))
 
 
