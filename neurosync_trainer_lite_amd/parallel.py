@@ -263,6 +263,7 @@ class _DeviceTransport:
         self.shard = comm.shard
         self.recv = torch.empty(max(1, n_slots) * comm.shard, dtype=torch.float32, device=grads.device)
         self.sides = {r: torch.cuda.Stream(grads.device) for r in range(comm.world) if r != comm.rank}
+        self.gmap = {}
         mine = K.ipc_handle(self.recv)
         allh = [None] * comm.world
         dist.all_gather_object(allh, mine, group=comm.group)
@@ -282,6 +283,30 @@ class _DeviceTransport:
         side.wait_stream(torch.cuda.current_stream(src.device))
         dst = self.peer[owner] + (slot * self.shard + off) * 4
         self.K.copy_engine(dst, src, src.numel() * 4, stream=side.cuda_stream)
+
+    def gather(self, t, lo, hi, comm):
+        """The all-gather of t (a device tensor every rank holds at the same shape)
+        by the copy engines: this rank's elements [lo, hi) (the updated shard) go
+        to the same offsets of every peer's t, one stream per peer.  Each peer's t
+        is IPC-mapped once (t must keep its storage: the engine's arenas do)."""
+        key = (t.data_ptr(), t.numel(), t.dtype)
+        if key not in self.gmap:
+            h = self.K.ipc_handle(t)
+            allh = [None] * comm.world
+            dist.all_gather_object(allh, h, group=comm.group)
+            peers = {}
+            for r, (hh, off) in enumerate(allh):
+                if r != comm.rank:
+                    base = self.K.ipc_open(hh)
+                    self._opened.append(base)
+                    peers[r] = base + off
+            self.gmap[key] = peers
+        esz = t.element_size()
+        cur = torch.cuda.current_stream(t.device)
+        for r, base in self.gmap[key].items():
+            side = self.sides[r]
+            side.wait_stream(cur)
+            self.K.copy_engine(base + lo * esz, t[lo:hi], (hi - lo) * esz, stream=side.cuda_stream)
 
     def flush(self):
         cur = torch.cuda.current_stream(self.recv.device)
@@ -437,6 +462,21 @@ class ShardPusher(GradAllReducer):
         or k + 1."""
         return self.transport.slots(self.n_slots)
 
+    def all_gather(self, tensors):
+        """After the sharded Adam: every tensor's shard [lo, hi) to every peer
+        (copy engines over IPC mappings of the peers' tensors, as the gradient
+        pushes), then one stream-ordered sync, so the next forward on every rank
+        reads whole weights.  The host transport (CPU tests) all-gathers with
+        the collective."""
+        if not isinstance(self.transport, _DeviceTransport):
+            for t in tensors:
+                self.comm.all_gather(t[:self.comm.numel])
+            return
+        for t in tensors:
+            self.transport.gather(t, self.comm.lo, self.comm.hi, self.comm)
+        self.transport.flush()
+        self.transport.sync(self.group)
+
     def close(self):
         if self.transport is not None:
             self.transport.close()
@@ -467,7 +507,8 @@ class ShardComm:
         dist.all_gather_into_tensor(full, full[self.lo:self.hi].clone(), group=self.group)
 
 
-def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=None, reduced=False, sum_fn=None):
+def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=None, reduced=False, sum_fn=None,
+               gather_fn=None):
     """One sharded clip + Adam step (the FusedAdam kernels passed in as callables,
     so the orchestration is testable on CPU): reduce-scatter the gradients of
     the shardable region [0, comm.numel) (``reduced``: GradShardReducer already
@@ -477,7 +518,8 @@ def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=N
     all-reduce of the partial sums; `tail` = (lo, hi), a small replicated region
     (the f32 vectors), is all-reduced whole, its squares added once and updated
     on every rank; Adam on this shard (+ tail), then all-gather each tensor of
-    `gather` over the shardable region."""
+    `gather` over the shardable region (``gather_fn(tensors)``: ShardPusher's
+    copy-engine all-gather instead of the collective)."""
     if sum_fn is not None:
         sum_fn(g_shard, partial)
     else:
@@ -496,5 +538,8 @@ def zero1_step(comm, g_full, g_shard, partial, sumsq_fn, adam_fn, gather, tail=N
         partial += part_t
         adam_fn(lo, hi - lo, gt, partial)
     adam_fn(comm.lo, comm.shard, g_shard, partial)
+    if gather_fn is not None:
+        gather_fn(gather)
+        return
     for t in gather:
         comm.all_gather(t[:comm.numel])

@@ -213,7 +213,10 @@ class FusedAdam(torch.optim.Optimizer):
         # raised): otherwise the step reduce-scatters as plain zero1 does
         red = eng.grad_reducer
         reduced = isinstance(red, parallel.GradShardReducer) and red.active and red.consume()
-        sum_fn = None
+        sum_fn = gather_fn = None
+        if isinstance(red, parallel.ShardPusher) and red.active:
+            # the updated bf16 shard goes to the peers by the copy engines too
+            gather_fn = red.all_gather
         if isinstance(red, parallel.ShardPusher) and red.active and red.consume():
             # the other ranks' slices arrived in this rank's receive slots during
             # backward (copy engines): own + slots and the clip norm's partials
@@ -225,7 +228,7 @@ class FusedAdam(torch.optim.Optimizer):
                             stream=st)
         parallel.zero1_step(self._comm, eng.g32, self._gs, self.partial, sumsq_fn, adam_fn,
                             [eng.p16] if eng.p16 is not eng.p32 else [eng.p32], tail=(eng.n_shardable, eng.numel),
-                            reduced=reduced, sum_fn=sum_fn)
+                            reduced=reduced, sum_fn=sum_fn, gather_fn=gather_fn)
         eng.master_stale = eng.p16 is not eng.p32
         self._moments_stale = True
         self._snapshot_norm(max_norm)
