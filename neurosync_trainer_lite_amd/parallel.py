@@ -248,21 +248,29 @@ class GradShardReducer(GradAllReducer):
         self.completed = True
 
 
+def push_streams():
+    """NSTL_PUSH_STREAMS: copy streams of the copy-engine exchange (default 2)."""
+    return int(os.environ.get("NSTL_PUSH_STREAMS", "2"))
+
+
 class _DeviceTransport:
     """The receive buffers of a ShardPusher in device memory, shared between the
     ranks' processes through HIP IPC handles (nstl_ipc_*); pushes are copy-engine
-    copies (nstl_copy_engine: hipMemcpyDeviceToDeviceNoCU, no kernel), one side
-    stream per owner: xGMI is point to point, so the copies to different peers
-    travel different links and, on their own streams, different copy engines
-    (one stream would run a rank's 7/8 of the arena through one engine and one
-    link at a time)."""
+    copies (nstl_copy_engine: hipMemcpyDeviceToDeviceNoCU, no kernel) on
+    NSTL_PUSH_STREAMS side streams (owner r on stream r mod n).  xGMI is point to
+    point, so more streams put the copies to different peers on different links
+    and copy engines at once; on one GPU, though, concurrent copy engines cost the
+    step more than their bytes, hence the measured default."""
 
     def __init__(self, grads, comm, n_slots):
         from . import _hip as K
         self.K = K
         self.shard = comm.shard
         self.recv = torch.empty(max(1, n_slots) * comm.shard, dtype=torch.float32, device=grads.device)
-        self.sides = {r: torch.cuda.Stream(grads.device) for r in range(comm.world) if r != comm.rank}
+        n = max(1, min(push_streams(), comm.world - 1))
+        pool = [torch.cuda.Stream(grads.device) for _ in range(n)]
+        self.sides = {r: pool[r % n] for r in range(comm.world) if r != comm.rank}
+        self._pool = pool
         self.gmap = {}
         mine = K.ipc_handle(self.recv)
         allh = [None] * comm.world
@@ -310,7 +318,7 @@ class _DeviceTransport:
 
     def flush(self):
         cur = torch.cuda.current_stream(self.recv.device)
-        for side in self.sides.values():
+        for side in self._pool:
             cur.wait_stream(side)
 
     def sync(self, group):

@@ -8,8 +8,8 @@ as much; on its own HBM that is the same bytes read (its pushes) and written
 the real mechanism: a stand-in reducer on the engine (the ShardPusher
 interface: begin / ready / finish) copies (n-1)/n of every final arena bucket
 into a device buffer with nstl_copy_engine (hipMemcpyDeviceToDeviceNoCU: copy
-engines, no kernel) -- one stream per destination owner, n - 1 of them, as
-_DeviceTransport does (--streams 1: one stream) -- at the points of backward where
+engines, no kernel) -- on NSTL_PUSH_STREAMS streams as _DeviceTransport does
+(--streams k: k streams), the bucket's part cut in one slice per stream -- at the points of backward where
 ShardPusher would push, and the step waits for the copies before its optimizer
 (as ShardPusher.finish does).  The step time is compared with the same step
 without the copies, in alternating blocks.  A kernel trace of the run
@@ -40,7 +40,10 @@ class CopyProbe:
         self.frac = (ranks - 1) / ranks
         self.bucket = bucket_bytes // 4
         self.dst = torch.empty(int(g.numel() * self.frac) + self.bucket, dtype=torch.float32, device=g.device)
-        self.sides = [torch.cuda.Stream(g.device) for _ in range(streams or max(1, ranks - 1))]
+        if not streams:
+            from neurosync_trainer_lite_amd.parallel import push_streams
+            streams = min(push_streams(), ranks - 1)
+        self.sides = [torch.cuda.Stream(g.device) for _ in range(max(1, streams))]
         self.sent = 0
         self.out = 0
         self.bytes = 0
@@ -86,7 +89,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--streams", type=int, default=0, help="copy streams (default ranks - 1, as the product)")
+    ap.add_argument("--streams", type=int, default=0, help="copy streams (default NSTL_PUSH_STREAMS, as the product)")
     ap.add_argument("--trace-only", action="store_true", help="a few steps with the copies (for a kernel trace)")
     args = ap.parse_args()
     from neurosync_trainer_lite_amd import _hip as K
