@@ -249,8 +249,11 @@ class GradShardReducer(GradAllReducer):
 
 
 def push_streams():
-    """NSTL_PUSH_STREAMS: copy streams of the copy-engine exchange (default 2)."""
-    return int(os.environ.get("NSTL_PUSH_STREAMS", "2"))
+    """NSTL_PUSH_STREAMS: copy streams of the copy-engine exchange.  Default 1:
+    on one GPU with an 8-rank push volume the step pays +2.85 % with one stream,
+    +3.8 / +5.6 / +8.5 % with 2 / 3 / 7 (profiles/r5_push_streams.txt); one
+    engine moves the 824 MB in ~14 ms at ~60 GB/s, inside the backward."""
+    return int(os.environ.get("NSTL_PUSH_STREAMS", "1"))
 
 
 class _DeviceTransport:
