@@ -273,7 +273,11 @@ class _DeviceTransport:
         n = max(1, min(push_streams(), comm.world - 1))
         pool = [torch.cuda.Stream(grads.device) for _ in range(n)]
         self.sides = {r: pool[r % n] for r in range(comm.world) if r != comm.rank}
-        self._pool = pool
+        # the weight all-gather runs alone between the optimizer and the next
+        # forward (no compute beside it to disturb): one stream per peer, so the
+        # seven copies travel seven links at once
+        self.gsides = {r: torch.cuda.Stream(grads.device) for r in range(comm.world) if r != comm.rank}
+        self._pool = pool + list(self.gsides.values())
         self.gmap = {}
         mine = K.ipc_handle(self.recv)
         allh = [None] * comm.world
@@ -298,8 +302,9 @@ class _DeviceTransport:
     def gather(self, t, lo, hi, comm):
         """The all-gather of t (a device tensor every rank holds at the same shape)
         by the copy engines: this rank's elements [lo, hi) (the updated shard) go
-        to the same offsets of every peer's t, one stream per peer.  Each peer's t
-        is IPC-mapped once (t must keep its storage: the engine's arenas do)."""
+        to the same offsets of every peer's t, one stream per peer (gsides).  Each
+        peer's t is IPC-mapped once (t must keep its storage: the engine's arenas
+        do)."""
         key = (t.data_ptr(), t.numel(), t.dtype)
         if key not in self.gmap:
             h = self.K.ipc_handle(t)
@@ -315,7 +320,7 @@ class _DeviceTransport:
         esz = t.element_size()
         cur = torch.cuda.current_stream(t.device)
         for r, base in self.gmap[key].items():
-            side = self.sides[r]
+            side = self.gsides[r]
             side.wait_stream(cur)
             self.K.copy_engine(base + lo * esz, t[lo:hi], (hi - lo) * esz, stream=side.cuda_stream)
 
