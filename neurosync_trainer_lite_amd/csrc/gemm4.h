@@ -404,10 +404,32 @@ NSTL_DEV int rope_off8(int t, int chunk, int row_bytes, int swz) { return t * ro
 // C = 0 MFMAs (mma16z: the dX / dW layouts and fp8) read without zeroing (256
 // fewer v_accvgpr_write per tile and wave); the K-major-B (forward) and stream-K
 // instantiations keep the zeroing: with C = 0 their register allocation spilled.
-template <bool ZW = true>
-NSTL_DEV f32x4 rd_acc(f32x4& x) {
+// ZW 2: zeroed by one MFMA on zero operands (0 x 0 + 0) instead of four
+// v_accvgpr_write (half the issue cycles; the next reader of x is the next tile's
+// first MFMA, far past any MFMA-result hazard window) -- the forward
+// instantiations; 1: the four writes (stream-K: with the MFMA form it spilled)
+// z: the zero operand of the ZW 2 form, from zero_operand() -- written by asm
+// followed by wait states of its own: the compiler cannot see that the asm below
+// is an MFMA, so it would not separate a VALU write of a zero it materialised
+// itself from the MFMA's read (that missing hazard wait gave NaN)
+NSTL_DEV s16x4 zero_operand() {
+  uint64_t zz;
+  asm volatile("v_mov_b64 %0, 0\n\ts_nop 4" : "=v"(zz));
+  return __builtin_bit_cast(s16x4, zz);
+}
+template <int ZW = 1>
+NSTL_DEV f32x4 rd_acc(f32x4& x, s16x4 z = {}) {
   float r0, r1, r2, r3;
-  if constexpr (ZW) {
+  if constexpr (ZW == 2) {
+    asm volatile(
+        "v_accvgpr_read_b32 %0, %4\n\t"
+        "v_accvgpr_read_b32 %1, %5\n\t"
+        "v_accvgpr_read_b32 %2, %6\n\t"
+        "v_accvgpr_read_b32 %3, %7"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+        : "a"(x[0]), "a"(x[1]), "a"(x[2]), "a"(x[3]));
+    asm volatile("v_mfma_f32_16x16x16_bf16 %0, %1, %1, 0" : "+a"(x) : "v"(z));
+  } else if constexpr (ZW == 1) {
     asm volatile(
         "v_accvgpr_read_b32 %0, %4\n\t"
         "v_accvgpr_read_b32 %1, %5\n\t"
@@ -572,11 +594,13 @@ NSTL_DEV bool sk_handoff(const StreamK& sk, f32x4 (&acc)[8][8], const Seg& s, in
 // loaded first (bias, dReLU mask words) or read from LDS (RoPE tables).
 // SC (the fp8 kernel): C = a_scale[row] b_scale[col] acc, applied as (acc (a_scale
 // alpha)) b_scale -- the fp8 ring kernel's order -- before the bias.
-template <int EM, bool SC = false, int EDBG = 0, bool ZW = true>
+template <int EM, bool SC = false, int EDBG = 0, int ZW = 1>
 NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, int lane, int wave, int tile_id,
                        const char* rope_lds, bool fin = true) {
   const int g = lane >> 4, c = lane & 15, odd = g & 1;
   const float alpha = p.alpha;
+  s16x4 z = {};
+  if constexpr (ZW == 2) z = zero_operand();
   float rsc[8], csc[8][4];  // SC: the lane's row scales (times alpha) and column scales
   if constexpr (SC) {
 #pragma unroll
@@ -601,11 +625,11 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       for (int b = 0; b < 8; ++b) {
         f32x4 v;
         if constexpr (SC) {
-          v = rd_acc<ZW>(acc[a][b]) * rsc[a];
+          v = rd_acc<ZW>(acc[a][b], z) * rsc[a];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] *= csc[b][e];
         } else {
-          v = rd_acc<ZW>(acc[a][b]) * alpha;
+          v = rd_acc<ZW>(acc[a][b], z) * alpha;
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) ssq += v[e] * v[e];
@@ -690,7 +714,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       }
 #pragma unroll
       for (int bp = 0; bp < 8; bp += 2) {
-        f32x4 uv[2] = {rd_acc<ZW>(acc[a][bp]), rd_acc<ZW>(acc[a][bp + 1])};
+        f32x4 uv[2] = {rd_acc<ZW>(acc[a][bp], z), rd_acc<ZW>(acc[a][bp + 1], z)};
         if (!fin) {  // a stream-K first contributor: only the zeroing reads above
           G4_SB();
           continue;
@@ -1037,7 +1061,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     }
     bool fin = true;
     if constexpr (SK) fin = sk_handoff(gp.sk, acc, sg, wk.rank, wave, lane);
-    epilogue<EM, false, (DBG & 8192) ? 1 : 0, !ZC>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, fin);
+    epilogue<EM, false, (DBG & 8192) ? 1 : 0, ZC ? 0 : (SK ? 1 : 2)>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt,
+                                                                  rope_lds, fin);
     if (!has_next) break;
     sg = ns;
     prob = nprob;
@@ -1279,8 +1304,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
     }
     G4_LGKM0();  // the next tile's last B fragment: before the epilogue's own LDS reads
     lt = sg.t < T ? xcd_remap(sg.t, T) : sg.t;
-    epilogue<EM, true, (DBG & 8192) ? 1 : 0, false>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds,
-                                                   true);
+    epilogue<EM, true, (DBG & 8192) ? 1 : 0, 0>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, true);
     if (!has_next) break;
     if constexpr (EM != EM_BF16) {
       // the per-lane DMA offsets and read addresses, recomputed after every
