@@ -299,12 +299,8 @@ class _DeviceTransport:
         dst = self.peer[owner] + (slot * self.shard + off) * 4
         self.K.copy_engine(dst, src, src.numel() * 4, stream=side.cuda_stream)
 
-    def gather(self, t, lo, hi, comm):
-        """The all-gather of t (a device tensor every rank holds at the same shape)
-        by the copy engines: this rank's elements [lo, hi) (the updated shard) go
-        to the same offsets of every peer's t, one stream per peer (gsides).  Each
-        peer's t is IPC-mapped once (t must keep its storage: the engine's arenas
-        do)."""
+    def map(self, t, comm):
+        """Every peer's copy of t, IPC-mapped (a collective on first use of t)."""
         key = (t.data_ptr(), t.numel(), t.dtype)
         if key not in self.gmap:
             h = self.K.ipc_handle(t)
@@ -317,9 +313,18 @@ class _DeviceTransport:
                     self._opened.append(base)
                     peers[r] = base + off
             self.gmap[key] = peers
+        return self.gmap[key]
+
+    def gather(self, t, lo, hi, comm):
+        """The all-gather of t (a device tensor every rank holds at the same shape)
+        by the copy engines: this rank's elements [lo, hi) (the updated shard) go
+        to the same offsets of every peer's t, one stream per peer (gsides).  Each
+        peer's t is IPC-mapped once (t must keep its storage: the engine's arenas
+        do)."""
+        peers = self.map(t, comm)
         esz = t.element_size()
         cur = torch.cuda.current_stream(t.device)
-        for r, base in self.gmap[key].items():
+        for r, base in peers.items():
             side = self.gsides[r]
             side.wait_stream(cur)
             self.K.copy_engine(base + lo * esz, t[lo:hi], (hi - lo) * esz, stream=side.cuda_stream)
@@ -406,13 +411,19 @@ class ShardPusher(GradAllReducer):
 
     mode = "zero1_push"
 
-    def __init__(self, grads, comm, bucket_bytes=DEFAULT_BUCKET_BYTES, min_world=2):
+    def __init__(self, grads, comm, bucket_bytes=DEFAULT_BUCKET_BYTES, min_world=2, gather=()):
         self.comm = comm
         super().__init__(grads, comm.group, bucket_bytes, min_world)
         self.n_slots = comm.world - 1
         self.transport = None
         if self.active:
             self.transport = (_DeviceTransport if grads.is_cuda else _HostTransport)(grads, comm, self.n_slots)
+            if isinstance(self.transport, _DeviceTransport):
+                # the all-gather's targets (the weight arena) mapped now, so that a
+                # mapping failure falls back to zero1 on every rank (create) rather
+                # than surfacing in the first optimizer step
+                for t in gather:
+                    self.transport.map(t, comm)
 
     @classmethod
     def create(cls, grads, comm, **kw):

@@ -206,7 +206,10 @@ def attach_data_parallel(model, optimizer, world):
         optimizer.shard()
         if mode == "zero1_push":
             from ..parallel import ShardPusher
-            eng.grad_reducer = ShardPusher.create(eng.g32, optimizer._comm)  # None: zero1 (every rank agrees)
+            # None: zero1 (every rank agrees); gather: the bf16 weight arena the
+            # sharded step all-gathers (parallel.zero1_step)
+            eng.grad_reducer = ShardPusher.create(eng.g32, optimizer._comm,
+                                                  gather=[eng.p16 if eng.p16 is not eng.p32 else eng.p32])
         elif mode == "zero1_overlap":
             from ..parallel import GradShardReducer, cede_cus
             cede_cus(int(os.environ.get("NSTL_CEDE_CUS", "32")), eng.device)
