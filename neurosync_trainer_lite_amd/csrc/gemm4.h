@@ -116,6 +116,20 @@ NSTL_DEV void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds, 16, voff, soff, 0, 0);
 }
 
+// Epilogue side data in LDS (round 5): a wave's bias columns (BF16, RELU_DROP)
+// or dReLU keep-bit words (DRELU), DMA'd into its own 2 KB at the tile's start.
+// Loaded in the epilogue instead, they sat behind the next tile's stage pieces
+// in vmcnt order (issued during the last two steps), so the epilogue began with
+// a wait for those, and the keep-bit words come cold from HBM.  Issued at the
+// tile's start they are older than every stage piece a K step waits for, so they
+// have landed by the epilogue, which reads them by inline asm (a plain LDS load
+// would make the compiler wait for the DMA in flight).
+constexpr int SIDE_W = 2048;             // per wave
+constexpr int SIDE_LDS = 4 * SIDE_W;
+// side layout: bias floats [128] (columns col0 ..); keep-bit words [hb][r0][16]
+// (word (row block hb, row & 7 = r0, column group k of the wave's 16) at
+// hb * 1024 + r0 * 128 + 8 k).  side_dma follows mask_word.
+
 // Per-lane DMA source offsets of this wave's 8 pieces of one operand's stage,
 // relative to the tile's first row (K-major) / column (MN-major): fixed per
 // problem.  The tile's offset and the K advance go in the scalar offset.
@@ -380,6 +394,32 @@ NSTL_DEV int64_t mask_word(int N, int row, int col) {
   return ((int64_t)(row >> 6) * 8 + (row & 7)) * ((N + 7) >> 3) + (col >> 3);
 }
 
+// the wave's side data of its 128 x 128 block (row0, col0) (see SIDE_W)
+template <int EM>
+NSTL_DEV void side_dma(const Params& p, char* side, int row0, int col0, int lane) {
+  if constexpr (EM == EM_DRELU) {
+    // 2 x 8 rows of 16 words (128 B): lane l of piece j loads words 2 (l & 7),
+    // + 1 of row (j, l >> 3)
+    const uint32_t wpr = (uint32_t)((p.N + 7) >> 3);  // words per mask row
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.relu_mask, 0, (int)((uint32_t)(p.M >> 6) * 8u * wpr * 8u), 0x00020000);
+    // the lane's part in the vector offset, the block's in the scalar one
+    const uint32_t vo = ((uint32_t)(lane >> 3) * wpr + 2u * (uint32_t)(lane & 7)) * 8u;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t so =
+          __builtin_amdgcn_readfirstlane((((uint32_t)((row0 >> 6) + j) * 8u) * wpr + (uint32_t)(col0 >> 3)) * 8u);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(side + j * 1024), 16, vo, so, 0, 0);
+    }
+  } else if (p.bias != nullptr) {
+    // 128 floats from lanes 0..31; lanes 32..63 read the next 128 (zeros past N)
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, 0, (int)((uint32_t)p.N * 4u), 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)side, 16, (uint32_t)lane * 16u,
+                                             __builtin_amdgcn_readfirstlane((uint32_t)col0 * 4u), 0, 0);
+  }
+}
+
 // RoPE tables in LDS (EM_ROPE): row t holds rope_dim / 2 (cos, sin) pairs,
 // 16-byte chunk k (pairs 2k, 2k + 1) at k ^ (t & m): the 16 lanes of a read
 // (16 consecutive positions, one chunk) hit 16 distinct bank slots when the row
@@ -594,9 +634,9 @@ NSTL_DEV bool sk_handoff(const StreamK& sk, f32x4 (&acc)[8][8], const Seg& s, in
 // loaded first (bias, dReLU mask words) or read from LDS (RoPE tables).
 // SC (the fp8 kernel): C = a_scale[row] b_scale[col] acc, applied as (acc (a_scale
 // alpha)) b_scale -- the fp8 ring kernel's order -- before the bias.
-template <int EM, bool SC = false, int EDBG = 0, int ZW = 1>
+template <int EM, bool SC = false, int EDBG = 0, int ZW = 1, bool SIDE = false>
 NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, int lane, int wave, int tile_id,
-                       const char* rope_lds, bool fin = true) {
+                       const char* rope_lds, bool fin = true, const char* side = nullptr) {
   const int g = lane >> 4, c = lane & 15, odd = g & 1;
   const float alpha = p.alpha;
   s16x4 z = {};
@@ -646,11 +686,23 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
     }
   } else {
     f32x4 bias[8];
+    if constexpr (SIDE && EM != EM_DRELU) {  // side_dma's copy (see SIDE_W)
+      if (p.bias != nullptr) {
+        const uint32_t ba = lds_addr(side + 16 * g);
 #pragma unroll
-    for (int b = 0; b < 8; ++b)
+        for (int b = 0; b < 8; ++b) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bias[b]) : "v"(ba), "i"(64 * b));
+        G4_LGKM0();
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        bias[b][e] = (EM != EM_DRELU && p.bias != nullptr) ? p.bias[col0 + 16 * b + 4 * g + e] : 0.f;
+        for (int b = 0; b < 8; ++b) bias[b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          bias[b][e] = (EM != EM_DRELU && p.bias != nullptr) ? p.bias[col0 + 16 * b + 4 * g + e] : 0.f;
+    }
     const uint32_t seed_term = nstl_seed_term(p.seed);
     const bool rmask = (EM == EM_RELU_DROP || EM == EM_DRELU) && p.relu_mask != nullptr;
     // mask nibbles: [row block hb][column block b], 4 rows (a & 3) x 4 bits
@@ -660,17 +712,28 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
 #pragma unroll
       for (int b = 0; b < 8; ++b) mbits[hb][b] = 0;
     if (EM == EM_DRELU) {
+      // side_dma's copy: word (hb, c & 7, 2b + (g >> 1)); a row block's 8 reads, one wait
+      const uint32_t ma = lds_addr(side + (c & 7) * 128 + (g >> 1) * 8);
       // the lane's nibble of each word: byte 2 a2 + (c >> 3), bits 4 (g & 1)
 #pragma unroll
-      for (int hb = 0; hb < 2; ++hb)
+      for (int hb = 0; hb < 2; ++hb) {
+        i32x2_t sw[8];
+        if constexpr (SIDE) {
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(sw[b]) : "v"(ma), "i"(hb * 1024 + 16 * b));
+          G4_LGKM0();
+        }
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
-          const uint64_t w = p.relu_mask[mask_word(p.N, row0 + 64 * hb + c, col0 + 16 * b + 4 * g)];
+          const uint64_t w = SIDE ? (((uint64_t)(uint32_t)sw[b][1] << 32) | (uint32_t)sw[b][0])
+                                  : p.relu_mask[mask_word(p.N, row0 + 64 * hb + c, col0 + 16 * b + 4 * g)];
           uint32_t s = 0;
 #pragma unroll
           for (int a2 = 0; a2 < 4; ++a2) s |= ((uint32_t)(w >> (8 * (2 * a2 + (c >> 3)) + 4 * odd)) & 0xF) << (4 * a2);
           mbits[hb][b] = s;
         }
+      }
     }
     float csum[8][4];
 #pragma unroll
@@ -699,17 +762,28 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       const int t = EM != EM_ROPE ? 0 : ((p.rope_T & (p.rope_T - 1)) == 0 ? row & (p.rope_T - 1) : row % p.rope_T);
       // RoPE: the row's 8 table reads issued together (one at the point of use
       // exposed an LDS round trip per 4 outputs)
+      // Read by inline asm: a plain LDS load here may alias the next tile's stage
+      // DMA in flight, so the compiler put vmcnt(0) in front of every row's reads
+      // -- a wait for the stage pieces and for every store of the rows before.
       f32x4 rcs[8];
       if constexpr (EM == EM_ROPE) {
+        if (p.rope_bf16) {  // (cos, sin) pairs as bf16 (8-byte chunks): the fp8 kernel at T = 256
+          i32x2_t w[8];
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          if (p.rope_bf16) {  // (cos, sin) pairs as bf16 (8-byte chunks): the fp8 kernel at T = 256
-            const uint2 w = *(const uint2*)(rope_lds + rope_off8(t, rchunk[b], p.rope_dim * 2, rswz));
-            rcs[b] = (f32x4){__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xFFFF0000u),
-                             __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xFFFF0000u)};
-          } else {
-            rcs[b] = *(const f32x4*)(rope_lds + rope_off(t, rchunk[b], rope_rb, rswz));
+          for (int b = 0; b < 8; ++b)
+            asm volatile("ds_read_b64 %0, %1" : "=v"(w[b]) : "v"(lds_addr(rope_lds + rope_off8(t, rchunk[b], p.rope_dim * 2, rswz))));
+          G4_LGKM0();
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            const uint32_t x = (uint32_t)w[b][0], y = (uint32_t)w[b][1];
+            rcs[b] = (f32x4){__uint_as_float(x << 16), __uint_as_float(x & 0xFFFF0000u), __uint_as_float(y << 16),
+                             __uint_as_float(y & 0xFFFF0000u)};
           }
+        } else {
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+            asm volatile("ds_read_b128 %0, %1" : "=v"(rcs[b]) : "v"(lds_addr(rope_lds + rope_off(t, rchunk[b], rope_rb, rswz))));
+          G4_LGKM0();
         }
       }
 #pragma unroll
@@ -856,7 +930,10 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   // R3 1: A has the ring of three (DMA'd in h = 0), B the ring of two; 2: the reverse
   constexpr bool A3 = R3 == 1, B3 = R3 == 2;
   static_assert(!(R3 && EM == EM_ROPE), "the 3 + 2 ring fills the LDS: no room for the RoPE table");
-  constexpr int SMEM_ALL = R3 ? 5 * OPS : SMEM + (EM == EM_ROPE ? ROPE_LDS : 0);
+  // epilogue side data (SIDE_W): not with the 3 + 2 ring (no LDS left) or RoPE,
+  // nor for the ReLU-dropout epilogue on an MN-major B (one VGPR short: spills)
+  constexpr bool SIDE = !R3 && (EM == EM_BF16 || (EM == EM_RELU_DROP && BKM) || EM == EM_DRELU) && !(DBG & 16384);
+  constexpr int SMEM_ALL = R3 ? 5 * OPS : SMEM + (EM == EM_ROPE ? ROPE_LDS : 0) + (SIDE ? SIDE_LDS : 0);
   constexpr int B_BASE = A3 ? 3 * OPS : 2 * OPS;  // B's slot 0
   constexpr bool ZC = !BKM && !SK;                 // tiles start with C = 0 MFMAs (rd_acc)
   __shared__ __attribute__((aligned(16))) char smem[SMEM_ALL];
@@ -873,6 +950,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
   char* const adst0 = smem + wave * 8 * 1024;
   char* const bdst0 = smem + B_BASE + wave * 8 * 1024;
   const char* rope_lds = smem + SMEM;
+  char* const side = smem + SMEM + wave * SIDE_W;  // SIDE
   if constexpr (EM == EM_ROPE) {
     // the whole cos/sin table, once per workgroup (one problem per launch)
     const Params& p0 = gp.g[0];
@@ -1044,6 +1122,9 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     if (!has_next) ns = sg;
     int nprob = prob, nm0 = m0, nn0 = n0, nlt = lt;
     if (has_next) locate(ns.t, nprob, nm0, nn0, nlt);
+    // older than every stage piece the steps wait for: landed by the epilogue; the
+    // previous epilogue's reads of the side area completed before its values were used
+    if constexpr (SIDE) side_dma<EM>(p, side, m0 + wm * 128, n0 + wn * 128, lane);
     // step kt (slot kt & 1: nk is even, so every tile starts on slot 0) stages
     // stage kt + 2: this tile's while kt + 2 < nk, then the next tile's 0 and 1.
     // Three step sites (more make the register allocator give the fragment sets
@@ -1061,8 +1142,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     }
     bool fin = true;
     if constexpr (SK) fin = sk_handoff(gp.sk, acc, sg, wk.rank, wave, lane);
-    epilogue<EM, false, (DBG & 8192) ? 1 : 0, ZC ? 0 : (SK ? 1 : 2)>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt,
-                                                                  rope_lds, fin);
+    epilogue<EM, false, (DBG & 8192) ? 1 : 0, ZC ? 0 : (SK ? 1 : 2), SIDE>(p, acc, m0 + wm * 128, n0 + wn * 128, lane,
+                                                                        wave, lt, rope_lds, fin, side);
     if (!has_next) break;
     sg = ns;
     prob = nprob;

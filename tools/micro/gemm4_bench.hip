@@ -330,6 +330,98 @@ int f8_abl(const bf16* A, const bf16* B, bf16* C, hipStream_t st) {
   return 0;
 }
 
+// G4_EPI_COST=1: what each fused epilogue costs beside the plain bf16 one on its
+// step shape (timing only): FFN1 forward (ReLU, + dropout hash, + keep-bit words),
+// FFN2 dX (dReLU from the keep bits, + bias column sums), q|k|v forward (RoPE)
+int epi_cost(const bf16* A, const bf16* B, bf16* C, hipStream_t st) {
+  uint64_t* mask;
+  float *colsum, *rc, *rs;
+  CK(hipMalloc(&mask, 16384LL * 4096 / 8));
+  CK(hipMemset(mask, 0x5A, 16384LL * 4096 / 8));
+  CK(hipMalloc(&colsum, 128LL * 4096 * 4));
+  CK(hipMalloc(&rc, 128 * 32 * 4));
+  CK(hipMalloc(&rs, 128 * 32 * 4));
+  CK(hipMemset(rc, 0, 128 * 32 * 4));
+  CK(hipMemset(rs, 0, 128 * 32 * 4));
+  float* bias;
+  CK(hipMalloc(&bias, 4096 * 4));
+  CK(hipMemset(bias, 0, 4096 * 4));
+  // cold keep-bit words: 40 copies (320 MB, past the Infinity Cache), one per launch
+  uint64_t* cold;
+  const int64_t mwords = 16384LL * 4096 / 64;
+  CK(hipMalloc(&cold, 40 * mwords * 8));
+  CK(hipMemset(cold, 0x5A, 40 * mwords * 8));
+  struct Arm { const char* name; int M, N, K; bool bkm; int em; bool drop, msk, csum, bias = false, cold = false; bool old = false; };
+  const Arm arms[] = {{"ffn1 fwd  bf16          ", 16384, 4096, 1024, true, g4::EM_BF16, false, false, false},
+                      {"ffn1 fwd  relu          ", 16384, 4096, 1024, true, g4::EM_RELU_DROP, false, false, false},
+                      {"ffn1 fwd  relu+drop     ", 16384, 4096, 1024, true, g4::EM_RELU_DROP, true, false, false},
+                      {"ffn1 fwd  relu+mask     ", 16384, 4096, 1024, true, g4::EM_RELU_DROP, false, true, false},
+                      {"ffn1 fwd  relu+drop+mask", 16384, 4096, 1024, true, g4::EM_RELU_DROP, true, true, false},
+                      {"ffn2 dX   bf16          ", 16384, 4096, 1024, false, g4::EM_BF16, false, false, false},
+                      {"ffn2 dX   drelu         ", 16384, 4096, 1024, false, g4::EM_DRELU, true, true, false},
+                      {"ffn2 dX   drelu+colsum  ", 16384, 4096, 1024, false, g4::EM_DRELU, true, true, true},
+                      {"qkv fwd   bf16          ", 16384, 3072, 1024, true, g4::EM_BF16, false, false, false},
+                      {"qkv fwd   rope          ", 16384, 3072, 1024, true, g4::EM_ROPE, false, false, false},
+                      {"ffn1 fwd  bf16 +bias    ", 16384, 4096, 1024, true, g4::EM_BF16, false, false, false, true},
+                      {"ffn1 fwd  r+d+m +bias   ", 16384, 4096, 1024, true, g4::EM_RELU_DROP, true, true, false, true},
+                      {"qkv fwd   rope +bias    ", 16384, 3072, 1024, true, g4::EM_ROPE, false, false, false, true},
+                      {"ffn2 dX   drelu+cs cold ", 16384, 4096, 1024, false, g4::EM_DRELU, true, true, true, false, true},
+                      {"ffn1 fwd  r+d+m +bias OLD", 16384, 4096, 1024, true, g4::EM_RELU_DROP, true, true, false, true, false, true},
+                      {"ffn1 fwd  bf16 +bias OLD", 16384, 4096, 1024, true, g4::EM_BF16, false, false, false, true, false, true},
+                      {"ffn2 dX   drelu+cs cold OLD", 16384, 4096, 1024, false, g4::EM_DRELU, true, true, true, false, true, true},
+                      {"out fwd   bf16 +bias    ", 16384, 1024, 1024, true, g4::EM_BF16, false, false, false, true},
+                      {"out fwd   bf16 +bias OLD", 16384, 1024, 1024, true, g4::EM_BF16, false, false, false, true, false, true}};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int round = 0; round < 4; ++round)
+    for (const Arm& c : arms) {
+      g4::GroupParams gp{};
+      g4::Params& p = gp.g[0];
+      p.M = c.M; p.N = c.N; p.K = c.K; p.alpha = 1.f;
+      p.A = (const char*)A; p.lda = c.K; p.B = (const char*)B; p.ldb = c.bkm ? c.K : c.N; p.C = (char*)C; p.ldc = c.N;
+      p.a_bytes = (uint32_t)((int64_t)c.M * c.K * 2); p.b_bytes = (uint32_t)((int64_t)c.N * c.K * 2);
+      p.inv_keep = 1.f / 0.7f; p.thresh = c.drop ? 19661u : 0u; p.seed = 1234;
+      p.relu_mask = c.msk ? mask : nullptr;
+      p.bias = c.bias ? bias : nullptr;
+      int launch_no = 0;
+      p.colsum_part = c.csum ? colsum : nullptr;
+      p.rope_cos = rc; p.rope_sin = rs; p.rope_T = 128; p.rope_dim = 64; p.rope_cols = 2048;
+      p.tiles_m = c.M / 256; p.tiles_n = c.N / 256;
+      gp.n = 1; gp.tile_end[0] = p.tiles_m * p.tiles_n;
+      typedef void (*F)(const g4::GroupParams&, hipStream_t);
+      F f = nullptr;
+      if (c.em == g4::EM_BF16)
+        f = c.old ? launch_any<true, true, g4::EM_BF16, 16384>
+                  : (c.bkm ? launch_any<true, true, g4::EM_BF16, 0> : launch_any<true, false, g4::EM_BF16, 0>);
+      if (c.em == g4::EM_RELU_DROP)
+        f = c.old ? launch_any<true, true, g4::EM_RELU_DROP, 16384> : launch_any<true, true, g4::EM_RELU_DROP, 0>;
+      if (c.em == g4::EM_DRELU)
+        f = c.old ? launch_any<true, false, g4::EM_DRELU, 16384> : launch_any<true, false, g4::EM_DRELU, 0>;
+      if (c.em == g4::EM_ROPE) f = launch_any<true, true, g4::EM_ROPE, 0>;
+      auto run = [&]() {
+        if (c.cold) gp.g[0].relu_mask = cold + (launch_no++ % 40) * mwords;
+        f(gp, st);
+      };
+      for (int w = 0; w < 3; ++w) run();
+      std::vector<float> ts;
+      for (int r = 0; r < 15; ++r) {
+        CK(hipEventRecord(e0, st)); run(); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+      }
+      std::sort(ts.begin(), ts.end());
+      // sustained: 100 launches back to back (the clock a busy step holds), mean
+      CK(hipEventRecord(e0, st));
+      for (int r = 0; r < 100; ++r) run();
+      CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+      float msum; CK(hipEventElapsedTime(&msum, e0, e1));
+      const double us = ts[7] * 1e3, fl = 2.0 * c.M * c.N * c.K, sus = msum * 10.0;
+      if (round > 0) printf("round %d  %s %8.1f us  %7.1f TF/s   sustained %8.1f us  %7.1f TF/s\n", round, c.name, us, fl / us * 1e-6, sus, fl / sus * 1e-6);
+      fflush(stdout);
+    }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   struct Shape { const char* name; int M, N, K, bkm; };
   const Shape shapes[] = {
@@ -361,6 +453,7 @@ int main(int argc, char** argv) {
   }
   if (getenv("G4_STORE_AB")) return store_ab(A, B, C, st);
   if (getenv("G4_F8_ABL")) return f8_abl(A, B, C, st);
+  if (getenv("G4_EPI_COST")) return epi_cost(A, B, C, st);
   if (getenv("G4_DMA_AB")) {
     float* Cf;
     CK(hipMalloc(&Cf, 4096LL * 4096 * 4));
