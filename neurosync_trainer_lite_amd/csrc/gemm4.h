@@ -245,9 +245,12 @@ NSTL_DEV void dma_lanes(Dma& d, const Params& p, int wave, int lane) {
 // would wrap every DMA in a readfirstlane loop)
 // (ks: the first 256-deep K unit of a stream-K segment)
 template <bool AK, bool BKM>
-NSTL_DEV void dma_tile(Dma& d, const Params& p, int m0, int n0, int ks) {
-  d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)p.a_bytes, 0x00020000);
-  d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, (int)p.b_bytes, 0x00020000);
+// live = false: the refill after a workgroup's last tile, with empty buffer
+// ranges (its pieces return zeros without touching memory: no HBM / L2 traffic
+// beside the last epilogue's stores, and the exit drain waits for less)
+NSTL_DEV void dma_tile(Dma& d, const Params& p, int m0, int n0, int ks, bool live = true) {
+  d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, live ? (int)p.a_bytes : 0, 0x00020000);
+  d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, live ? (int)p.b_bytes : 0, 0x00020000);
   d.a_kb = AK ? 2 * BK : (uint32_t)(2 * BK * p.lda);
   d.b_kb = BKM ? 2 * BK : (uint32_t)(2 * BK * p.ldb);
   const uint32_t k0 = (uint32_t)ks * 4u;  // stages
@@ -1117,7 +1120,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
     const int nk = sg.ke < 0 ? p.K / BK : 4 * (sg.ke - sg.ks);
     Seg ns;
     const bool has_next = wk.next(ns);
-    // the next segment (after the workgroup's last: itself again, a harmless
+    // the next segment (after the workgroup's last: itself again, an empty-range
     // refill of slots nobody reads afterwards, drained before exit)
     if (!has_next) ns = sg;
     int nprob = prob, nm0 = m0, nn0 = n0, nlt = lt;
@@ -1135,7 +1138,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4_kernel(const GroupParams gp) {
       if (kt + 1 < nk) {
         if (kt + 1 == nk - 2) {
           if (GROUPED && nprob != prob) dma_lanes<AK, BKM>(d, gp.g[nprob], wave, lane);
-          dma_tile<AK, BKM>(d, gp.g[nprob], nm0, nn0, ns.ks);
+          dma_tile<AK, BKM>(d, gp.g[nprob], nm0, nn0, ns.ks, has_next || (DBG & 32768));
         }
         step(S0{}, W0{}, (uint32_t)(kt + 3 < nk ? kt + 3 : kt + 3 - nk), d);
       }
@@ -1196,9 +1199,9 @@ NSTL_DEV void dma_lane_offsets_f8(uint32_t (&vo)[8], int64_t ld, int wave, int l
     vo[s] = (uint32_t)((int64_t)row * ld + lc * 16);
   }
 }
-NSTL_DEV void dma_tile_f8(Dma& d, const Params& p, int m0, int n0) {
-  d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)p.a_bytes, 0x00020000);
-  d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, (int)p.b_bytes, 0x00020000);
+NSTL_DEV void dma_tile_f8(Dma& d, const Params& p, int m0, int n0, bool live = true) {  // live: dma_tile
+  d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, live ? (int)p.a_bytes : 0, 0x00020000);
+  d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, live ? (int)p.b_bytes : 0, 0x00020000);
   d.a_kb = F8_BK;
   d.b_kb = F8_BK;
   d.ta = __builtin_amdgcn_readfirstlane((uint32_t)(m0 * p.lda));
@@ -1379,7 +1382,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
     for (int kt = 1; kt < nk; kt += 2) {
       step(S1{}, W0{}, (uint32_t)(kt + 2 < nk ? kt + 2 : kt + 2 - nk));
       if (kt + 1 < nk) {
-        if (kt + 1 == nk - 2) dma_tile_f8(d, p, nm0, nn0);
+        if (kt + 1 == nk - 2) dma_tile_f8(d, p, nm0, nn0, has_next);
         step(S0{}, W0{}, (uint32_t)(kt + 3 < nk ? kt + 3 : kt + 3 - nk));
       }
     }

@@ -351,7 +351,7 @@ int epi_cost(const bf16* A, const bf16* B, bf16* C, hipStream_t st) {
   const int64_t mwords = 16384LL * 4096 / 64;
   CK(hipMalloc(&cold, 40 * mwords * 8));
   CK(hipMemset(cold, 0x5A, 40 * mwords * 8));
-  struct Arm { const char* name; int M, N, K; bool bkm; int em; bool drop, msk, csum, bias = false, cold = false; bool old = false; };
+  struct Arm { const char* name; int M, N, K; bool bkm; int em; bool drop, msk, csum, bias = false, cold = false; int old = 0; };  // old: 1 DBG 16384 (no side data), 2 DBG 32768 (live refill)
   const Arm arms[] = {{"ffn1 fwd  bf16          ", 16384, 4096, 1024, true, g4::EM_BF16, false, false, false},
                       {"ffn1 fwd  relu          ", 16384, 4096, 1024, true, g4::EM_RELU_DROP, false, false, false},
                       {"ffn1 fwd  relu+drop     ", 16384, 4096, 1024, true, g4::EM_RELU_DROP, true, false, false},
@@ -370,7 +370,11 @@ int epi_cost(const bf16* A, const bf16* B, bf16* C, hipStream_t st) {
                       {"ffn1 fwd  bf16 +bias OLD", 16384, 4096, 1024, true, g4::EM_BF16, false, false, false, true, false, true},
                       {"ffn2 dX   drelu+cs cold OLD", 16384, 4096, 1024, false, g4::EM_DRELU, true, true, true, false, true, true},
                       {"out fwd   bf16 +bias    ", 16384, 1024, 1024, true, g4::EM_BF16, false, false, false, true},
-                      {"out fwd   bf16 +bias OLD", 16384, 1024, 1024, true, g4::EM_BF16, false, false, false, true, false, true}};
+                      {"out fwd   bf16 +bias OLD", 16384, 1024, 1024, true, g4::EM_BF16, false, false, false, true, false, true},
+                      {"out fwd   bf16 +bias REFILL", 16384, 1024, 1024, true, g4::EM_BF16, false, false, false, true, false, 2},
+                      {"ffn1 fwd  r+d+m +bias REFILL", 16384, 4096, 1024, true, g4::EM_RELU_DROP, true, true, false, true, false, 2},
+                      {"out dX    bf16          ", 16384, 1024, 1024, false, g4::EM_BF16, false, false, false},
+                      {"out dX    bf16 REFILL   ", 16384, 1024, 1024, false, g4::EM_BF16, false, false, false, false, false, 2}};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -392,10 +396,12 @@ int epi_cost(const bf16* A, const bf16* B, bf16* C, hipStream_t st) {
       typedef void (*F)(const g4::GroupParams&, hipStream_t);
       F f = nullptr;
       if (c.em == g4::EM_BF16)
-        f = c.old ? launch_any<true, true, g4::EM_BF16, 16384>
-                  : (c.bkm ? launch_any<true, true, g4::EM_BF16, 0> : launch_any<true, false, g4::EM_BF16, 0>);
+        f = c.old == 1 ? launch_any<true, true, g4::EM_BF16, 16384>
+            : c.old == 2 ? (c.bkm ? launch_any<true, true, g4::EM_BF16, 32768> : launch_any<true, false, g4::EM_BF16, 32768>)
+                         : (c.bkm ? launch_any<true, true, g4::EM_BF16, 0> : launch_any<true, false, g4::EM_BF16, 0>);
       if (c.em == g4::EM_RELU_DROP)
-        f = c.old ? launch_any<true, true, g4::EM_RELU_DROP, 16384> : launch_any<true, true, g4::EM_RELU_DROP, 0>;
+        f = c.old == 1 ? launch_any<true, true, g4::EM_RELU_DROP, 16384>
+            : c.old == 2 ? launch_any<true, true, g4::EM_RELU_DROP, 32768> : launch_any<true, true, g4::EM_RELU_DROP, 0>;
       if (c.em == g4::EM_DRELU)
         f = c.old ? launch_any<true, false, g4::EM_DRELU, 16384> : launch_any<true, false, g4::EM_DRELU, 0>;
       if (c.em == g4::EM_ROPE) f = launch_any<true, true, g4::EM_ROPE, 0>;
