@@ -639,11 +639,17 @@ NSTL_DEV void ring_epi(const GemmParams& p, const ACC& acc, int row0, int col0, 
       const char* src = scr + (it * RPI + r0) * RING_EPI_RB + c * 4;
       float v[CW];
       {
-        const f32x4 v0 = *(const f32x4*)src;
+        // the wave's own scratch, read by asm: as plain loads the compiler put
+        // vmcnt(0) in front of each (the ring's stage DMA may alias), i.e. a wait
+        // for every store of the iterations before
+        f32x4 v0, v1;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(v0) : "v"(lds_u32(src)) : "memory");
+        if (CW == 8) asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(v1) : "v"(lds_u32(src)) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = v0[e];
         if (CW == 8) {
-          const f32x4 v1 = *(const f32x4*)(src + 16);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[(4 + e) % CW] = v1[e];
         }
