@@ -279,16 +279,36 @@ class _DeviceTransport:
         self.gsides = {r: torch.cuda.Stream(grads.device) for r in range(comm.world) if r != comm.rank}
         self._pool = pool + list(self.gsides.values())
         self.gmap = {}
-        mine = K.ipc_handle(self.recv)
+        self._opened = []
+        # a local failure is recorded, not raised, until every rank has taken the
+        # same collectives (ShardPusher raises it afterwards; create() agrees)
+        self.error = None
+        self.peer = self._exchange(self.recv, comm)
+
+    def _exchange(self, t, comm):
+        """IPC handle of t to every rank, every peer's t mapped here (a collective;
+        failures recorded in self.error)."""
+        try:
+            mine = self.K.ipc_handle(t)
+        except Exception as e:  # noqa: BLE001
+            mine, self.error = None, self.error or e
         allh = [None] * comm.world
         dist.all_gather_object(allh, mine, group=comm.group)
-        self.peer = {}
-        self._opened = []
-        for r, (h, off) in enumerate(allh):
-            if r != comm.rank:
-                base = K.ipc_open(h)
-                self._opened.append(base)
-                self.peer[r] = base + off
+        peers = {}
+        for r, hh in enumerate(allh):
+            if r == comm.rank:
+                continue
+            if hh is None:
+                self.error = self.error or RuntimeError("rank %d has no IPC handle" % r)
+                continue
+            try:
+                base = self.K.ipc_open(hh[0])
+            except Exception as e:  # noqa: BLE001
+                self.error = self.error or e
+                continue
+            self._opened.append(base)
+            peers[r] = base + hh[1]
+        return peers
 
     def push(self, owner, slot, off, src):
         """src (a contiguous f32 slice of the arena) -> owner's receive slot `slot`
@@ -303,16 +323,7 @@ class _DeviceTransport:
         """Every peer's copy of t, IPC-mapped (a collective on first use of t)."""
         key = (t.data_ptr(), t.numel(), t.dtype)
         if key not in self.gmap:
-            h = self.K.ipc_handle(t)
-            allh = [None] * comm.world
-            dist.all_gather_object(allh, h, group=comm.group)
-            peers = {}
-            for r, (hh, off) in enumerate(allh):
-                if r != comm.rank:
-                    base = self.K.ipc_open(hh)
-                    self._opened.append(base)
-                    peers[r] = base + off
-            self.gmap[key] = peers
+            self.gmap[key] = self._exchange(t, comm)
         return self.gmap[key]
 
     def gather(self, t, lo, hi, comm):
@@ -425,25 +436,78 @@ class ShardPusher(GradAllReducer):
                 for t in gather:
                     self.transport.map(t, comm)
 
+    def setup_error(self):
+        """A local failure of the transport's setup (every rank took the same
+        collectives regardless), or None."""
+        return getattr(self.transport, "error", None)
+
+    def _self_test(self, n=256, timeout_s=60.0):
+        """Every rank pushes a marker into its slot of every peer's receive buffer
+        over the real path (IPC mapping + copy engine between devices), then checks
+        the markers its peers pushed.  Raises on a missing or wrong marker, or when
+        the copies have not landed within timeout_s, so that create() falls back to
+        zero1 on every rank instead of the first step training on bad sums."""
+        import time
+        g = self.g
+        src = torch.full((n,), float(self.comm.rank + 1), dtype=torch.float32, device=g.device)
+        for owner in range(self.comm.world):
+            if owner != self.comm.rank:
+                self.transport.push(owner, self.slot(self.comm.rank, owner), 0, src)
+        self.transport.flush()
+        self.transport.sync(self.group)
+        if g.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(g.device))
+            t0 = time.monotonic()
+            while not ev.query():
+                if time.monotonic() - t0 > timeout_s:
+                    raise RuntimeError("zero1_push self-test: copies not landed after %.0f s" % timeout_s)
+                time.sleep(0.001)
+        slots = self.transport.slots(self.n_slots)
+        for k in range(self.n_slots):
+            sender = k if k < self.comm.rank else k + 1
+            got = slots[k, :n]
+            if not bool(torch.all(got == float(sender + 1))):
+                raise RuntimeError("zero1_push self-test: slot %d (from rank %d) holds %s, expected %d"
+                                   % (k, sender, got[:4].tolist(), sender + 1))
+
     @classmethod
     def create(cls, grads, comm, **kw):
         """A ShardPusher, or None on EVERY rank when any rank could not map its
         peers' receive buffers (IPC unavailable): the ranks agree, so they all
         take the same collectives afterwards (the caller falls back to zero1)."""
-        err, red = None, None
-        try:
-            red = cls(grads, comm, **kw)
-        except Exception as e:  # noqa: BLE001 -- any setup failure: agree on the fallback
-            err = e
-        ok = torch.tensor([0.0 if err is not None else 1.0], device=grads.device if grads.is_cuda else "cpu")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=comm.group)
-        if ok.item() < 1.0:
+        dev = grads.device if grads.is_cuda else "cpu"
+
+        def agree(err):
+            ok = torch.tensor([0.0 if err is not None else 1.0], device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=comm.group)
+            return ok.item() >= 1.0
+
+        def fallback(red, err, what):
             if red is not None:
                 red.close()
             import sys
-            print("NSTL_DP=zero1_push: receive buffers not mapped on every rank (%s); falling back to zero1"
-                  % (err or "another rank failed"), file=sys.stderr)
+            print("NSTL_DP=zero1_push: %s on some rank (%s); falling back to zero1"
+                  % (what, err or "another rank failed"), file=sys.stderr)
+
+        err, red = None, None
+        try:
+            red = cls(grads, comm, **kw)
+            err = red.setup_error()
+        except Exception as e:  # noqa: BLE001 -- any setup failure: agree on the fallback
+            err = e
+        if not agree(err):
+            fallback(red, err, "receive buffers not mapped")
             return None
+        if red.active:
+            # the mapped path exercised once (collectives: every rank gets here)
+            try:
+                red._self_test()
+            except Exception as e:  # noqa: BLE001
+                err = e
+            if not agree(err):
+                fallback(red, err, "copy-engine self-test failed")
+                return None
         return red
 
     def slot(self, src_rank, owner):

@@ -278,3 +278,42 @@ def test_reducer_consume_and_abort_bookkeeping_gloo(tmp_path):
     gradients raises instead of counting the other ranks' first micro-batch
     twice."""
     mp.spawn(_reducer_state_worker, args=(_port(), str(tmp_path)), nprocs=WORLD, join=True)
+
+
+def _push_fallback_worker(rank, port, out_dir, world, fail):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from neurosync_trainer_lite_amd import parallel
+    parallel.init_from_env(backend="gloo")
+    ns = 64 * 840
+    comm = parallel.ShardComm(ns)
+    g = torch.zeros(comm.numel)
+    if fail == "self_test" and rank == world - 1:
+        # this rank's markers come out wrong: its peers' checks fail, and so must every rank's setup
+        real_push = parallel._HostTransport.push
+        parallel._HostTransport.push = lambda self, owner, slot, off, src: real_push(self, owner, slot, off, src * 0 - 7)
+    if fail == "setup" and rank == 0:
+        parallel.ShardPusher.setup_error = lambda self: RuntimeError("simulated IPC mapping failure")
+    red = parallel.ShardPusher.create(g, comm, bucket_bytes=4000)
+    # every rank takes the same collectives afterwards, whatever the outcome
+    ok = torch.tensor([1.0 if red is not None else 0.0])
+    dist.all_reduce(ok)
+    torch.save({"made": red is not None, "sum": float(ok)}, os.path.join(out_dir, "f%d.pt" % rank))
+    if red is not None:
+        red.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail", [(2, None), (4, None), (4, "self_test"), (2, "setup")])
+def test_push_setup_agrees_on_fallback_gloo(tmp_path, world, fail):
+    """ShardPusher.create: the transport is set up, then exercised once (every rank
+    pushes a marker into its slot of every peer, then checks its own slots). A
+    setup error or a wrong marker on ANY rank makes create() return None on EVERY
+    rank (the caller falls back to zero1), with no rank left waiting in a
+    collective the others skipped."""
+    mp.spawn(_push_fallback_worker, args=(_port(), str(tmp_path), world, fail), nprocs=world, join=True)
+    res = [torch.load(tmp_path / ("f%d.pt" % r), weights_only=True) for r in range(world)]
+    for r in res:
+        assert r["made"] == (fail is None)
+        assert r["sum"] == (world if fail is None else 0)
