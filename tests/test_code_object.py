@@ -59,3 +59,45 @@ def test_every_kernel_is_gfx950_and_spill_free(tmp_path):
         assert any(must in k for k in kernels), must
     spilling = {k: v for k, v in kernels.items() if v and not ALLOWED.search(k)}
     assert not spilling, "kernels with VGPR spills: %s" % spilling
+
+
+OBJDUMP = os.path.join(LLVM, "llvm-objdump")
+
+
+def test_gemm4_epilogues_have_no_compiler_vmcnt0_before_lds_reads(tmp_path):
+    """The 4-wave GEMM reads its LDS with inline asm wherever an LDS-DMA may be in
+    flight (stage pieces, epilogue side data, RoPE tables: DESIGN.md section 4,
+    "Epilogue inputs off the vmcnt queue").  A plain LDS load there makes the
+    compiler emit `s_waitcnt vmcnt(0)` in front of it: a wait for the next tile's
+    stage pieces and every store before it.  Guard: no gemm4 kernel outside the
+    stream-K tail form has a vmcnt(0) directly ahead of a ds_read."""
+    if not os.path.exists(LIB):
+        pytest.skip("libnstl_hip.so not built")
+    if not (shutil.which("objcopy") and os.path.exists(BUNDLER) and os.path.exists(OBJDUMP)):
+        pytest.skip("objcopy / clang-offload-bundler / llvm-objdump not available")
+    fat = tmp_path / "fatbin.bin"
+    subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=%s" % fat, LIB], check=True, capture_output=True)
+    data = fat.read_bytes()
+    offs = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+    checked, bad = 0, {}
+    for i, o in enumerate(offs):
+        part, co = tmp_path / ("d%d.bin" % i), tmp_path / ("d%d.o" % i)
+        part.write_bytes(data[o:offs[i + 1] if i + 1 < len(offs) else len(data)])
+        subprocess.run([BUNDLER, "--type=o", "--unbundle", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                        "--input=%s" % part, "--output=%s" % co], check=True, capture_output=True)
+        text = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", str(co)], check=True, capture_output=True,
+                              text=True).stdout
+        for block in re.split(r"\n(?=[0-9a-f]+ <)", text):
+            m = re.match(r"[0-9a-f]+ <(.*)>:", block)
+            # gemm4_kernel<AK, BKM, EM, GROUPED, DBG, SK, R3>: skip SK = true (..ELb1ELi<R3>E)
+            if not m or "gemm4_kernel" not in m.group(1) or re.search(r"ELb1ELi[0-9]EEEv", m.group(1)):
+                continue
+            ins = [ln.split("//")[0].strip() for ln in block.split("\n")[1:]]
+            ins = [x for x in ins if x and not x.startswith(";")]
+            n = sum(1 for k in range(len(ins) - 1) if ins[k].startswith("s_waitcnt") and "vmcnt(0)" in ins[k]
+                    and any(x.startswith("ds_read") for x in ins[k + 1:k + 3]))
+            checked += 1
+            if n:
+                bad[m.group(1)] = n
+    assert checked >= 10, checked
+    assert not bad, bad
