@@ -397,9 +397,27 @@ NSTL_DEV int64_t mask_word(int N, int row, int col) {
   return ((int64_t)(row >> 6) * 8 + (row & 7)) * ((N + 7) >> 3) + (col >> 3);
 }
 
-// the wave's side data of its 128 x 128 block (row0, col0) (see SIDE_W)
-template <int EM>
+// the fp8 kernel's side area (SC): its row and column scales first (1 KB each,
+// the wave's 128 in the first 512 B), then the bias / keep-bit words
+constexpr int SIDE_SC_OFF = 2048;
+constexpr int SIDE_W_SC = SIDE_SC_OFF + SIDE_W;
+
+// the wave's side data of its 128 x 128 block (row0, col0) (see SIDE_W); SC: the
+// fp8 scales too, and the rest at SIDE_SC_OFF
+template <int EM, bool SC = false>
 NSTL_DEV void side_dma(const Params& p, char* side, int row0, int col0, int lane) {
+  if constexpr (SC) {
+    // 128 row scales from lanes 0..31 (lanes 32..63: the next 128, zeros past M)
+    const __amdgpu_buffer_rsrc_t ra =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.a_scale, 0, (int)((uint32_t)p.M * 4u), 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)side, 16, (uint32_t)lane * 16u,
+                                             __builtin_amdgcn_readfirstlane((uint32_t)row0 * 4u), 0, 0);
+    const __amdgpu_buffer_rsrc_t rb =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.b_scale, 0, (int)((uint32_t)p.N * 4u), 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(side + 1024), 16, (uint32_t)lane * 16u,
+                                             __builtin_amdgcn_readfirstlane((uint32_t)col0 * 4u), 0, 0);
+    side += SIDE_SC_OFF;
+  }
   if constexpr (EM == EM_DRELU) {
     // 2 x 8 rows of 16 words (128 B): lane l of piece j loads words 2 (l & 7),
     // + 1 of row (j, l >> 3)
@@ -645,7 +663,23 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
   s16x4 z = {};
   if constexpr (ZW == 2) z = zero_operand();
   float rsc[8], csc[8][4];  // SC: the lane's row scales (times alpha) and column scales
-  if constexpr (SC) {
+  if constexpr (SC && SIDE) {  // side_dma's copies (SIDE_SC_OFF), read by asm
+    const uint32_t ra = lds_addr(side + 4 * c), cb = lds_addr(side + 1024 + 16 * g);
+    float rv[8];
+    f32x4 cv[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(rv[a]) : "v"(ra), "i"(64 * a));
+#pragma unroll
+    for (int b = 0; b < 8; ++b) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(cv[b]) : "v"(cb), "i"(64 * b));
+    G4_LGKM0();
+#pragma unroll
+    for (int a = 0; a < 8; ++a) rsc[a] = rv[a] * alpha;
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csc[b][e] = cv[b][e];
+    side += SIDE_SC_OFF;
+  } else if constexpr (SC) {
 #pragma unroll
     for (int a = 0; a < 8; ++a) rsc[a] = p.a_scale[row0 + 16 * a + c] * alpha;
 #pragma unroll
@@ -1283,7 +1317,10 @@ NSTL_DEV void half_step_f8(f32x4 (&acc)[8][8], const i32x8_t (&ca)[4], i32x8_t (
 // the table fits ROPE_LDS as f32 or (rope_bf16) as bf16.
 template <int EM, int DBG = 0>
 __global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + (EM == EM_ROPE ? ROPE_LDS : 0)];
+  // epilogue side data (scales, bias / keep-bit words: side_dma<EM, true>); not
+  // with the RoPE table (no LDS left)
+  constexpr bool SIDE = EM != EM_ROPE && EM != EM_F32 && !(DBG & 16384);
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + (EM == EM_ROPE ? ROPE_LDS : 0) + (SIDE ? 4 * SIDE_W_SC : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -1298,6 +1335,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
   char* const adst0 = smem + wave * 8 * 1024;
   char* const bdst0 = smem + 2 * OPS + wave * 8 * 1024;
   const char* rope_lds = smem + SMEM;
+  char* const side = smem + SMEM + wave * SIDE_W_SC;  // SIDE
   if constexpr (EM == EM_ROPE) {
     const int half = p.rope_dim >> 1, chunks = p.rope_dim >> 2, swz = rope_swz(p.rope_dim);
     for (int i = tid; i < p.rope_T * chunks; i += NT) {
@@ -1378,6 +1416,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
     if (!has_next) ns = sg;
     int nm0 = m0, nn0 = n0;
     if (has_next) tile_coords(xcd_remap(ns.t, T), p.tiles_m, p.tiles_n, nm0, nn0);
+    if constexpr (SIDE) side_dma<EM, true>(p, side, m0 + wm * 128, n0 + wn * 128, lane);
     step(S0{}, WE{}, 2u);
     for (int kt = 1; kt < nk; kt += 2) {
       step(S1{}, W0{}, (uint32_t)(kt + 2 < nk ? kt + 2 : kt + 2 - nk));
@@ -1388,7 +1427,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4f8_kernel(const GroupParams gp) {
     }
     G4_LGKM0();  // the next tile's last B fragment: before the epilogue's own LDS reads
     lt = sg.t < T ? xcd_remap(sg.t, T) : sg.t;
-    epilogue<EM, true, (DBG & 8192) ? 1 : 0, 0>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, true);
+    epilogue<EM, true, (DBG & 8192) ? 1 : 0, 0, SIDE>(p, acc, m0 + wm * 128, n0 + wn * 128, lane, wave, lt, rope_lds, true,
+                                                     side);
     if (!has_next) break;
     if constexpr (EM != EM_BF16) {
       // the per-lane DMA offsets and read addresses, recomputed after every
