@@ -4,11 +4,12 @@
 //   hipcc -O3 --offload-arch=gfx950 -o tools/micro/valu_rate tools/micro/valu_rate.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define REP16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
 template <int OP>
-__global__ __launch_bounds__(64) void rate(unsigned* out, unsigned seed, int iters) {
+__global__ __launch_bounds__(512) void rate(unsigned* out, unsigned seed, int iters) {
   unsigned v[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) v[i] = seed + threadIdx.x * 16 + i;
@@ -34,7 +35,9 @@ __global__ __launch_bounds__(64) void rate(unsigned* out, unsigned seed, int ite
   }
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // argv[1]: waves per workgroup (one workgroup per CU: 1 = one wave alone on a SIMD, 8 = two per SIMD)
+  const int waves = argc > 1 ? atoi(argv[1]) : 1;
   unsigned* d;
   hipMalloc(&d, 2 * 256 * sizeof(unsigned));
   unsigned h[512];
@@ -43,12 +46,12 @@ int main() {
   void (*ks[])(unsigned*, unsigned, int) = {rate<0>, rate<1>, rate<2>, rate<3>, rate<4>};
   for (int rep = 0; rep < 2; ++rep)
     for (int k = 0; k < 5; ++k) {
-      hipLaunchKernelGGL(ks[k], dim3(256), dim3(64), 0, 0, d, 12345u + rep, iters);
+      hipLaunchKernelGGL(ks[k], dim3(256), dim3(64 * waves), 0, 0, d, 12345u + rep, iters);
       hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
       double s = 0;
       for (int b = 0; b < 256; ++b) s += h[2 * b];
       // s_memtime counts at the shader clock
-      printf("rep %d  %-26s %6.2f cycles per instruction (one wave per SIMD)\n", rep, names[k],
+      printf("rep %d  %d waves/CU  %-26s %6.2f cycles per instruction and wave\n", rep, waves, names[k],
              s / 256.0 / ((double)iters * 16 * (k == 4 ? 2 : 1)));
     }
   return 0;
