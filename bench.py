@@ -8,7 +8,14 @@ bf16 compute, dropout 0.3 on, synthetic seeded inputs of the reference shapes
 (features [B,T,256] f32, targets [B,T,61] f32, already resident in HBM).
 
   python bench.py [--gpus N --steps K --warmup W]
-  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+N>1: started as `python bench.py --gpus N`, this process touches no GPU and
+runs `python -m torch.distributed.run --nnodes 1 --nproc-per-node N
+--master-addr 127.0.0.1 ... bench.py ...` as a child, relaying rank 0's line
+(launch_ranks); started by torchrun itself (WORLD_SIZE set), it is one rank, and
+WORLD_SIZE must equal --gpus.  Under the self-launch, a first attempt with the
+default exchange (NSTL_DP=zero1_push) that fails or stalls is followed by one
+with NSTL_DP=zero1, and the line records both (`launch.attempts`).
 
 Prints ONE JSON line on rank 0.  `roofline` is measured live for the dominant
 kernel (nstl GEMM: ~97% of the step's FLOPs): HIP events around every GEMM launch
@@ -363,7 +370,121 @@ def fwd_parity(cfg, dev, T, windows=2):
     return out
 
 
-def main():
+def rank_launch_cmd(args, argv, port):
+    """The torch.distributed.run command that starts args.gpus ranks of this
+    bench on one node (the form the reference's ≤4-replica loop becomes: one
+    process per GPU, /root/reference/train.py:62-78)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run_ranks(cmd, env, stall_s, limit_s):
+    """Run the rank launcher as a child process group: stderr relayed line by
+    line, stdout collected.  Killed (the whole group) after stall_s seconds
+    without a line on either stream, or after limit_s.  Returns (rc or None if
+    killed, stdout lines, last stderr lines, why killed)."""
+    import signal
+    import subprocess
+    import threading
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    out, tail, last = [], [], [time.monotonic()]
+
+    def pump(src, sink):
+        for line in src:
+            last[0] = time.monotonic()
+            sink(line)
+
+    def err_line(line):
+        sys.stderr.write(line)
+        sys.stderr.flush()
+        tail.append(line.rstrip())
+        del tail[:-30]
+    ts = [threading.Thread(target=pump, args=(p.stdout, out.append), daemon=True),
+          threading.Thread(target=pump, args=(p.stderr, err_line), daemon=True)]
+    for t in ts:
+        t.start()
+    t0, why = time.monotonic(), None
+    while p.poll() is None:
+        time.sleep(0.5)
+        now = time.monotonic()
+        if now - last[0] > stall_s:
+            why = "no output for %.0f s" % stall_s
+        elif now - t0 > limit_s:
+            why = "over the %.0f s limit" % limit_s
+        if why:
+            log("rank launcher %s: stopping its process group" % why)
+            for sig, wait in ((signal.SIGTERM, 20), (signal.SIGKILL, 10)):
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    break
+                try:
+                    p.wait(wait)
+                    break
+                except subprocess.TimeoutExpired:
+                    continue
+            break
+    for t in ts:
+        t.join(5)
+    return (None if why else p.returncode), out, tail, why
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` (N > 1) without torchrun's environment: start the N
+    ranks as a child torch.distributed.run (before this process makes any GPU
+    call: torch.cuda.device_count() does not initialise HIP here), relay rank
+    0's JSON line with `launch` added, and return the exit code.  With NSTL_DP
+    unset the first attempt runs the default exchange (zero1_push, whose
+    cross-device copy path first executes on a multi-GPU node); if it fails or
+    stalls, a second attempt runs NSTL_DP=zero1 and the line says so
+    (config.dp_fallback)."""
+    n_dev = torch.cuda.device_count()
+    if n_dev < args.gpus:
+        log("--gpus %d needs %d GPUs on this node; %d visible" % (args.gpus, args.gpus, n_dev))
+        return 2
+    modes = [os.environ["NSTL_DP"]] if os.environ.get("NSTL_DP") else ["zero1_push", "zero1"]
+    attempts, line = [], None
+    for mode in modes:
+        cmd = rank_launch_cmd(args, argv, _free_port())
+        env = dict(os.environ, NSTL_DP=mode, NSTL_BENCH_SELF_LAUNCH="1", MASTER_ADDR="127.0.0.1")
+        log("starting %d ranks (NSTL_DP=%s): %s" % (args.gpus, mode, " ".join(cmd)))
+        t0 = time.monotonic()
+        rc, out, tail, why = _run_ranks(cmd, env, args.launch_stall_s, args.launch_limit_s)
+        js = [ln for ln in out if ln.lstrip().startswith("{")]
+        att = {"NSTL_DP": mode, "rc": rc, "s": round(time.monotonic() - t0, 1)}
+        if rc == 0 and js:
+            attempts.append(att)
+            line = json.loads(js[-1])
+            break
+        att["failure"] = why or ("exit %s" % rc if rc else "no JSON line from rank 0")
+        att["stderr_tail"] = tail[-6:]
+        attempts.append(att)
+        log("attempt NSTL_DP=%s failed: %s" % (mode, att["failure"]))
+    if line is None:
+        print(json.dumps({"metric": "train frames/sec (audio->blendshape) 228M cfg", "value": None,
+                          "n_gpus": args.gpus, "error": "every rank-launch attempt failed",
+                          "launch": {"attempts": attempts}}), flush=True)
+        return 1
+    line["launch"] = {"how": "bench.py --gpus %d started torch.distributed.run --nproc-per-node %d as a child"
+                             % (args.gpus, args.gpus), "attempts": attempts}
+    if len(attempts) > 1:
+        line["config"]["dp_fallback"] = "NSTL_DP=%s attempt failed (%s); measured with NSTL_DP=%s" % (
+            attempts[0]["NSTL_DP"], attempts[0]["failure"], attempts[-1]["NSTL_DP"])
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -388,12 +509,25 @@ def main():
                          "C5 also doubles the clip length: --seq 256 --batch 64")
     ap.add_argument("--fp8-bwd", action="store_true",
                     help="with --fp8: every FFN linear2 input-gradient GEMM on e4m3 operands too")
-    args = ap.parse_args()
+    ap.add_argument("--launch-stall-s", type=float, default=300.0,
+                    help="--gpus N self-launch: an attempt with no output line for this long is stopped")
+    ap.add_argument("--launch-limit-s", type=float, default=1500.0,
+                    help="--gpus N self-launch: an attempt running longer than this is stopped")
+    args = ap.parse_args(argv)
+
+    env_world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if env_world == 0 and args.gpus > 1:
+        # N ranks wanted and not started by torchrun: start them (no GPU call here)
+        sys.exit(launch_ranks(args, sys.argv[1:] if argv is None else argv))
+    if env_world and env_world != args.gpus:
+        raise SystemExit("bench.py --gpus %d, but this rank was started in a world of %d (WORLD_SIZE): pass "
+                         "--gpus %d or start %d ranks" % (args.gpus, env_world, env_world, args.gpus))
 
     from neurosync_trainer_lite_amd import _hip as K
     from neurosync_trainer_lite_amd import parallel
     from neurosync_trainer_lite_amd.config import training_config
     from neurosync_trainer_lite_amd.utils.model_utils import build_model, prepare_training_components
+    from neurosync_trainer_lite_amd.utils.training_utils import gradient_exchange
 
     # PMC traffic passes first: child processes, started before this one touches the GPU
     traffic, traffic_src, mfma_busy = None, "skipped (--no-traffic or n>1)", None
@@ -402,6 +536,8 @@ def main():
         counters = measure_gemm_counters(args)
         traffic, traffic_src, mfma_busy = counters["traffic"], counters["note"], counters["mfma_busy"]
     rank, world, local = parallel.init_from_env()
+    if world != args.gpus:
+        raise SystemExit("bench.py --gpus %d ran in a world of %d" % (args.gpus, world))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = dict(training_config)
@@ -526,8 +662,12 @@ def main():
     elapsed = time.perf_counter() - t0
     K.gemm = real_gemm
     K.gemm_grouped = real_grouped
+    rank_ms = None
     if world > 1:
         tt = torch.tensor([elapsed], device=dev)
+        per = [torch.zeros(1, device=dev) for _ in range(world)]
+        torch.distributed.all_gather(per, tt)
+        rank_ms = [round(float(x) / args.steps * 1e3, 3) for x in per]
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = tt.item()
     log("timed %d steps in %.3fs" % (args.steps, elapsed))
@@ -708,9 +848,8 @@ def main():
             "config": {"workload": "228M Seq2Seq train step (L8/H16/D1024, dropout 0.3, clip+Adam)",
                        "model": "NeuroSync Seq2Seq 228M", "global_batch": B * world, "seq_len": T,
                        "frames_per_step": B * T * world, "parallelism": "dp%d" % world,
-                       "gradient_exchange": (None if world == 1 else
-                                             type(eng.grad_reducer).__name__ if eng.grad_reducer is not None
-                                             else "zero1 (reduce-scatter after backward)")},
+                       "gradient_exchange": gradient_exchange(model, opt),
+                       "dp_fallback": (None if world == 1 else opt.dp_fallback or False)},
             "roofline": {"bound": "mfma", "kernel": "nstl GEMM family, all hand-written: gemm4_kernel (4-wave persistent "
                                                     "256^2: every full-tile forward / dX / grouped dW), gemm256r_kernel "
                                                     "(8-wave ring: f32 beta-1 dX, the memory gradient), gemm_kernel "
@@ -729,6 +868,13 @@ def main():
             "step_mfma_frac": round(step_tf / BF16_DENSE_PEAK_TFLOPS, 4),
             "final_loss": round(loss_v, 4),
         }
+        if world > 1:
+            out["dist"] = {"backend": torch.distributed.get_backend(), "world_size": torch.distributed.get_world_size(),
+                           "launch": ("bench.py self-launch (torch.distributed.run child)"
+                                      if os.environ.get("NSTL_BENCH_SELF_LAUNCH") == "1" else "external torchrun"),
+                           "rank_ms_per_step": rank_ms,
+                           "rank_spread_pct": round((max(rank_ms) / min(rank_ms) - 1) * 100, 2),
+                           "exchange_check": opt.dp_check}
         fam_traffic = counters.get("traffic_by_family") or {}
         for fam, d in by_family.items():
             t = fam_traffic.get(fam)

@@ -8,6 +8,7 @@
 
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "../../include/nstl.h"
 #include "common.h"
@@ -40,32 +41,26 @@ struct SkSpace {
   unsigned* cnt = nullptr;
   int G = 0;
 };
-// At most SK_SPACES of them (2 G x 256 KB each, 128 MB at G = 256): a new
-// stream past that synchronizes the devices and frees the others (stream-K is
-// opt-in; streams that launch it are few and long-lived).
+// At most SK_SPACES of them (2 G x 256 KB each, 128 MB at G = 256).  Nothing
+// is ever freed on the launch path: a space handed out may still be waiting
+// for its launch on another host thread, and a free there would also break
+// stream capture.  So a new stream past SK_SPACES gets no space (its launches
+// run whole tiles), and a space outgrown by a larger grid is retired, not
+// freed (grids change only with a stream's CU mask; stream-K is opt-in).
 constexpr size_t SK_SPACES = 4;
 bool sk_space(hipStream_t st, int G, g4::StreamK& sk) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, SkSpace> spaces;
+  static std::vector<SkSpace> retired;
   const int dev = nstl::stream_device(st);  // the stream's device, not the current one
   std::lock_guard<std::mutex> lk(mu);
-  if (spaces.find({dev, st}) == spaces.end() && spaces.size() >= SK_SPACES) {
-    for (auto& kv : spaces) {
-      nstl::DeviceGuard on(kv.first.first);
-      if (hipDeviceSynchronize() != hipSuccess) return false;
-      if (kv.second.slab) (void)hipFree(kv.second.slab);
-      if (kv.second.cnt) (void)hipFree(kv.second.cnt);
-    }
-    spaces.clear();
-  }
+  if (spaces.find({dev, st}) == spaces.end() && spaces.size() >= SK_SPACES) return false;
   SkSpace& s = spaces[{dev, st}];
   if (s.G < G) {
     nstl::DeviceGuard on(dev);
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
-    if (hipStreamSynchronize(st) != hipSuccess) return false;  // the old space may be in use
-    if (s.slab) (void)hipFree(s.slab);
-    if (s.cnt) (void)hipFree(s.cnt);
+    if (s.slab) retired.push_back(s);
     s = SkSpace();
     if (hipMalloc((void**)&s.slab, (size_t)2 * G * 262144) != hipSuccess) return false;
     if (hipMalloc((void**)&s.cnt, (size_t)8 * G * sizeof(unsigned)) != hipSuccess) return false;

@@ -53,6 +53,10 @@ import torch.distributed as dist
 DEFAULT_BUCKET_BYTES = 64 << 20
 
 
+class PushTimeout(RuntimeError):
+    """A copy-engine copy of the zero1_push exchange did not complete in time."""
+
+
 def init_from_env(backend=None):
     """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK).
     Returns (rank, world, local_rank); (0, 1, 0) when not launched distributed."""
@@ -269,37 +273,54 @@ class _DeviceTransport:
         from . import _hip as K
         self.K = K
         self.shard = comm.shard
-        self.recv = torch.empty(max(1, n_slots) * comm.shard, dtype=torch.float32, device=grads.device)
-        n = max(1, min(push_streams(), comm.world - 1))
-        pool = [torch.cuda.Stream(grads.device) for _ in range(n)]
-        self.sides = {r: pool[r % n] for r in range(comm.world) if r != comm.rank}
-        # the weight all-gather runs alone between the optimizer and the next
-        # forward (no compute beside it to disturb): one stream per peer, so the
-        # seven copies travel seven links at once
-        self.gsides = {r: torch.cuda.Stream(grads.device) for r in range(comm.world) if r != comm.rank}
-        self._pool = pool + list(self.gsides.values())
         self.gmap = {}
         self._opened = []
+        self.sides, self.gsides, self._pool, self.recv = {}, {}, [], None
         # a local failure is recorded, not raised, until every rank has taken the
-        # same collectives (ShardPusher raises it afterwards; create() agrees)
+        # same collectives (ShardPusher raises it afterwards; create() agrees):
+        # a rank whose receive buffer or streams cannot be made (e.g. out of
+        # memory: (world - 1) f32 shards, ~0.8 GB at 8 ranks) still takes the
+        # handle exchange, with no handle of its own
         self.error = None
+        try:
+            self.recv = torch.empty(max(1, n_slots) * comm.shard, dtype=torch.float32, device=grads.device)
+            n = max(1, min(push_streams(), comm.world - 1))
+            pool = [torch.cuda.Stream(grads.device) for _ in range(n)]
+            self.sides = {r: pool[r % n] for r in range(comm.world) if r != comm.rank}
+            # the weight all-gather runs alone between the optimizer and the next
+            # forward (no compute beside it to disturb): one stream per peer, so the
+            # seven copies travel seven links at once
+            self.gsides = {r: torch.cuda.Stream(grads.device) for r in range(comm.world) if r != comm.rank}
+            self._pool = pool + list(self.gsides.values())
+        except Exception as e:  # noqa: BLE001
+            self.error = e
+        self.device = grads.device
         self.peer = self._exchange(self.recv, comm)
 
     def _exchange(self, t, comm):
         """IPC handle of t to every rank, every peer's t mapped here (a collective;
-        failures recorded in self.error)."""
-        try:
-            mine = self.K.ipc_handle(t)
-        except Exception as e:  # noqa: BLE001
-            mine, self.error = None, self.error or e
+        failures recorded in self.error).  Before a peer on another device is
+        mapped, hipDeviceCanAccessPeer must allow this device to reach it (the
+        copy engines write over xGMI into the mapping)."""
+        mine = None
+        if t is not None:
+            try:
+                mine = self.K.ipc_handle(t) + (t.device.index,)
+            except Exception as e:  # noqa: BLE001
+                mine, self.error = None, self.error or e
         allh = [None] * comm.world
         dist.all_gather_object(allh, mine, group=comm.group)
         peers = {}
+        here = self.device.index
         for r, hh in enumerate(allh):
             if r == comm.rank:
                 continue
             if hh is None:
                 self.error = self.error or RuntimeError("rank %d has no IPC handle" % r)
+                continue
+            if hh[2] != here and not torch.cuda.can_device_access_peer(here, hh[2]):
+                self.error = self.error or RuntimeError("hipDeviceCanAccessPeer(%d, %d) = 0: rank %d's memory is "
+                                                        "not reachable from this device" % (here, hh[2], r))
                 continue
             try:
                 base = self.K.ipc_open(hh[0])
@@ -314,10 +335,28 @@ class _DeviceTransport:
         """src (a contiguous f32 slice of the arena) -> owner's receive slot `slot`
         at element offset `off`; ordered after the work queued on the current
         stream so far."""
+        if off < 0 or off + src.numel() > self.shard:
+            raise ValueError("push of %d elements at %d leaves the %d-element slot" % (src.numel(), off, self.shard))
         side = self.sides[owner]
         side.wait_stream(torch.cuda.current_stream(src.device))
         dst = self.peer[owner] + (slot * self.shard + off) * 4
         self.K.copy_engine(dst, src, src.numel() * 4, stream=side.cuda_stream)
+
+    def mark(self):
+        """[(event, peers)]: an event recorded on every copy stream now, with the
+        peers whose copies that stream carries (pending() names them)."""
+        out = []
+        for st in self._pool:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            out.append((ev, sorted(r for r, s in list(self.sides.items()) + list(self.gsides.items()) if s is st)))
+        return out
+
+    @staticmethod
+    def pending(marks):
+        """The peers whose copies behind `marks` have not completed (a host-side
+        query: nothing waits)."""
+        return sorted({r for ev, peers in marks if not ev.query() for r in peers})
 
     def map(self, t, comm):
         """Every peer's copy of t, IPC-mapped (a collective on first use of t)."""
@@ -341,7 +380,7 @@ class _DeviceTransport:
             self.K.copy_engine(base + lo * esz, t[lo:hi], (hi - lo) * esz, stream=side.cuda_stream)
 
     def flush(self):
-        cur = torch.cuda.current_stream(self.recv.device)
+        cur = torch.cuda.current_stream(self.device)
         for side in self._pool:
             cur.wait_stream(side)
 
@@ -350,9 +389,9 @@ class _DeviceTransport:
         if dist.get_backend(group) == "nccl":
             # stream-ordered: each rank's all-reduce starts after its own pushes
             # (flush) and ends after every rank's has started
-            dist.all_reduce(torch.zeros(1, device=self.recv.device), group=group)
+            dist.all_reduce(torch.zeros(1, device=self.device), group=group)
         else:
-            torch.cuda.current_stream(self.recv.device).synchronize()
+            torch.cuda.current_stream(self.device).synchronize()
             dist.barrier(group=group)
 
     def slots(self, n_slots):
@@ -374,19 +413,40 @@ class _HostTransport:
         dist.broadcast_object_list(tag, src=dist.get_global_rank(comm.group, 0) if comm.group is not None else 0,
                                    group=comm.group)
         self.shard = comm.shard
+        self.error = None
         n = max(1, n_slots) * comm.shard
         self.paths = {r: "/dev/shm/nstl_push_%s_%d" % (tag[0], r) for r in range(comm.world)}
-        self.recv = torch.from_file(self.paths[comm.rank], shared=True, size=n, dtype=torch.float32)
+        self.recv, self.peer = None, {}
+        # failures are recorded, and every rank still takes both barriers
+        # (create() agrees on the outcome afterwards)
+        try:
+            self.recv = torch.from_file(self.paths[comm.rank], shared=True, size=n, dtype=torch.float32)
+        except Exception as e:  # noqa: BLE001
+            self.error = e
         dist.barrier(group=comm.group)
-        self.peer = {r: torch.from_file(p, shared=True, size=n, dtype=torch.float32)
-                     for r, p in self.paths.items() if r != comm.rank}
+        for r, p in self.paths.items():
+            if r == comm.rank:
+                continue
+            try:
+                self.peer[r] = torch.from_file(p, shared=True, size=n, dtype=torch.float32)
+            except Exception as e:  # noqa: BLE001
+                self.error = self.error or e
         dist.barrier(group=comm.group)
-        import os as _os
-        _os.unlink(self.paths[comm.rank])  # mapped by every rank: the memory stays until they exit
+        if self.recv is not None:
+            os.unlink(self.paths[comm.rank])  # mapped by every rank: the memory stays until they exit
 
     def push(self, owner, slot, off, src):
+        if off < 0 or off + src.numel() > self.shard:
+            raise ValueError("push of %d elements at %d leaves the %d-element slot" % (src.numel(), off, self.shard))
         o = slot * self.shard + off
         self.peer[owner][o:o + src.numel()].copy_(src)
+
+    def mark(self):
+        return []  # the copies above are synchronous
+
+    @staticmethod
+    def pending(marks):
+        return []
 
     def flush(self):
         pass
@@ -441,28 +501,41 @@ class ShardPusher(GradAllReducer):
         collectives regardless), or None."""
         return getattr(self.transport, "error", None)
 
-    def _self_test(self, n=256, timeout_s=60.0):
+    def _self_test(self, n=256, timeout_s=None):
         """Every rank pushes a marker into its slot of every peer's receive buffer
         over the real path (IPC mapping + copy engine between devices), then checks
-        the markers its peers pushed.  Raises on a missing or wrong marker, or when
-        the copies have not landed within timeout_s, so that create() falls back to
-        zero1 on every rank instead of the first step training on bad sums."""
+        the markers its peers pushed.  Raises on a missing or wrong marker, so that
+        create() falls back to zero1 on every rank instead of the first step
+        training on bad sums.
+
+        The copies are watched from the host before anything is chained behind
+        them: events recorded on the copy streams are polled against the deadline
+        (NSTL_PUSH_TIMEOUT_S, 60 s), and only once they have completed does the
+        compute stream join the copy streams and the ranks sync.  A copy that has
+        not landed by then raises PushTimeout naming the peers it was for: a copy
+        queue that does not drain cannot be trusted by this process, so create()
+        does not fall back but lets it end the process (non-zero exit)."""
         import time
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("NSTL_PUSH_TIMEOUT_S", "60"))
+        n = min(n, self.comm.shard)
         g = self.g
         src = torch.full((n,), float(self.comm.rank + 1), dtype=torch.float32, device=g.device)
         for owner in range(self.comm.world):
             if owner != self.comm.rank:
                 self.transport.push(owner, self.slot(self.comm.rank, owner), 0, src)
+        marks = self.transport.mark()
+        t0 = time.monotonic()
+        while True:
+            stuck = self.transport.pending(marks)
+            if not stuck:
+                break
+            if time.monotonic() - t0 > timeout_s:
+                raise PushTimeout("zero1_push self-test on rank %d: copy-engine copies to rank(s) %s not landed "
+                                  "after %.0f s" % (self.comm.rank, stuck, timeout_s))
+            time.sleep(0.001)
         self.transport.flush()
         self.transport.sync(self.group)
-        if g.is_cuda:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(g.device))
-            t0 = time.monotonic()
-            while not ev.query():
-                if time.monotonic() - t0 > timeout_s:
-                    raise RuntimeError("zero1_push self-test: copies not landed after %.0f s" % timeout_s)
-                time.sleep(0.001)
         slots = self.transport.slots(self.n_slots)
         for k in range(self.n_slots):
             sender = k if k < self.comm.rank else k + 1
@@ -474,8 +547,10 @@ class ShardPusher(GradAllReducer):
     @classmethod
     def create(cls, grads, comm, **kw):
         """A ShardPusher, or None on EVERY rank when any rank could not map its
-        peers' receive buffers (IPC unavailable): the ranks agree, so they all
-        take the same collectives afterwards (the caller falls back to zero1)."""
+        peers' receive buffers (IPC unavailable) or its self-test markers came out
+        wrong: the ranks agree, so they all take the same collectives afterwards
+        (the caller falls back to zero1).  A copy that never lands raises
+        PushTimeout instead (see _self_test)."""
         dev = grads.device if grads.is_cuda else "cpu"
 
         def agree(err):
@@ -503,6 +578,8 @@ class ShardPusher(GradAllReducer):
             # the mapped path exercised once (collectives: every rank gets here)
             try:
                 red._self_test()
+            except PushTimeout:
+                raise
             except Exception as e:  # noqa: BLE001
                 err = e
             if not agree(err):
@@ -515,11 +592,52 @@ class ShardPusher(GradAllReducer):
         return src_rank if src_rank < owner else src_rank - 1
 
     def begin(self, fresh):
-        # no accumulation check: pushes overwrite the slots (see the class doc)
+        # no accumulation check: pushes overwrite the slots (see the class doc).
+        # Copies an aborted backward left in flight still read the arena the new
+        # backward is about to overwrite: the compute stream waits for them first.
         if not self.active:
             return
+        self.transport.flush()
         self.reset()
         self.completed = False
+
+    # the first step's pushed shard sums are checked against RCCL's reduce-scatter
+    # of the same arena (NSTL_PUSH_VERIFY=0: not)
+    verify_pending = os.environ.get("NSTL_PUSH_VERIFY", "1") != "0"
+    failed = False
+    check = None
+
+    def verify(self, g_full, g_shard, partial, sumsq_fn, rtol=1e-4):
+        """g_shard (own slice + the pushed slots, nstl_shard_sum) against the
+        reduce-scatter of the same gradient arena, once (the first step): the
+        copies cross devices only on a multi-GPU node, so this is where per-step
+        ordering of pushes, sync and owner reads is checked on the hardware.
+        The sums add the same f32 terms in another order, so they agree to
+        rounding (|diff| <= rtol * max|sum|); a lost or stale slice is off by a
+        whole contribution.  The ranks agree on the outcome; on a mismatch this
+        step continues with the reduce-scatter's shard (and partial sums of
+        squares) and self.failed is set: the step's caller then runs zero1.
+        Returns whether the pushed sums were right (on every rank)."""
+        self.verify_pending = False
+        ref = torch.empty_like(g_shard)
+        self.comm.reduce_scatter(g_full[:self.comm.numel], ref)
+        diff = float((g_shard - ref).abs().max())
+        scale = float(ref.abs().max())
+        ok_here = diff <= rtol * scale
+        flag = torch.tensor([1.0 if ok_here else 0.0], device=g_shard.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        ok = flag.item() >= 1.0
+        self.check = {"max_abs_diff": diff, "max_abs": scale, "rtol": rtol, "ok": ok,
+                      "what": "first step: pushed shard sums vs reduce-scatter of the same arena"}
+        if not ok:
+            import sys
+            print("NSTL_DP=zero1_push: pushed shard sums differ from the reduce-scatter (rank %d: max |diff| %.3g of "
+                  "max %.3g); this step uses the reduce-scatter, later steps run zero1" % (self.comm.rank, diff, scale),
+                  file=sys.stderr)
+            g_shard.copy_(ref)
+            sumsq_fn(g_shard, partial)
+            self.failed = True
+        return ok
 
     def ready(self, upto):
         if not self.active:

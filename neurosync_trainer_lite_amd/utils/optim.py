@@ -53,6 +53,11 @@ class FusedAdam(torch.optim.Optimizer):
         self.trust_backward_norm = False
         self._overlap_allowed = os.environ.get("NSTL_ADAM_OVERLAP", "0") == "1"
         self._upd_stream = None
+        # why the data-parallel exchange left NSTL_DP=zero1_push for zero1, if it did
+        # (attach_data_parallel at setup, ShardPusher.verify at the first step)
+        self.dp_fallback = None
+        # the first step's check of the pushed shard sums (ShardPusher.verify)
+        self.dp_check = None
 
     # --------------------------------------------------------------- arena
     def _bind(self):
@@ -216,19 +221,35 @@ class FusedAdam(torch.optim.Optimizer):
         sum_fn = gather_fn = None
         if isinstance(red, parallel.ShardPusher) and red.active:
             # the updated bf16 shard goes to the peers by the copy engines too
-            gather_fn = red.all_gather
+            # (unless this step's check of the pushed sums failed: then the
+            # collective, as zero1)
+            comm = self._comm
+
+            def gather_fn(tensors):
+                if red.failed:
+                    for t in tensors:
+                        comm.all_gather(t[:comm.numel])
+                else:
+                    red.all_gather(tensors)
         if isinstance(red, parallel.ShardPusher) and red.active and red.consume():
             # the other ranks' slices arrived in this rank's receive slots during
             # backward (copy engines): own + slots and the clip norm's partials
             # in one pass (nstl_shard_sum), instead of reduce-scatter + sumsq
-            comm = self._comm
-
             def sum_fn(g_shard, partial):
                 K.shard_sum(eng.g32[comm.lo:comm.hi], red.slots(), red.n_slots, g_shard, partial, N_PARTIAL,
                             stream=st)
+                if red.verify_pending:
+                    red.verify(eng.g32, g_shard, partial, sumsq_fn)
+                    self.dp_check = red.check
         parallel.zero1_step(self._comm, eng.g32, self._gs, self.partial, sumsq_fn, adam_fn,
                             [eng.p16] if eng.p16 is not eng.p32 else [eng.p32], tail=(eng.n_shardable, eng.numel),
                             reduced=reduced, sum_fn=sum_fn, gather_fn=gather_fn)
+        if isinstance(red, parallel.ShardPusher) and red.failed:
+            # every rank agreed the pushed sums were wrong (ShardPusher.verify):
+            # from the next step on, the reduce-scatter
+            red.close()
+            eng.grad_reducer = None
+            self.dp_fallback = "zero1_push -> zero1 (pushed shard sums differed from the reduce-scatter)"
         eng.master_stale = eng.p16 is not eng.p32
         self._moments_stale = True
         self._snapshot_norm(max_norm)

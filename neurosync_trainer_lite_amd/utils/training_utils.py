@@ -210,10 +210,26 @@ def attach_data_parallel(model, optimizer, world):
             # sharded step all-gathers (parallel.zero1_step)
             eng.grad_reducer = ShardPusher.create(eng.g32, optimizer._comm,
                                                   gather=[eng.p16 if eng.p16 is not eng.p32 else eng.p32])
+            if eng.grad_reducer is None:
+                optimizer.dp_fallback = "zero1_push -> zero1 (setup: IPC mapping or copy-engine self-test failed)"
         elif mode == "zero1_overlap":
             from ..parallel import GradShardReducer, cede_cus
             cede_cus(int(os.environ.get("NSTL_CEDE_CUS", "32")), eng.device)
             eng.grad_reducer = GradShardReducer(eng.g32, optimizer._comm)
+
+
+def gradient_exchange(model, optimizer):
+    """The gradient exchange a rank is running now (after attach_data_parallel;
+    it can change after the first step, see ShardPusher.verify): "zero1_push",
+    "zero1_overlap", "allreduce", "zero1" (the post-backward reduce-scatter), or
+    None (one process)."""
+    eng = _engine_of(model)
+    if eng is None or eng.grad_scale_t is None:
+        return None
+    red = eng.grad_reducer
+    if red is not None and red.active:
+        return red.mode
+    return "zero1" if getattr(optimizer, "_comm", None) is not None else "allreduce"
 
 
 def train_one_epoch_multi_gpu(epoch, models, dataloader, criterion, optimizer, devices, clip, batch_step=0,

@@ -317,3 +317,92 @@ def test_push_setup_agrees_on_fallback_gloo(tmp_path, world, fail):
     for r in res:
         assert r["made"] == (fail is None)
         assert r["sum"] == (world if fail is None else 0)
+
+
+def _push_timeout_worker(rank, port, out_dir, world):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), NSTL_PUSH_TIMEOUT_S="1")
+    torch.set_num_threads(1)
+    import time
+    from neurosync_trainer_lite_amd import parallel
+    parallel.init_from_env(backend="gloo")
+    comm = parallel.ShardComm(64 * 840)
+    # a transport whose copies never complete (a wedged copy engine): every
+    # mark stays pending
+    parallel._HostTransport.mark = lambda self: [("never", [r for r in range(world) if r != rank])]
+    parallel._HostTransport.pending = staticmethod(lambda marks: sorted(r for _, peers in marks for r in peers))
+    t0 = time.monotonic()
+    try:
+        parallel.ShardPusher.create(torch.zeros(comm.numel), comm, bucket_bytes=4000)
+        res = "returned"
+    except parallel.PushTimeout as e:
+        res = str(e)
+    torch.save({"res": res, "s": time.monotonic() - t0}, os.path.join(out_dir, "t%d.pt" % rank))
+    dist.destroy_process_group()
+
+
+def test_push_self_test_deadline_raises_gloo(tmp_path):
+    """the zero1_push self-test polls its copies from the host
+    against the deadline BEFORE anything (stream join, sync, the ranks'
+    agreement) is chained behind them, so copies that never land end setup with
+    PushTimeout naming the peers, instead of blocking forever; create() does not
+    turn it into a zero1 fallback (a copy queue that does not drain cannot be
+    trusted by the process)."""
+    mp.spawn(_push_timeout_worker, args=(_port(), str(tmp_path), 2), nprocs=2, join=True)
+    for r in range(2):
+        out = torch.load(tmp_path / ("t%d.pt" % r), weights_only=True)
+        assert "not landed after 1 s" in out["res"] and ("[%d]" % (1 - r)) in out["res"], out
+        assert out["s"] < 30
+
+
+def _push_verify_worker(rank, port, out_dir, world, corrupt):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from neurosync_trainer_lite_amd import parallel
+    parallel.init_from_env(backend="gloo")
+    ns = 64 * 840
+    comm = parallel.ShardComm(ns)
+    grads = torch.randn(ns, generator=torch.Generator().manual_seed(10 + rank))
+    red = parallel.ShardPusher.create(grads, comm, bucket_bytes=4000)
+    red.begin(True)
+    red.ready(ns)
+    red.finish()
+    assert red.consume()
+    slots = red.slots()
+    if corrupt and rank == 0:
+        slots[0, 17] += 1.0  # one stale element in one slot of one rank
+    gs, part = torch.empty(comm.shard), torch.zeros(4)
+
+    def sumsq_fn(x, p):
+        p.zero_()
+        p[0] = (x.double() ** 2).sum().float()
+    x = grads[comm.lo:comm.hi].clone()
+    for k in range(red.n_slots):
+        x += slots[k]
+    gs.copy_(x)
+    sumsq_fn(gs, part)
+    ok = red.verify(grads, gs, part, sumsq_fn)
+    ref = torch.empty(comm.shard)
+    comm.reduce_scatter(grads, ref)
+    torch.save({"ok": ok, "failed": red.failed, "check": red.check["ok"], "pending": red.verify_pending,
+                "gs_ok": torch.allclose(gs, ref, rtol=1e-6, atol=1e-6),
+                "part_ok": abs(float(part[0]) - float((ref.double() ** 2).sum())) <= 1e-3 * float(part[0])},
+               os.path.join(out_dir, "v%d.pt" % rank))
+    red.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,corrupt", [(2, False), (4, False), (4, True)])
+def test_push_first_step_verified_against_reduce_scatter_gloo(tmp_path, world, corrupt):
+    """the first step's pushed shard sums (own + slots) are checked
+    against the reduce-scatter of the same arena, on every rank, and the ranks
+    agree: one stale element on one rank fails the check everywhere; that step
+    then continues on the reduce-scatter's shard and sums of squares, and the
+    reducer is marked failed (the optimizer runs zero1 from then on)."""
+    mp.spawn(_push_verify_worker, args=(_port(), str(tmp_path), world, corrupt), nprocs=world, join=True)
+    for r in range(world):
+        out = torch.load(tmp_path / ("v%d.pt" % r), weights_only=True)
+        assert out["ok"] == out["check"] == (not corrupt), out
+        assert out["failed"] == corrupt and out["pending"] is False
+        assert out["gs_ok"] and out["part_ok"], out

@@ -56,6 +56,11 @@ def _worker(rank, port, out_dir, mode="zero1"):
         opt.zero_grad()
         crit(model(src), trg).backward()
         opt.step(max_norm=2.0)
+    if mode == "zero1_push":
+        # the first step's pushed sums were checked against the reduce-scatter
+        # (ShardPusher.verify) and the exchange stayed on the copy engines
+        assert opt.dp_check is not None and opt.dp_check["ok"], opt.dp_check
+        assert isinstance(model.engine().grad_reducer, parallel.ShardPusher) and opt.dp_fallback is None
     with pytest.raises(RuntimeError, match="consolidate"):
         model.state_dict()
     opt.consolidate()
