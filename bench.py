@@ -449,7 +449,8 @@ def launch_ranks(args, argv):
     stalls, a second attempt runs NSTL_DP=zero1 and the line says so
     (config.dp_fallback)."""
     n_dev = torch.cuda.device_count()
-    if n_dev < args.gpus:
+    # NSTL_DIST_BACKEND=gloo: a rehearsal with several ranks per GPU (parallel.init_from_env)
+    if n_dev < args.gpus and not (n_dev and os.environ.get("NSTL_DIST_BACKEND") == "gloo"):
         log("--gpus %d needs %d GPUs on this node; %d visible" % (args.gpus, args.gpus, n_dev))
         return 2
     modes = [os.environ["NSTL_DP"]] if os.environ.get("NSTL_DP") else ["zero1_push", "zero1"]
