@@ -177,7 +177,7 @@ def cpu_baseline(cfg, T, budget_s=20.0):
     if os.environ.get("OMP_NUM_THREADS", "").isdigit():
         cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(cores)
-    B = 4
+    B = 8  # the CPU sample is B=8 windows x T frames
     params = model_ref.seeded_params(model_ref.param_shapes(cfg["input_dim"], cfg["hidden_dim"], cfg["n_layers"],
                                                             cfg["output_dim"]), 0)
     tr = model_ref.OracleTrainer(params, cfg["num_heads"], dropout=cfg["dropout"])

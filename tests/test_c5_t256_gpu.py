@@ -1,12 +1,12 @@
 """BASELINE config C5's fp8 path at its own sequence length, T = 256 (2x the
 default window: the long-clip stress), held to the fp32 ORACLE.
 
-At T = 256 the q|k|v / cross q / cross k|v + RoPE GEMMs take a different route
-from T = 128: the 256-position table (64 KB) does not fit beside the 4-wave
-kernel's stages, so in fp8 they run on the fp8 ring kernel with T = 256 tables
-(and the attention on the split backward).  The C5 bench line is measured on
-this route, so it gets the same checks as the T = 128 production step
-(tests/test_production_gpu.py::test_fp8_backward_production_step_vs_oracle):
+At T = 256 the q|k|v / cross q / cross k|v + RoPE GEMMs run on the fp8 4-wave
+kernel (gemm4f8_kernel) with the 256-position RoPE table kept as bf16 (cos,
+sin) pairs (32 KB, beside its stages), like every other fp8 GEMM of the scope;
+the attention runs the split backward (T > 128).  The C5 bench line is
+measured on this route, so it gets the same checks as the T = 128 production
+step (tests/test_production_gpu.py::test_fp8_backward_production_step_vs_oracle):
 
   * forward within the metric's MSE gate (1e-3) of model_ref.seq2seq_forward;
   * every parameter gradient within 0.35 relative of the oracle's, or 2 x the
@@ -14,7 +14,8 @@ this route, so it gets the same checks as the T = 128 production step
     relative error on a single GEMM);
   * the clip norm within 5 %;
   * the launch counters: the fp8 scope ran (5 forward GEMMs + 2 FFN linear2
-    input gradients per layer) and 4 per layer of them carried the RoPE epilogue.
+    input gradients per layer), 4 per layer of them carried the RoPE epilogue,
+    and all 7 per layer ran on the 4-wave kernel (NSTL_K_GEMM4F8).
 
 Reference ops: /root/reference/utils/model.py:60-83 (apply_rope_qk),
 :113-115 (q/k/v projections), :153-158 (FFN).
@@ -85,6 +86,7 @@ def test_c5_fp8_t256_step_vs_oracle(problem):
     # cross k|v forward + enc and dec FFN linear2 dX; 4 of them with RoPE tables
     assert c["gemm_fp8"] == 7 * L, c
     assert c["gemm_fp8_rope"] == 4 * L, c
+    assert c["gemm4_fp8"] == 7 * L, c  # every fp8 GEMM of the scope on the 4-wave kernel, RoPE at T = 256 too
     assert c["attn_bwd_split"] == 3 * L and c["attn_bwd_fused"] == 0, c  # T > 128: the split backward
     mse = ((pred.double() - o_pred.double()) ** 2).mean().item()
     p16, _, n16, g16, _ = run_step(params, src, trg, fp8=False)
