@@ -646,7 +646,9 @@ def main(argv=None):
         fl = sum(2.0 * M * N * Kd for _, _, _, M, N, Kd, _ in problems)
         by = sum((M * Kd + N * Kd) * A.element_size() + M * N * C.element_size() for A, _, C, M, N, Kd, _ in problems)
         fam = launched_family()
-        gemm_events.append((e0, e1, fl, by, False, True, "gemm4_grouped_dw" if fam == "gemm4" else fam))
+        # the weight gradients (f32 out) vs the decoder's grouped cross k|v + RoPE projections (bf16 out)
+        dw = all(C.dtype == torch.float32 for _, _, C, _, _, _, _ in problems)
+        gemm_events.append((e0, e1, fl, by, False, dw, "gemm4_grouped_dw" if fam == "gemm4" and dw else fam))
 
     K.gemm = timed_gemm
     K.gemm_grouped = timed_grouped

@@ -1448,13 +1448,21 @@ extern "C" int nstl_gemm_grouped(const nstl_gemm_args* args, int n, void* stream
     if (int rc = make_params(a, p)) return rc;
     NSTL_CHECK_ARG(a->dtype == NSTL_BF16 && a->K % 64 == 0 && a->M >= BIG && a->N >= BIG,
                    "nstl_gemm_grouped: problem %d is not a 256-kernel problem (bf16, M, N >= 256, K %% 64 == 0)", g);
-    NSTL_CHECK_ARG(a->epilogue == NSTL_EPI_NONE && a->split_k <= 1 && !a->colsum_part && !a->relu_mask,
-                   "nstl_gemm_grouped: problem %d: no epilogue, no split-K", g);
+    // no epilogue (the weight gradients), or bias + RoPE with one shared table
+    // (the decoder's cross-attention k|v projections of every layer at once)
+    NSTL_CHECK_ARG((a->epilogue == NSTL_EPI_NONE || a->epilogue == NSTL_EPI_BIAS_ROPE) &&
+                       a->epilogue == args[0].epilogue && a->split_k <= 1 && !a->colsum_part && !a->relu_mask,
+                   "nstl_gemm_grouped: problem %d: no epilogue or bias + RoPE (the same for all), no split-K", g);
     NSTL_CHECK_ARG(a->a_kmajor == args[0].a_kmajor && a->b_kmajor == args[0].b_kmajor &&
                        a->c_dtype == args[0].c_dtype && (a->beta != 0.f) == (args[0].beta != 0.f),
                    "nstl_gemm_grouped: problem %d differs in layout, output type or beta use", g);
+    NSTL_CHECK_ARG(a->epilogue != NSTL_EPI_BIAS_ROPE ||
+                       (a->rope_cos == args[0].rope_cos && a->rope_sin == args[0].rope_sin &&
+                        a->rope_T == args[0].rope_T && a->rope_dim == args[0].rope_dim),
+                   "nstl_gemm_grouped: problem %d: RoPE problems share one table (cos, sin, T, dim)", g);
     const int em = ring_epi_mode(a, p);
-    NSTL_CHECK_ARG(em == EM_F32 || em == EM_BF16, "nstl_gemm_grouped: f32 output, or bf16 without beta");
+    NSTL_CHECK_ARG(em == EM_F32 || em == EM_BF16 || (em == EM_ROPE && a->epilogue == NSTL_EPI_BIAS_ROPE),
+                   "nstl_gemm_grouped: f32 output, or bf16 without beta");
     NSTL_CHECK_ARG(!a->sq_part || em == EM_F32, "nstl_gemm_grouped: sq_part needs f32 output");
   }
   hipStream_t st = (hipStream_t)stream;

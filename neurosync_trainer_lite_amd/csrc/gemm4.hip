@@ -192,7 +192,11 @@ void launch_em(int em, dim3 grid, hipStream_t st, const g4::GroupParams& gp) {
 template <bool SK, int R3>
 int launch_sk(int em, bool ak, bool bk, bool grouped, dim3 grid, hipStream_t st, const g4::GroupParams& gp) {
   if (ak && bk) {
-    if (grouped) return 0;
+    if (grouped) {  // the cross-attention k|v projections of all decoder layers
+      if (em != g4::EM_ROPE || SK || R3) return 0;
+      hipLaunchKernelGGL((g4::gemm4_kernel<true, true, g4::EM_ROPE, true, 0, false, 0>), grid, dim3(g4::NT), 0, st, gp);
+      return 1;
+    }
     launch_em<true, true, false, SK, R3>(em, grid, st, gp);
   } else if (ak && !bk) {
     if (grouped) return 0;
@@ -316,13 +320,19 @@ int gemm4(const nstl_gemm_args* a, hipStream_t st, int* handled) {
   return 0;
 }
 
-// A group of weight-gradient problems (same layout, f32 output, beta 0).
+// A group of weight-gradient problems (same layout, f32 output, beta 0), or of
+// forward projections with the bias + RoPE epilogue and one shared table (TT:
+// the decoder's cross-attention k|v of every layer in one launch; nstl_gemm_grouped
+// checked the table is shared).
 int gemm4_grouped(const nstl_gemm_args* args, int n, hipStream_t st, int* handled) {
   *handled = 0;
   if (!gemm4_env() || n < 1 || n > g4::GROUP_MAX) return 0;
+  const int em = g4_mode(args);
+  if (em != g4::EM_F32 && em != g4::EM_ROPE) return 0;
   for (int i = 0; i < n; ++i) {
     const nstl_gemm_args* a = args + i;
-    if (!g4_shape_ok(a) || g4_mode(a) != g4::EM_F32 || a->epilogue != NSTL_EPI_NONE) return 0;
+    if (!g4_shape_ok(a) || g4_mode(a) != em) return 0;
+    if (em == g4::EM_F32 && a->epilogue != NSTL_EPI_NONE) return 0;
     if (a->a_kmajor != args[0].a_kmajor || a->b_kmajor != args[0].b_kmajor) return 0;
   }
   const int G = nstl::stream_cus(st);
@@ -336,7 +346,7 @@ int gemm4_grouped(const nstl_gemm_args* args, int n, hipStream_t st, int* handle
     gp.tile_end[i] = tiles;
   }
   gp.n = n;
-  if (!launch(g4::EM_F32, args[0].a_kmajor, args[0].b_kmajor, true, G, st, gp)) return 0;
+  if (!launch(em, args[0].a_kmajor, args[0].b_kmajor, true, G, st, gp)) return 0;
   NSTL_LAUNCH_CHECK("nstl_gemm_grouped (4-wave persistent)");
   nstl::count(NSTL_K_GEMM4);
   nstl::count(NSTL_K_GEMM4_TILES, tiles);

@@ -52,6 +52,8 @@ ARENA_ALIGN = 64 * 840
 # encoder layers whose weight gradients share one grouped GEMM: 4 x 192 tiles of
 # 256^2 = 768 = three full rounds on 256 CUs (one layer alone: 0.75 of a round)
 ENC_GROUP = 4
+# the 4-wave GEMM's RoPE table budget in LDS (csrc/gemm4.h ROPE_LDS): T * rope_dim * 4 bytes
+ROPE_LDS_BYTES = 32768
 
 
 def _pad64(n):
@@ -222,6 +224,7 @@ class Seq2SeqEngine:
         # K = 2D GEMM per decoder layer instead of one K = L * 2D GEMM after the decoder
         self.dmem_concat = os.environ.get("NSTL_DMEM_CONCAT", "1") != "0"
         self._wkv = None           # [W_kv_0; ...; W_kv_{L-1}] slab (_kv_weights)
+        self._kv_all_done = False  # decode(): every layer's cross k|v projected in one launch
         # NSTL_RELU_MASK=0: the FFN2 dX epilogue reads the saved hidden h for its
         # dReLU instead of the 1-bit keep&positive mask the FFN1 epilogue writes
         self.relu_mask_on = os.environ.get("NSTL_RELU_MASK", "1") != "0"
@@ -1034,8 +1037,9 @@ class Seq2SeqEngine:
         qc, kvc = L_(bb.d_qc), L_(bb.d_kvc)
         self._gemm_fwd(x1, pre + "multihead_attn.q_linear.weight", qc, K.EPI_BIAS_ROPE,
                        rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D)
-        self._gemm_fwd(mem, pre + "multihead_attn.k_linear.weight", kvc, K.EPI_BIAS_ROPE, rows=2,
-                       rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D, xq=self._mem_q)
+        if not self._kv_all_done:
+            self._gemm_fwd(mem, pre + "multihead_attn.k_linear.weight", kvc, K.EPI_BIAS_ROPE, rows=2,
+                           rope=(*self.rope(T, self.dh), T, self.dh), rope_cols=D, xq=self._mem_q)
         self._attn(qc, kvc[:, :D], kvc[:, D:], L_(bb.d_oc), L_(bb.d_lsec), sd("xattn"), T, B,
                    mask=bb.d_maskc[l] if bb.save else None)
         self._gemm_fwd(L_(bb.d_oc), pre + "multihead_attn.out_linear.weight", bb.y, K.EPI_BIAS)
@@ -1052,6 +1056,31 @@ class Seq2SeqEngine:
         self._ln(x2, bb.y, x3, st[4:6], pre + "norm3", 1, (sd("drop3"), 0), L_(bb.d_s3),
                  q8="scratch" if l + 1 < self.L else None)
         return x3
+
+    def _cross_kv_all(self, bb, mem, T):
+        """The cross-attention k|v projections of every decoder layer (their A is
+        the same encoder output) as ONE grouped launch before the decoder layers:
+        on the 4-wave kernel one launch of L x 512 tiles instead of L launches of
+        two rounds each, so the per-launch fill, drain and boundary are paid once
+        (gemm4_kernel<..., EM_ROPE, GROUPED>).  Only when every layer keeps its own
+        k|v buffer (a training forward), the projections are bf16 (not in the fp8
+        scope) and the RoPE table fits beside the 4-wave kernel's stages (T = 128
+        at head dim 64); otherwise each layer projects its own (returns False).
+        NSTL_KV_GROUPED=0: per layer (A/B)."""
+        D, L = self.D, self.L
+        name = "decoder.transformer_decoder.%d.multihead_attn.k_linear.weight"
+        if (not bb.save or L < 2 or os.environ.get("NSTL_KV_GROUPED", "1") == "0" or self.dt != torch.bfloat16
+                or T * self.dh * 4 > ROPE_LDS_BYTES or any(self.fp8 and (name % l, 2) in self._fp8_w for l in range(L))):
+            return False
+        if self._wpending:
+            self._await(*self._stage_rng["dec_kv"])
+        rope = (*self.rope(T, self.dh), T, self.dh)
+        probs = [(mem, self.w(name % l, 2), bb.d_kvc[l], bb.M, 2 * D, D,
+                  dict(epilogue=K.EPI_BIAS_ROPE, bias=self.b((name % l).replace(".weight", ".bias"), 2), rope=rope,
+                       rope_cols=D)) for l in range(L)]
+        for i in range(0, L, K.GEMM_GROUP_MAX):
+            K.gemm_grouped(probs[i:i + K.GEMM_GROUP_MAX], stream=self.st)
+        return True
 
     def _prologue(self, training):
         self.ensure_bound()
@@ -1092,6 +1121,7 @@ class Seq2SeqEngine:
             xdec0 = bb.xdec0
         x = xdec0
         self._mem_q = (self._xq.get(mem.data_ptr()) or self._fp8_quant(mem, mem=True)) if self.fp8 else None
+        self._kv_all_done = self._cross_kv_all(bb, mem, T)
         for l in range(self.L):
             x = self._dec_layer(bb, l, x, mem, T)
         self._ln(None, x, bb.xf, bb.decf_stats, "decoder.layer_norm", 0, (0, 0), None)

@@ -166,6 +166,38 @@ def test_gemm4_rope_matches_ring(monkeypatch, T, rope_cols, dim):
     assert rel_err(c4, zr) < 1e-2
 
 
+@pytest.mark.parametrize("L,M", [(8, 2048), (3, 4096)])
+def test_gemm4_grouped_rope_bit_identical_to_single(L, M):
+    """The decoder's cross-attention k|v projections of all L layers as ONE grouped
+    launch (gemm4_kernel<..., EM_ROPE, GROUPED>: shared A, per-problem B / C /
+    bias, one RoPE table) give exactly the outputs of L single launches: the same
+    tiles, the same k order and the same epilogue per element.  Also the engine's
+    switch (NSTL_KV_GROUPED) and the argument check that the table is shared."""
+    D, T, dim = 1024, 128, 64
+    X = rnd(M, D, dtype=bf, seed=41)
+    Ws = [rnd(2 * D, D, dtype=bf, scale=0.05, seed=42 + l) for l in range(L)]
+    bs = [rnd(2 * D, seed=60 + l) for l in range(L)]
+    cs, sn = rotation_tables(T, dim, DEV)
+    kw = lambda l: dict(epilogue=K.EPI_BIAS_ROPE, bias=bs[l], rope=(cs, sn, T, dim), rope_cols=D)
+    single = []
+    for l in range(L):
+        C = torch.empty(M, 2 * D, dtype=bf, device=DEV)
+        K.gemm(X, Ws[l], C, M, 2 * D, D, **kw(l))
+        single.append(C)
+    grouped = [torch.full((M, 2 * D), float("nan"), dtype=bf, device=DEV) for _ in range(L)]
+    K.kernel_counts_reset()
+    K.gemm_grouped([(X, Ws[l], grouped[l], M, 2 * D, D, kw(l)) for l in range(L)])
+    torch.cuda.synchronize()
+    c = K.kernel_counts()
+    assert c["gemm4"] == 1 and c["gemm4_tiles"] == L * (M // 256) * (2 * D // 256), c
+    for l in range(L):
+        assert torch.equal(grouped[l], single[l]), l
+    cs2, sn2 = rotation_tables(T, dim, DEV)
+    with pytest.raises(RuntimeError, match="share one table"):
+        K.gemm_grouped([(X, Ws[0], grouped[0], M, 2 * D, D, kw(0)),
+                        (X, Ws[1], grouped[1], M, 2 * D, D, dict(kw(1), rope=(cs2, sn2, T, dim)))])
+
+
 def test_gemm4_odd_stage_count_stays_on_ring():
     """K % 128 != 0 (an odd number of 64-deep stages): the ring kernel runs it."""
     M, N, Kd = 2048, 1024, 320
