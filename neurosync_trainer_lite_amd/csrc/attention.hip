@@ -20,11 +20,6 @@
 
 #include "../../include/nstl.h"
 #include "common.h"
-// cache policy of the persistent forward's O stores (aux bits; build-time
-// experiment: 0 plain, 16 sc1 = device scope, written through the XCD's L2)
-#ifndef NSTL_ATTN_O_AUX
-#define NSTL_ATTN_O_AUX 0
-#endif
 #include "status.h"
 
 namespace {
@@ -422,7 +417,7 @@ NSTL_DEV void fwd_queries(const AttnParams& p, const char* Kimg, const char* Vim
     for (int dt = 0; dt < 4; ++dt) {
       const f32x4 x = o[dt] * inv;
       const bf16x4 b = {(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2a, b), ro, ob + 32 * dt, 0, NSTL_ATTN_O_AUX);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2a, b), ro, ob + 32 * dt, 0, 0);
     }
   } else {
     T* orow = (T*)p.o + (tok0 + q0 + c) * p.o_ld + h * DH + 4 * g;

@@ -644,32 +644,6 @@ NSTL_DEV bool sk_handoff(const StreamK& sk, f32x4 (&acc)[8][8], const Seg& s, in
   return !part || last;
 }
 
-// The bf16 epilogue's 16-byte output store.  G4_STORE_POL (build-time, an
-// experiment): 0 plain (L2 write-back), 1 sc1 (device scope: written through
-// the XCD's L2), 2 nt (streaming), 3 sc0 sc1 (system scope).  Dirty output lines
-// left in the L2s at a kernel's end are written back at the boundary, before
-// the next kernel of the stream starts (MI355X_MICROARCH.md, boundary cost).
-#ifndef G4_STORE_POL
-#define G4_STORE_POL 0
-#endif
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-// dst: the element address (POL 0, 2); rc / off: the same as a buffer resource
-// over C and a byte offset (POL 1, 3: the cache-policy bits need a compiler-
-// visible store -- an inline-asm store's data registers could be overwritten by
-// the next VALU before the store has read them)
-NSTL_DEV void store_c16(void* dst, __amdgpu_buffer_rsrc_t rc, uint32_t voff, uint32_t soff, uint4 v) {
-  const u32x4_t w = {v.x, v.y, v.z, v.w};
-  if constexpr (G4_STORE_POL == 1) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, w), rc, voff, soff, 16 /* sc1 */);
-  } else if constexpr (G4_STORE_POL == 2) {
-    __builtin_nontemporal_store(w, (u32x4_t*)dst);
-  } else if constexpr (G4_STORE_POL == 3) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, w), rc, voff, soff, 17 /* sc0 sc1 */);
-  } else {
-    *(uint4*)dst = v;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Epilogues, from registers.  row0 / col0: the wave's 128 x 128 block.
 // bf16 outputs: per (a, pair of column blocks bp, bp + 1) the elementwise math
@@ -817,13 +791,6 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
       }
     }
     bf16* const cbase = (bf16*)p.C + (int64_t)(row0 + c) * p.ldc + col0;
-    // (G4_STORE_POL 1 / 3 only; the host keeps a bf16 C under 2^31 bytes for them)
-    const __amdgpu_buffer_rsrc_t rcb =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.C, 0, G4_STORE_POL & 1 ? (int)((uint32_t)p.M * (uint32_t)p.ldc * 2u) : 0,
-                                          0x00020000);
-    // the lane's byte offset of its first store (row row0 + c); a row block adds a
-    // uniform 32 a ldc (scalar offset), a column pair 32 bp (immediate)
-    const uint32_t cvo = ((uint32_t)(row0 + c) * (uint32_t)p.ldc + col0 + 16 * odd + 4 * (g - odd)) * 2u;
 #pragma unroll
     for (int a = 0; a < 8; ++a) {
       const int row = row0 + 16 * a + c;
@@ -927,9 +894,7 @@ NSTL_DEV void epilogue(const Params& p, f32x4 (&acc)[8][8], int row0, int col0, 
         const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
         // EDBG & 1 (experiment: timing only): the stores skipped, the math kept
-        if (!(EDBG & 1) || p.ldc < 0)
-          store_c16(crow + 16 * (bp + odd) + 4 * (g - odd), rcb, cvo + 32u * bp,
-                    __builtin_amdgcn_readfirstlane(32u * (uint32_t)a * (uint32_t)p.ldc), make_uint4(s0[0], s1[0], s0[1], s1[1]));
+        if (!(EDBG & 1) || p.ldc < 0) *(uint4*)(crow + 16 * (bp + odd) + 4 * (g - odd)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         G4_SB();  // one (a, bp) group at a time: hoisting the accumulator reads spills
       }
     }

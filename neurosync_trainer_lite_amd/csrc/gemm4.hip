@@ -134,7 +134,7 @@ bool g4_shape_ok(const nstl_gemm_args* a) {
   const int64_t ae = a->a_kmajor ? ((int64_t)(a->M - 1) * a->lda + a->K) * 2 : ((int64_t)(a->K - 1) * a->lda + a->M) * 2;
   const int64_t be = a->b_kmajor ? ((int64_t)(a->N - 1) * a->ldb + a->K) * 2 : ((int64_t)(a->K - 1) * a->ldb + a->N) * 2;
   // f32 C through a buffer resource (its epilogue's stores): 32-bit extent
-  const int64_t ce = (int64_t)a->M * a->ldc * (a->c_dtype == NSTL_F32 ? 4 : 2);  // C through a buffer resource
+  const int64_t ce = a->c_dtype == NSTL_F32 ? (int64_t)a->M * a->ldc * 4 : 0;
   return ae < (1ll << 31) && be < (1ll << 31) && ce < (1ll << 31);
 }
 
@@ -254,7 +254,7 @@ bool g4f8_shape_ok(const nstl_gemm_args* a) {
   if (a->lda % 16 || a->ldb % 16) return false;
   if (a->ldc % (a->c_dtype == NSTL_F32 ? 4 : 8)) return false;
   const int64_t ae = (int64_t)(a->M - 1) * a->lda + a->K, be = (int64_t)(a->N - 1) * a->ldb + a->K;
-  const int64_t ce = (int64_t)a->M * a->ldc * (a->c_dtype == NSTL_F32 ? 4 : 2);  // C through a buffer resource
+  const int64_t ce = a->c_dtype == NSTL_F32 ? (int64_t)a->M * a->ldc * 4 : 0;
   return ae < (1ll << 31) && be < (1ll << 31) && ce < (1ll << 31);
 }
 

@@ -12,10 +12,6 @@
 
 #include "../../include/nstl.h"
 #include "common.h"
-// the 16-byte bf16 stores written through the XCD's L2 (sc1; build-time experiment)
-#ifndef NSTL_LN_STORE_SC1
-#define NSTL_LN_STORE_SC1 0
-#endif
 #include "status.h"
 
 namespace {
@@ -270,14 +266,7 @@ NSTL_DEV void storeG(T* p, const float* v) {
     T* e = (T*)&u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) e[j] = from_f32<T>(v[j]);
-    if constexpr (NSTL_LN_STORE_SC1) {  // through a one-store buffer resource: the sc1 bit, compiler-visible
-      typedef int i32x4_t __attribute__((ext_vector_type(4)));
-      const i32x4_t w = {(int)u.x, (int)u.y, (int)u.z, (int)u.w};
-      __builtin_amdgcn_raw_buffer_store_b128(w, __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, 16, 0x00020000), 0, 0,
-                                             16 /* sc1 */);
-    } else {
-      *(uint4*)p = u;
-    }
+    *(uint4*)p = u;
   } else {
     *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
     *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
