@@ -1064,12 +1064,15 @@ class Seq2SeqEngine:
         two rounds each, so the per-launch fill, drain and boundary are paid once
         (gemm4_kernel<..., EM_ROPE, GROUPED>).  Only when every layer keeps its own
         k|v buffer (a training forward), the projections are bf16 (not in the fp8
-        scope) and the RoPE table fits beside the 4-wave kernel's stages (T = 128
-        at head dim 64); otherwise each layer projects its own (returns False).
+        scope), the shapes are whole 256 x 256 tiles and the RoPE table fits beside
+        the 4-wave kernel's stages (T = 128 at head dim 64); otherwise each layer
+        projects its own (returns False).
         NSTL_KV_GROUPED=0: per layer (A/B)."""
         D, L = self.D, self.L
         name = "decoder.transformer_decoder.%d.multihead_attn.k_linear.weight"
-        if (not bb.save or L < 2 or os.environ.get("NSTL_KV_GROUPED", "1") == "0" or self.dt != torch.bfloat16
+        # the 4-wave kernel's whole-tile shapes (M, N multiples of 256; K of 128, >= 256)
+        tiles_ok = bb.M % 256 == 0 and (2 * D) % 256 == 0 and D % 128 == 0 and D >= 256
+        if (not bb.save or L < 2 or not tiles_ok or os.environ.get("NSTL_KV_GROUPED", "1") == "0" or self.dt != torch.bfloat16
                 or T * self.dh * 4 > ROPE_LDS_BYTES or any(self.fp8 and (name % l, 2) in self._fp8_w for l in range(L))):
             return False
         if self._wpending:
