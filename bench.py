@@ -561,10 +561,11 @@ def main(argv=None):
 
     # as train_one_epoch sets it: nothing writes the gradients between backward
     # and step, so the clip norm may come from the weight-gradient epilogues'
-    # partials.  (train_one_epoch also sets overlap_next_forward; that overlap only
-    # runs under NSTL_ADAM_OVERLAP=1, off by default, so it is not set here: the
-    # timed update runs on the main stream after backward.)
+    # partials.
     opt.trust_backward_norm = world == 1
+    # as train_one_epoch: the next use of the parameters is the next forward, so the
+    # update MAY run under it -- only with NSTL_ADAM_OVERLAP=1 (FusedAdam: opt-in)
+    opt.overlap_next_forward = True
 
     def step(x=src, y=trg):
         opt.zero_grad()

@@ -40,9 +40,12 @@ class FusedAdam(torch.optim.Optimizer):
         # queue_update), so it runs under the forward of earlier layers.  Results
         # are identical; any other reader of the parameters syncs first
         # (state_dict, module-level forwards, backward).
-        # Opt-in (NSTL_ADAM_OVERLAP=1): measured no faster at the 228M config
-        # (562.0k vs 561.3k frames/s): the ring GEMMs lose ~5 % to any kernel that
-        # holds CUs beside them, about what the update saves
+        # On by default since round 6 (NSTL_ADAM_OVERLAP=0: the update in order):
+        # beside the 4-wave GEMMs (one wave per SIMD, 480 of 512 registers) the
+        # update's 28-register waves co-reside, and the 228M step gains ~1 %
+        # same-box (649.9k vs 643.6k frames/s, profiles/r6_adam_overlap_ab.txt).
+        # Round 2 measured no gain beside the 8-wave ring GEMMs, which hold every
+        # register of a SIMD (562.0k vs 561.3k).
         self.overlap_next_forward = False
         # The caller guarantees nothing writes the gradients between backward and
         # step() (train_one_epoch's own loop sets this): the clip norm may then
@@ -51,7 +54,7 @@ class FusedAdam(torch.optim.Optimizer):
         # reference's multi-GPU path copies into p.grad.data,
         # utils/training_utils.py:235) gets the norm re-read from the arena.
         self.trust_backward_norm = False
-        self._overlap_allowed = os.environ.get("NSTL_ADAM_OVERLAP", "0") == "1"
+        self._overlap_allowed = os.environ.get("NSTL_ADAM_OVERLAP", "1") == "1"
         self._upd_stream = None
         # why the data-parallel exchange left NSTL_DP=zero1_push for zero1, if it did
         # (attach_data_parallel at setup, ShardPusher.verify at the first step)
@@ -159,7 +162,16 @@ class FusedAdam(torch.optim.Optimizer):
             # the side stream (nstl_adam_step reads the coefficient: no LDS, so its
             # workgroups fit beside the forward's ring-GEMM workgroups)
             main = torch.cuda.current_stream(eng.device)
-            if max_norm is not None:
+            sq = eng.take_sq_partials() if max_norm is not None and self.trust_backward_norm else None
+            eng.invalidate_sq()
+            if sq is not None:  # as below: the dW epilogues' partials + the rest of the arena
+                parts, rp = self._norm_parts(sq), eng.sq_rest_partials
+                o = sq.numel()
+                for lo, hi in eng.norm_rest:
+                    K.sumsq(eng.g32[lo:hi], hi - lo, parts[o:o + rp], rp, stream=st)
+                    o += rp
+                K.clip_coef(parts, o, max_norm, self.coef, self.norm, stream=st)
+            elif max_norm is not None:
                 sumsq_fn(eng.g32, self.partial)
                 K.clip_coef(self.partial, N_PARTIAL, max_norm, self.coef, self.norm, stream=st)
             else:

@@ -433,8 +433,8 @@ def test_module_level_forwards_match_reference_layers(golden):
         enc(x)
 
 
-@pytest.mark.parametrize("amp", [True, False])
-def test_update_overlapped_with_next_forward_is_identical(amp):
+@pytest.mark.parametrize("amp,trust", [(True, False), (False, False), (True, True)])
+def test_update_overlapped_with_next_forward_is_identical(amp, trust):
     """FusedAdam.overlap_next_forward: the update runs on a side stream in arena
     ranges that the next forward waits for stage by stage.  Same kernels, same
     order per element: parameters, moments, losses and norms are bit-identical
@@ -447,6 +447,7 @@ def test_update_overlapped_with_next_forward_is_identical(amp):
         model.train()
         opt.overlap_next_forward = overlap
         opt._overlap_allowed = True  # the path is opt-in (NSTL_ADAM_OVERLAP=1)
+        opt.trust_backward_norm = trust  # the clip norm from the dW epilogues' partials (bench.py, train_one_epoch)
         g = torch.Generator().manual_seed(5)
         losses, norms = [], []
         for s in range(4):
