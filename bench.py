@@ -392,11 +392,27 @@ def _run_ranks(cmd, env, stall_s, limit_s):
     line, stdout collected.  Killed (the whole group) after stall_s seconds
     without a line on either stream, or after limit_s.  Returns (rc or None if
     killed, stdout lines, last stderr lines, why killed)."""
+    import ctypes
     import signal
     import subprocess
     import threading
+
+    def die_with_parent():  # in the child, before exec: SIGTERM when this process dies
+        try:
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                         start_new_session=True)
+                         start_new_session=True, preexec_fn=die_with_parent)
+
+    # the ranks run in their own session: a signal that ends this launcher ends them too
+    def forward(signum, frame):
+        try:
+            os.killpg(p.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+        raise SystemExit(128 + signum)
+    old = {sg: signal.signal(sg, forward) for sg in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)}
     out, tail, last = [], [], [time.monotonic()]
 
     def pump(src, sink):
@@ -436,6 +452,8 @@ def _run_ranks(cmd, env, stall_s, limit_s):
             break
     for t in ts:
         t.join(5)
+    for sg, h in old.items():
+        signal.signal(sg, h)
     return (None if why else p.returncode), out, tail, why
 
 
