@@ -17,6 +17,11 @@ WORLD_SIZE must equal --gpus.  Under the self-launch, a first attempt with the
 default exchange (NSTL_DP=zero1_push) that fails or stalls is followed by one
 with NSTL_DP=zero1, and the line records both (`launch.attempts`).
 
+Multi-rank lines also carry `dist` (backend, world size, launch form, per-rank
+ms/step and their spread, and `exchange_check`: the first step's pushed shard
+sums against an RCCL reduce-scatter, ShardPusher.verify), `config.gradient_exchange`
+(the exchange active after the timed steps) and `config.dp_fallback`.
+
 Prints ONE JSON line on rank 0.  `roofline` is measured live for the dominant
 kernel (nstl GEMM: ~97% of the step's FLOPs): HIP events around every GEMM launch
 of the last --gemm-sample-steps timed steps (events on all ~270 launches of every
